@@ -1,0 +1,508 @@
+// PyTorch custom-op layer for the MI355X DFT kernels (namespace `amd_dft`).
+//
+// Reference parity: the TensorRT plugins `Rfft` / `Irfft` version "1"
+// (/root/reference/src/dft_plugins/dft_plugins.cpp:385, :475, :43) with attributes
+// normalized/onesided/signal_ndim (:500-503) and their shape rules (:361-382, :415-436).
+// Here they are `torch.ops.amd_dft.Rfft` / `Irfft`, registered by static initialisers on
+// dlopen exactly like the reference's PluginRegistrar (:573-576).  Attribute violations
+// raise (the reference only asserts: SURVEY Q2).
+//
+// General ops (the native building blocks):
+//   r2c(x, dim, scale, keep, out_dtype)           real -> half spectrum, trailing re/im dim
+//   c2r(x, dim, out_size, scale, keep, out_dtype) half spectrum -> real
+//   c2c(x, dim, inverse, scale, out_dtype)
+// with optional mode pruning (`keep` = (lo, hi) per transformed dim) used by the FNO/AFNO
+// spectral layers.
+
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPGraphsC10Utils.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <unordered_map>
+
+#include "../fft/fft_plan.h"
+
+namespace amd_dft {
+namespace {
+
+// ------------------------------------------------------------------ plan cache
+struct DevPlan {
+  Plan1D plan;
+  at::Tensor tw;  // device float32 [2*tw_count]
+};
+
+class PlanCache {
+ public:
+  std::shared_ptr<DevPlan> get(int64_t L, const at::Device& dev) {
+    const uint64_t key = (static_cast<uint64_t>(dev.index() + 1) << 40) | static_cast<uint64_t>(L);
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = map_.find(key);
+    if (it != map_.end()) {
+      lru_.splice(lru_.begin(), lru_, it->second.second);
+      return it->second.first;
+    }
+    TORCH_CHECK(c10::hip::currentStreamCaptureStatusMayInitCtx() == c10::hip::CaptureStatus::None,
+                "amd_dft: FFT plan for length ", L,
+                " was not created before graph capture; run the model once (warm-up) before capturing");
+    auto dp = std::make_shared<DevPlan>();
+    dp->plan = make_plan_1d(static_cast<int32_t>(L));
+    auto host = at::from_blob(dp->plan.tw_host.data(), {static_cast<int64_t>(dp->plan.tw_host.size())},
+                              at::TensorOptions().dtype(at::kFloat));
+    dp->tw = host.to(dev);
+    lru_.push_front(key);
+    map_[key] = {dp, lru_.begin()};
+    while (map_.size() > capacity()) {
+      map_.erase(lru_.back());
+      lru_.pop_back();
+    }
+    return dp;
+  }
+  void clear() {
+    std::lock_guard<std::mutex> g(mu_);
+    map_.clear();
+    lru_.clear();
+  }
+  size_t size() {
+    std::lock_guard<std::mutex> g(mu_);
+    return map_.size();
+  }
+
+ private:
+  static size_t capacity() {
+    static size_t cap = [] {
+      const char* e = std::getenv("MI_DFT_PLAN_CACHE_SIZE");
+      long v = e ? std::atol(e) : 256;
+      return static_cast<size_t>(v > 0 ? v : 256);
+    }();
+    return cap;
+  }
+  std::mutex mu_;
+  std::list<uint64_t> lru_;
+  std::unordered_map<uint64_t, std::pair<std::shared_ptr<DevPlan>, std::list<uint64_t>::iterator>> map_;
+};
+
+PlanCache& plan_cache() {
+  static PlanCache c;
+  return c;
+}
+
+// ------------------------------------------------------------------ helpers
+DType to_dtype(at::ScalarType t) {
+  if (t == at::kFloat) return DType::F32;
+  if (t == at::kBFloat16) return DType::BF16;
+  TORCH_CHECK(false, "amd_dft: unsupported dtype ", t, " (float32 and bfloat16 are supported)");
+}
+
+struct DimSpec {
+  int axis;
+  int64_t n;       // full transform length
+  int64_t lo, hi;  // kept / stored ranges
+};
+
+std::vector<int> norm_dims(at::IntArrayRef dim, int64_t ndim) {
+  std::vector<int> d;
+  for (int64_t v : dim) {
+    const int64_t w = v < 0 ? v + ndim : v;
+    TORCH_CHECK(w >= 0 && w < ndim, "amd_dft: dim ", v, " out of range for a tensor of rank ", ndim);
+    TORCH_CHECK(std::find(d.begin(), d.end(), static_cast<int>(w)) == d.end(), "amd_dft: repeated dim ", v);
+    d.push_back(static_cast<int>(w));
+  }
+  TORCH_CHECK(!d.empty(), "amd_dft: at least one dim must be transformed");
+  return d;
+}
+
+// keep: empty or 2 entries per dim (in the order given); -1 entries mean "full".
+std::vector<std::pair<int64_t, int64_t>> parse_keep(at::IntArrayRef keep, size_t nd) {
+  std::vector<std::pair<int64_t, int64_t>> k(nd, {-1, -1});
+  if (keep.empty()) return k;
+  TORCH_CHECK(keep.size() == 2 * nd, "amd_dft: keep must have 2 entries (lo, hi) per transformed dim");
+  for (size_t i = 0; i < nd; ++i) k[i] = {keep[2 * i], keep[2 * i + 1]};
+  return k;
+}
+
+at::Tensor alloc_complex(const std::vector<int64_t>& logical, const at::TensorOptions& o, at::ScalarType dt) {
+  std::vector<int64_t> s = logical;
+  s.push_back(2);
+  return at::empty(s, o.dtype(dt));
+}
+
+void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
+              const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
+              int out_hi, float scale, bool inverse) {
+  auto dp = plan_cache().get(L, in.device());
+  PassDesc d;
+  d.kind = kind;
+  apply_plan(d, dp->plan);
+  d.tw = dp->tw.data_ptr();
+  set_axis_geometry(d, in_shape, out_shape, axis, kind != Kind::R2C, kind != Kind::C2R);
+  d.in_lo = in_lo;
+  d.in_hi = in_hi;
+  d.out_lo = out_lo;
+  d.out_hi = out_hi;
+  d.scale = scale;
+  d.inverse = inverse ? 1 : 0;
+  d.tin = to_dtype(in.scalar_type());
+  d.tout = to_dtype(out.scalar_type());
+  d.in = in.data_ptr();
+  d.out = out.data_ptr();
+  TORCH_CHECK(choose_tiling(d), "amd_dft: transform length ", L, " exceeds the LDS-resident limit (",
+              max_lds_length(), ")");
+  finalize_vec_flags(d, static_cast<int>(in.element_size()), static_cast<int>(out.element_size()));
+  launch_fft_pass(d, c10::hip::getCurrentHIPStream(in.device().index()).stream());
+}
+
+// ------------------------------------------------------------------ shape logic (shared)
+struct R2CShape {
+  std::vector<DimSpec> specs;  // sorted by axis ascending
+  std::vector<int64_t> out_logical;
+};
+
+R2CShape r2c_shape(at::IntArrayRef sizes, at::IntArrayRef dim, at::IntArrayRef keep) {
+  const int64_t nd = static_cast<int64_t>(sizes.size());
+  auto dims = norm_dims(dim, nd);
+  auto kp = parse_keep(keep, dims.size());
+  R2CShape r;
+  for (size_t i = 0; i < dims.size(); ++i) r.specs.push_back({dims[i], sizes[dims[i]], kp[i].first, kp[i].second});
+  std::sort(r.specs.begin(), r.specs.end(), [](const DimSpec& a, const DimSpec& b) { return a.axis < b.axis; });
+  r.out_logical.assign(sizes.begin(), sizes.end());
+  for (size_t i = 0; i < r.specs.size(); ++i) {
+    DimSpec& s = r.specs[i];
+    const bool last = i + 1 == r.specs.size();
+    TORCH_CHECK(s.n >= 1, "amd_dft: transform length must be >= 1");
+    const int64_t full = last ? s.n / 2 + 1 : s.n;
+    if (s.lo < 0) { s.lo = full; s.hi = 0; }
+    if (s.hi < 0) s.hi = 0;
+    TORCH_CHECK(!last || s.hi == 0, "amd_dft: the innermost (half-spectrum) dim keeps only low modes (hi == 0)");
+    TORCH_CHECK(s.lo + s.hi <= full && s.lo >= 0, "amd_dft: kept modes (", s.lo, ", ", s.hi, ") exceed ", full);
+    r.out_logical[s.axis] = s.lo + s.hi;
+  }
+  return r;
+}
+
+struct C2RShape {
+  std::vector<DimSpec> specs;
+  std::vector<int64_t> in_logical, out_real;
+};
+
+C2RShape c2r_shape(at::IntArrayRef sizes_with_2, at::IntArrayRef dim, at::IntArrayRef out_size, at::IntArrayRef keep) {
+  TORCH_CHECK(sizes_with_2.size() >= 2 && sizes_with_2.back() == 2,
+              "amd_dft: complex input must be a real tensor with a trailing dim of size 2");
+  std::vector<int64_t> logical(sizes_with_2.begin(), sizes_with_2.end() - 1);
+  const int64_t nd = static_cast<int64_t>(logical.size());
+  auto dims = norm_dims(dim, nd);
+  TORCH_CHECK(out_size.size() == dims.size(), "amd_dft: out_size needs one entry per transformed dim");
+  auto kp = parse_keep(keep, dims.size());
+  C2RShape r;
+  r.in_logical = logical;
+  for (size_t i = 0; i < dims.size(); ++i) r.specs.push_back({dims[i], out_size[i], kp[i].first, kp[i].second});
+  std::sort(r.specs.begin(), r.specs.end(), [](const DimSpec& a, const DimSpec& b) { return a.axis < b.axis; });
+  r.out_real = logical;
+  for (size_t i = 0; i < r.specs.size(); ++i) {
+    DimSpec& s = r.specs[i];
+    const bool last = i + 1 == r.specs.size();
+    const int64_t stored = logical[s.axis];
+    TORCH_CHECK(s.n >= 1, "amd_dft: output length must be >= 1");
+    if (s.lo < 0) { s.lo = stored; s.hi = 0; }
+    if (s.hi < 0) s.hi = 0;
+    TORCH_CHECK(s.lo + s.hi == stored, "amd_dft: keep (", s.lo, ", ", s.hi, ") does not match stored size ", stored,
+                " along dim ", s.axis);
+    const int64_t full = last ? s.n / 2 + 1 : s.n;
+    TORCH_CHECK(!last || s.hi == 0, "amd_dft: the innermost (half-spectrum) dim stores only low modes (hi == 0)");
+    // Inputs longer than the Hermitian half are truncated (torch.fft.irfft semantics).
+    if (s.lo + s.hi > full) {
+      TORCH_CHECK(s.hi == 0, "amd_dft: stored modes exceed the transform length along dim ", s.axis);
+    }
+    r.out_real[s.axis] = s.n;
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------ CUDA (HIP) impls
+at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
+                    std::optional<at::ScalarType> out_dtype) {
+  const c10::DeviceGuard guard(x_.device());
+  at::Tensor x = x_.contiguous();
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  R2CShape sh = r2c_shape(x.sizes(), dim, keep);
+  auto opts = x.options();
+  if (x.numel() == 0) return alloc_complex(sh.out_logical, opts, odt).zero_();
+  std::vector<int64_t> cur(x.sizes().begin(), x.sizes().end());
+  at::Tensor cur_t = x;
+  const int ns = static_cast<int>(sh.specs.size());
+  // innermost first: R2C on the last transformed axis, then C2C outwards.
+  for (int i = ns - 1; i >= 0; --i) {
+    const DimSpec& s = sh.specs[i];
+    std::vector<int64_t> nxt = cur;
+    nxt[s.axis] = s.lo + s.hi;
+    const bool final_pass = i == 0;
+    at::Tensor out = alloc_complex(nxt, opts, final_pass ? odt : at::kFloat);
+    const float sc = final_pass ? static_cast<float>(scale) : 1.0f;
+    if (i == ns - 1) {
+      run_pass(Kind::R2C, cur_t, out, cur, nxt, s.axis, s.n, static_cast<int>(s.n), 0, static_cast<int>(s.lo), 0,
+               sc, false);
+    } else {
+      run_pass(Kind::C2C, cur_t, out, cur, nxt, s.axis, s.n, static_cast<int>(s.n), 0, static_cast<int>(s.lo),
+               static_cast<int>(s.hi), sc, false);
+    }
+    cur = nxt;
+    cur_t = out;
+  }
+  return cur_t;
+}
+
+at::Tensor c2r_cuda(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                    at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
+  const c10::DeviceGuard guard(x_.device());
+  at::Tensor x = x_.contiguous();
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  C2RShape sh = c2r_shape(x.sizes(), dim, out_size, keep);
+  auto opts = x.options();
+  if (x.numel() == 0) return at::zeros(sh.out_real, opts.dtype(odt));
+  std::vector<int64_t> cur = sh.in_logical;
+  at::Tensor cur_t = x;
+  const int ns = static_cast<int>(sh.specs.size());
+  // C2C (inverse) on the outer axes first (outermost first), C2R on the innermost last.
+  for (int i = 0; i < ns; ++i) {
+    const DimSpec& s = sh.specs[i];
+    std::vector<int64_t> nxt = cur;
+    nxt[s.axis] = s.n;
+    const bool final_pass = i == ns - 1;
+    const float sc = final_pass ? static_cast<float>(scale) : 1.0f;
+    if (final_pass) {
+      at::Tensor out = at::empty(nxt, opts.dtype(odt));
+      const int64_t half = s.n / 2 + 1;
+      const int in_lo = static_cast<int>(std::min<int64_t>(s.lo, half));
+      // When more modes are stored than the half spectrum, the extra ones are ignored; the
+      // stored stride along the axis stays the stored size (geometry from `cur`).
+      run_pass(Kind::C2R, cur_t, out, cur, nxt, s.axis, s.n, in_lo, 0, static_cast<int>(s.n), 0, sc, true);
+      cur_t = out;
+    } else {
+      at::Tensor out = alloc_complex(nxt, opts, at::kFloat);
+      run_pass(Kind::C2C, cur_t, out, cur, nxt, s.axis, s.n, static_cast<int>(s.lo), static_cast<int>(s.hi),
+               static_cast<int>(s.n), 0, sc, true);
+      cur_t = out;
+    }
+    cur = nxt;
+  }
+  return cur_t;
+}
+
+at::Tensor c2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, bool inverse, double scale,
+                    std::optional<at::ScalarType> out_dtype) {
+  const c10::DeviceGuard guard(x_.device());
+  at::Tensor x = x_.contiguous();
+  TORCH_CHECK(x.dim() >= 2 && x.size(-1) == 2, "amd_dft: complex input must have a trailing dim of size 2");
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  std::vector<int64_t> cur(x.sizes().begin(), x.sizes().end() - 1);
+  auto dims = norm_dims(dim, static_cast<int64_t>(cur.size()));
+  std::sort(dims.begin(), dims.end());
+  if (x.numel() == 0) return at::empty_like(x, x.options().dtype(odt));
+  at::Tensor cur_t = x;
+  for (size_t i = 0; i < dims.size(); ++i) {
+    const int ax = dims[dims.size() - 1 - i];
+    const bool final_pass = i + 1 == dims.size();
+    at::Tensor out = alloc_complex(cur, x.options(), final_pass ? odt : at::kFloat);
+    const int64_t n = cur[ax];
+    run_pass(Kind::C2C, cur_t, out, cur, cur, ax, n, static_cast<int>(n), 0, static_cast<int>(n), 0,
+             final_pass ? static_cast<float>(scale) : 1.0f, inverse);
+    cur_t = out;
+  }
+  return cur_t;
+}
+
+// ------------------------------------------------------------------ CPU impls (torch.fft)
+at::Tensor select_modes(at::Tensor y, int axis, int64_t lo, int64_t hi) {
+  const int64_t n = y.size(axis);
+  if (lo + hi == n && hi == 0) return y;
+  if (hi == 0) return y.narrow(axis, 0, lo);
+  return at::cat({y.narrow(axis, 0, lo), y.narrow(axis, n - hi, hi)}, axis);
+}
+
+at::Tensor r2c_cpu(const at::Tensor& x, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
+                   std::optional<at::ScalarType> out_dtype) {
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  R2CShape sh = r2c_shape(x.sizes(), dim, keep);
+  std::vector<int64_t> dims;
+  for (auto& s : sh.specs) dims.push_back(s.axis);
+  at::Tensor y = at::fft_rfftn(x.to(at::kFloat), std::nullopt, dims, "backward");
+  for (auto& s : sh.specs) y = select_modes(y, s.axis, s.lo, s.hi);
+  at::Tensor r = at::view_as_real(y.contiguous()).mul(scale);
+  return r.to(odt).contiguous();
+}
+
+at::Tensor c2r_cpu(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                   at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  C2RShape sh = c2r_shape(x.sizes(), dim, out_size, keep);
+  at::Tensor X = at::view_as_complex(x.to(at::kFloat).contiguous());
+  const size_t ns = sh.specs.size();
+  std::vector<int64_t> dims, sizes;
+  for (size_t i = 0; i < ns; ++i) {
+    const DimSpec& s = sh.specs[i];
+    dims.push_back(s.axis);
+    sizes.push_back(s.n);
+    const bool last = i + 1 == ns;
+    const int64_t full = last ? s.n / 2 + 1 : s.n;
+    if (s.lo + s.hi > full) {
+      X = X.narrow(s.axis, 0, full);
+      continue;
+    }
+    if (s.lo + s.hi == full) continue;
+    std::vector<int64_t> zs(X.sizes().begin(), X.sizes().end());
+    zs[s.axis] = full;
+    at::Tensor Z = at::zeros(zs, X.options());
+    Z.narrow(s.axis, 0, s.lo).copy_(X.narrow(s.axis, 0, s.lo));
+    if (s.hi > 0) Z.narrow(s.axis, full - s.hi, s.hi).copy_(X.narrow(s.axis, s.lo, s.hi));
+    X = Z;
+  }
+  at::Tensor y = at::fft_irfftn(X, sizes, dims, "forward").mul(scale);
+  return y.to(odt).contiguous();
+}
+
+at::Tensor c2c_cpu(const at::Tensor& x, at::IntArrayRef dim, bool inverse, double scale,
+                   std::optional<at::ScalarType> out_dtype) {
+  TORCH_CHECK(x.dim() >= 2 && x.size(-1) == 2, "amd_dft: complex input must have a trailing dim of size 2");
+  to_dtype(x.scalar_type());
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(odt);
+  auto dims = norm_dims(dim, x.dim() - 1);
+  std::vector<int64_t> d64(dims.begin(), dims.end());
+  at::Tensor X = at::view_as_complex(x.to(at::kFloat).contiguous());
+  at::Tensor y = inverse ? at::fft_ifftn(X, std::nullopt, d64, "forward") : at::fft_fftn(X, std::nullopt, d64, "backward");
+  return at::view_as_real(y.contiguous()).mul(scale).to(odt).contiguous();
+}
+
+// ------------------------------------------------------------------ Meta impls
+at::Tensor r2c_meta(const at::Tensor& x, at::IntArrayRef dim, double, at::IntArrayRef keep,
+                    std::optional<at::ScalarType> out_dtype) {
+  R2CShape sh = r2c_shape(x.sizes(), dim, keep);
+  return alloc_complex(sh.out_logical, x.options(), out_dtype.value_or(x.scalar_type()));
+}
+at::Tensor c2r_meta(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double,
+                    at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
+  C2RShape sh = c2r_shape(x.sizes(), dim, out_size, keep);
+  return at::empty(sh.out_real, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+}
+at::Tensor c2c_meta(const at::Tensor& x, at::IntArrayRef, bool, double, std::optional<at::ScalarType> out_dtype) {
+  return at::empty_like(x, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+}
+
+// ------------------------------------------------------------------ ONNX-contrib parity ops
+void check_contrib_attrs(int64_t normalized, int64_t onesided, int64_t signal_ndim) {
+  // dft_plugins.cpp:54-57 ("mimics limitations of ONNX Contrib ops").
+  TORCH_CHECK(normalized == 0, "amd_dft.Rfft/Irfft: only normalized=0 is supported (got ", normalized, ")");
+  TORCH_CHECK(onesided == 1, "amd_dft.Rfft/Irfft: only onesided=1 is supported (got ", onesided, ")");
+  TORCH_CHECK(signal_ndim >= 1 && signal_ndim <= 3, "amd_dft.Rfft/Irfft: signal_ndim must be in [1, 3] (got ",
+              signal_ndim, ")");
+}
+
+at::Tensor contrib_rfft(const at::Tensor& x, int64_t normalized, int64_t onesided, int64_t signal_ndim) {
+  check_contrib_attrs(normalized, onesided, signal_ndim);
+  TORCH_CHECK(x.dim() >= signal_ndim, "amd_dft.Rfft: input rank ", x.dim(), " < signal_ndim ", signal_ndim);
+  TORCH_CHECK(x.dim() < 8, "amd_dft.Rfft: input rank must be < 8 (output adds a dim; dft_plugins.cpp:369)");
+  std::vector<int64_t> dims;
+  for (int64_t i = signal_ndim; i >= 1; --i) dims.push_back(x.dim() - i);
+  static auto op = c10::Dispatcher::singleton().findSchemaOrThrow("amd_dft::r2c", "").typed<decltype(r2c_cpu)>();
+  return op.call(x, dims, 1.0, {}, std::nullopt);
+}
+
+at::Tensor contrib_irfft(const at::Tensor& x, int64_t normalized, int64_t onesided, int64_t signal_ndim) {
+  check_contrib_attrs(normalized, onesided, signal_ndim);
+  TORCH_CHECK(x.dim() >= signal_ndim + 1 && x.size(-1) == 2,
+              "amd_dft.Irfft: input must be [..., signal dims, 2] with rank >= signal_ndim + 1");
+  const int64_t nd = x.dim() - 1;
+  std::vector<int64_t> dims, sizes;
+  int64_t total = 1;
+  for (int64_t i = signal_ndim; i >= 1; --i) {
+    const int64_t ax = nd - i;
+    dims.push_back(ax);
+    const int64_t n = i == 1 ? 2 * (x.size(ax) - 1) : x.size(ax);  // dft_plugins.cpp:428-434
+    TORCH_CHECK(n >= 1, "amd_dft.Irfft: last signal dim must be >= 2");
+    sizes.push_back(n);
+    total *= n;
+  }
+  static auto op = c10::Dispatcher::singleton().findSchemaOrThrow("amd_dft::c2r", "").typed<decltype(c2r_cpu)>();
+  // "backward" normalisation: 1/prod(n) on the inverse (dft_plugins.cpp:457-468), in double.
+  return op.call(x, dims, sizes, 1.0 / static_cast<double>(total), {}, std::nullopt);
+}
+
+// ------------------------------------------------------------------ introspection
+std::string plan_info(int64_t n) {
+  TORCH_CHECK(n >= 1 && n < (1 << 30), "amd_dft.plan_info: bad length");
+  Plan1D p = make_plan_1d(static_cast<int32_t>(n));
+  std::ostringstream os;
+  os << describe(p) << " lds_limit=" << max_lds_length();
+  return os.str();
+}
+
+std::string plugin_registry() {
+  // Mirrors the two TensorRT plugin creators (dft_plugins.cpp:497-570): name, version,
+  // namespace, field list in the creator's order.
+  return R"([{"name": "Rfft", "version": "1", "namespace": "", "domain": "com.microsoft", "op": "amd_dft::Rfft",)"
+         R"( "fields": [{"name": "normalized", "type": "INT32", "default": 0},)"
+         R"( {"name": "onesided", "type": "INT32", "default": 1},)"
+         R"( {"name": "signal_ndim", "type": "INT32", "default": 1}]},)"
+         R"( {"name": "Irfft", "version": "1", "namespace": "", "domain": "com.microsoft", "op": "amd_dft::Irfft",)"
+         R"( "fields": [{"name": "normalized", "type": "INT32", "default": 0},)"
+         R"( {"name": "onesided", "type": "INT32", "default": 1},)"
+         R"( {"name": "signal_ndim", "type": "INT32", "default": 1}]}])";
+}
+
+int64_t plan_cache_size() { return static_cast<int64_t>(plan_cache().size()); }
+void plan_cache_clear() { plan_cache().clear(); }
+
+}  // namespace
+}  // namespace amd_dft
+
+TORCH_LIBRARY(amd_dft, m) {
+  m.def("r2c(Tensor x, int[] dim, float scale=1.0, int[] keep=[], ScalarType? out_dtype=None) -> Tensor");
+  m.def("c2r(Tensor x, int[] dim, int[] out_size, float scale=1.0, int[] keep=[], ScalarType? out_dtype=None) -> Tensor");
+  m.def("c2c(Tensor x, int[] dim, bool inverse=False, float scale=1.0, ScalarType? out_dtype=None) -> Tensor");
+  m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
+  m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
+  m.def("plan_info(int n) -> str", &amd_dft::plan_info);
+  m.def("plugin_registry() -> str", &amd_dft::plugin_registry);
+  m.def("plan_cache_size() -> int", &amd_dft::plan_cache_size);
+  m.def("plan_cache_clear() -> ()", &amd_dft::plan_cache_clear);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
+  m.impl("r2c", &amd_dft::r2c_cuda);
+  m.impl("c2r", &amd_dft::c2r_cuda);
+  m.impl("c2c", &amd_dft::c2c_cuda);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
+  m.impl("r2c", &amd_dft::r2c_cpu);
+  m.impl("c2r", &amd_dft::c2r_cpu);
+  m.impl("c2c", &amd_dft::c2c_cpu);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
+  m.impl("r2c", &amd_dft::r2c_meta);
+  m.impl("c2r", &amd_dft::c2r_meta);
+  m.impl("c2c", &amd_dft::c2c_meta);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {
+  m.impl("Rfft", &amd_dft::contrib_rfft);
+  m.impl("Irfft", &amd_dft::contrib_irfft);
+}

@@ -1,0 +1,133 @@
+"""In-tree native build of ``_C.so`` for gfx950 (MI355X).
+
+The reference builds ``libtrt_dft_plugins.so`` with CMake driven by setup.py
+(/root/reference/CMakeLists.txt:22-28, /root/reference/setup.py:30-48).  Here the HIP
+kernels (no torch headers, fast) and the torch op layer (torch headers, slow) are compiled
+by ``hipcc --offload-arch=gfx950`` into objects under ``build/`` and linked into a single
+``tensorrt_dft_plugins_amd/_C.so`` that sits next to the package (where ``load_plugins()``
+looks, like the reference's CMAKE_LIBRARY_OUTPUT_DIRECTORY).  No hipify step, no CUDA
+sources, no rocFFT/hipFFT/hipBLAS link.
+
+Usage: ``python -m tensorrt_dft_plugins_amd._build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+PKG = os.path.join(ROOT, "tensorrt_dft_plugins_amd")
+LIB = os.path.join(PKG, "_C.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+
+def _hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    p = os.path.join(rocm, "bin", "hipcc")
+    return p if os.path.exists(p) else (shutil.which("hipcc") or "hipcc")
+
+
+def _torch_paths():
+    import torch
+
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    return inc, os.path.join(tdir, "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def sources():
+    """(path, needs_torch) for every native translation unit."""
+    out = []
+    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True)):
+        out.append((p, False))
+    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)):
+        out.append((p, "/ops/" in p.replace(os.sep, "/")))
+    return out
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max([os.path.getmtime(h) for h in hs] + [0.0])
+
+
+def _obj_path(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
+    obj = _obj_path(src)
+    cmd = [_hipcc(), "-c", "-fPIC", "-std=c++17", "-O3", "-Wall", "-Wno-unused-function",
+           "-Wno-unused-variable", "-Wno-sign-compare", "-I" + CSRC,
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-o", obj]
+    if src.endswith(".hip"):
+        cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+    else:
+        # host-only C++ that includes HIP runtime headers (torch's c10/hip)
+        rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+        cmd += ["-x", "c++", "-I" + os.path.join(rocm, "include"), "-D__HIP_PLATFORM_AMD__=1"]
+    if needs_torch:
+        cmd += ["-O2", "-DUSE_ROCM=1", "-Wno-deprecated-declarations", "-Wno-unknown-pragmas"]
+        cmd += ["-I" + p for p in tinc]
+        cmd += ["-I" + sysconfig.get_paths()["include"]]
+    cmd.append(src)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    """Compile every HIP/C++ source for gfx950 and link ``_C.so``; returns its path."""
+    os.makedirs(BUILD, exist_ok=True)
+    tinc, tlib, abi = _torch_paths()
+    hdr = _headers_mtime()
+    srcs = sources()
+    todo = []
+    for src, nt in srcs:
+        obj = _obj_path(src)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
+            todo.append((src, nt))
+    jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    if todo:
+        if verbose:
+            print(f"[amd_dft build] compiling {len(todo)} file(s) for {ARCH} with {jobs} jobs", flush=True)
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = {ex.submit(_compile, s, nt, tinc, abi): s for s, nt in todo}
+            for f in cf.as_completed(futs):
+                f.result()
+                if verbose:
+                    print("  built", os.path.relpath(futs[f], ROOT), flush=True)
+    objs = [_obj_path(s) for s, _ in srcs]
+    if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        tmp = LIB + ".tmp"
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
+            "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+            "-Wl,-rpath," + tlib]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print("[amd_dft build] linked", os.path.relpath(LIB, ROOT), flush=True)
+    return LIB
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
