@@ -1,0 +1,100 @@
+// Host side of the compile-time specialised Stockham kernels: configuration table and
+// selection (kernels: fft_fixed_impl.h, instantiated in fft_fixed_{c2c,r2c,c2r}.hip).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "fft_fixed_impl.h"
+
+namespace amd_dft {
+namespace fixed_detail {
+namespace {
+
+#define AMD_DFT_CFG(L_, COLS_, TP_, T_, ...) FixedCfg{L_, COLS_, TP_, T_, FL<__VA_ARGS__>::N, {__VA_ARGS__}},
+
+const std::vector<FixedCfg>& table() {
+  static const std::vector<FixedCfg> v = {AMD_DFT_FIXED_CONFIGS(AMD_DFT_CFG)};
+  return v;
+}
+
+}  // namespace
+}  // namespace fixed_detail
+
+using namespace fixed_detail;
+
+const std::vector<FixedCfg>& fixed_configs() { return table(); }
+
+std::vector<int32_t> fixed_radices(int32_t L) {
+  for (const auto& c : fixed_configs())
+    if (c.L == L) return std::vector<int32_t>(c.radix, c.radix + c.npass);
+  return {};
+}
+
+bool launch_fft_fixed(const PassDesc& d, void* stream) {
+  // MI_DFT_FIXED=0 disables the specialised kernels (A/B tests); MI_DFT_FIXED_CFG="TP,T"
+  // forces one configuration.
+  const char* fe = std::getenv("MI_DFT_FIXED");
+  if (fe && std::atoi(fe) == 0) return false;
+  if (d.tw_count == 0 && d.npass > 1) return false;  // ablation builds
+  const bool cols = d.Si_in < d.Sn_in || d.Si_out < d.Sn_out;
+  const bool paired = d.kind != Kind::C2C;
+  const int64_t nsig = paired ? (d.I + 1) / 2 : d.I;
+  std::vector<int32_t> rad(d.radix, d.radix + d.npass);
+  int force_tp = 0, force_t = 0;
+  if (const char* fc = std::getenv("MI_DFT_FIXED_CFG")) std::sscanf(fc, "%d,%d", &force_tp, &force_t);
+  const auto& cfgs = fixed_configs();
+  if (force_tp) {  // the override only applies where such a configuration exists
+    bool any = false;
+    for (const auto& c : cfgs) any |= c.L == d.L && c.cols == cols && c.TP == force_tp && c.T == force_t;
+    if (!any) force_tp = force_t = 0;
+  }
+  int best = -1;
+  double best_score = -1e300;
+  for (int i = 0; i < static_cast<int>(cfgs.size()); ++i) {
+    const FixedCfg& c = cfgs[i];
+    if (c.L != d.L || c.cols != cols) continue;
+    if (std::vector<int32_t>(c.radix, c.radix + c.npass) != rad) continue;
+    if (force_tp && (c.TP != force_tp || c.T != force_t)) continue;
+    const int64_t wgs = d.O * ((nsig + c.T - 1) / c.T);
+    const int64_t waves = wgs * ((c.TP * c.T + 63) / 64);
+    // enough waves to put >= 2 on every SIMD (1024 SIMDs), then the widest tile
+    // (coalescing, fewer twiddle re-reads); otherwise the most waves.
+    const double score = waves >= 2048 ? 1e12 + c.T * 1e6 + c.TP : static_cast<double>(waves);
+    if (score > best_score) {
+      best_score = score;
+      best = i;
+    }
+  }
+  if (best < 0) return false;
+  const FixedCfg& cfg = cfgs[best];
+  FixedArgs a;
+  a.in = d.in;
+  a.out = d.out;
+  a.tw = static_cast<const float2*>(d.tw);
+  // per-element offsets must fit in int32 (else the generic 64-bit kernel runs)
+  const int64_t lim = 0x7fffffffLL;
+  const int64_t nin = d.kind == Kind::C2C ? d.in_lo + d.in_hi : (d.kind == Kind::C2R ? d.in_lo : d.L);
+  const int64_t nout = d.kind == Kind::C2C ? d.out_lo + d.out_hi : (d.kind == Kind::R2C ? d.out_lo : d.L);
+  if ((d.I + 1) * d.Si_in + nin * d.Sn_in + 4 >= lim || (d.I + 1) * d.Si_out + nout * d.Sn_out + 4 >= lim) return false;
+  a.So_in = d.So_in; a.So_out = d.So_out; a.I = static_cast<int32_t>(d.I);
+  a.Si_in = static_cast<int32_t>(d.Si_in); a.Si_out = static_cast<int32_t>(d.Si_out);
+  a.Sn_in = static_cast<int32_t>(d.Sn_in); a.Sn_out = static_cast<int32_t>(d.Sn_out);
+  a.in_lo = d.in_lo; a.in_hi = d.in_hi; a.out_lo = d.out_lo; a.out_hi = d.out_hi;
+  a.tiles_per_outer = static_cast<int32_t>((nsig + cfg.T - 1) / cfg.T);
+  a.scale = d.scale;
+  a.inverse = d.inverse; a.vec_in = d.vec_in; a.vec_out = d.vec_out;
+  a.bf16_in = d.tin == DType::BF16; a.bf16_out = d.tout == DType::BF16;
+  const int64_t nblocks = d.O * a.tiles_per_outer;
+  if (nblocks <= 0) return true;
+  if (nblocks > 0x7fffffffLL) throw std::runtime_error("amd_dft: FFT grid too large");
+  LaunchFn fn = d.kind == Kind::C2C ? c2c_launcher(best) : (d.kind == Kind::R2C ? r2c_launcher(best) : c2r_launcher(best));
+  fn(a, dim3(static_cast<uint32_t>(nblocks)), static_cast<hipStream_t>(stream));
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) throw std::runtime_error(std::string("amd_dft: fixed FFT launch failed: ") + hipGetErrorString(err));
+  return true;
+}
+
+}  // namespace amd_dft

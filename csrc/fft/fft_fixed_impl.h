@@ -1,0 +1,367 @@
+// Kernel templates of the compile-time specialised Stockham FFT (see fft_fixed.h).
+// Included by fft_fixed_k{0,1,2}.hip (one translation unit per transform kind, compiled in
+// parallel) -- do not include elsewhere.
+//
+// Structure of one workgroup (T FFTs of length L, TP threads each):
+//   pass 0      : global -> registers (coalesced: lane = butterfly index j, or signal t for
+//                 column layouts), radix-R0 DFT, registers -> LDS
+//   pass 1..P-2 : LDS -> registers, twiddle (prefetched one pass ahead from the plan's
+//                 fp64-accurate table), DFT, registers -> LDS
+//   pass P-1    : LDS -> registers, twiddle, DFT, registers -> global (C2C / C2R) -- the
+//                 Stockham last pass writes n = j + r*L/R, i.e. contiguous across lanes;
+//                 R2C goes through LDS once more to pair Z[k] with Z[L-k].
+// Normalisation and the inverse conjugation are fused into the first load / last store.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "fft_fixed.h"
+#include "radix.h"
+
+namespace amd_dft {
+namespace fixed_detail {
+
+struct FixedArgs {
+  const void* in;
+  void* out;
+  const float2* tw;
+  int64_t So_in, So_out;              // outer offsets (64-bit, applied once per block)
+  int32_t I, Si_in, Si_out, Sn_in, Sn_out;  // per-element offsets fit 32 bits (host-checked)
+  int32_t in_lo, in_hi, out_lo, out_hi, tiles_per_outer;
+  float scale;
+  int32_t inverse, vec_in, vec_out, bf16_in, bf16_out;
+};
+
+template <int... Rs>
+struct FL {
+  static constexpr int N = sizeof...(Rs);
+  static constexpr int r[N] = {Rs...};
+  static constexpr int L = (Rs * ... * 1);
+  static constexpr int ns(int p) {
+    int v = 1;
+    for (int i = 0; i < p; ++i) v *= r[i];
+    return v;
+  }
+  // offset of pass p's twiddles in the plan table (passes with ns == 1 store none)
+  static constexpr int goff(int p) {
+    int o = 0;
+    for (int i = 0; i < p; ++i)
+      if (ns(i) > 1) o += (r[i] - 1) * ns(i);
+    return o;
+  }
+};
+
+constexpr __host__ __device__ int lds_pad(int i) { return i + (i >> 4); }
+
+__device__ __forceinline__ float bf_to_f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ uint32_t f_to_bf(float f) {
+  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<__bf16>(f)));
+}
+template <bool BF>
+__device__ __forceinline__ float ld_r(const void* p, int32_t off) {
+  if constexpr (BF) return bf_to_f(static_cast<const uint16_t*>(p)[off]);
+  else return static_cast<const float*>(p)[off];
+}
+template <bool BF>
+__device__ __forceinline__ float2 ld_c(const void* p, int32_t off) {
+  if constexpr (BF) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(p) + off);
+    return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float2*>(static_cast<const float*>(p) + off);
+  }
+}
+template <bool BF>
+__device__ __forceinline__ void st_r(void* p, int32_t off, float v) {
+  if constexpr (BF) static_cast<uint16_t*>(p)[off] = static_cast<uint16_t>(f_to_bf(v));
+  else static_cast<float*>(p)[off] = v;
+}
+template <bool BF>
+__device__ __forceinline__ void st_c(void* p, int32_t off, float2 v) {
+  if constexpr (BF) *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(p) + off) = f_to_bf(v.x) | (f_to_bf(v.y) << 16);
+  else *reinterpret_cast<float2*>(static_cast<float*>(p) + off) = v;
+}
+template <bool BF>
+__device__ __forceinline__ void st_c2(void* p, int32_t off, float2 a, float2 b) {
+  if constexpr (BF) {
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p) + off) =
+        make_uint2(f_to_bf(a.x) | (f_to_bf(a.y) << 16), f_to_bf(b.x) | (f_to_bf(b.y) << 16));
+  } else {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + off) = make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+__device__ __forceinline__ float2 sel(bool ok, float2 v) { return make_float2(ok ? v.x : 0.f, ok ? v.y : 0.f); }
+
+struct Ctx {
+  FixedArgs a;
+  const void* in;   // outer-offset applied
+  void* out;
+  int32_t c;        // complex signal index
+  int32_t cc;       // c clamped into [0, I) (C2C) -- loads are never predicated by branches
+  int32_t i0c, i1c; // paired logical signals 2c, 2c+1 clamped into [0, I) (R2C / C2R)
+  bool ok0, ok1;    // c < I (C2C) / 2c < I, 2c+1 < I (paired)
+  int t, tp;
+  float2* lds;
+};
+
+template <bool COLS, int T, int L>
+__device__ __forceinline__ int lidx(const Ctx& x, int n) {
+  constexpr int LP = lds_pad(L) + 1;
+  if constexpr (COLS) return lds_pad(n * T + x.t);
+  else return x.t * LP + lds_pad(n);
+}
+
+// First-pass element fetch (includes the C2R Hermitian assembly and input pruning).
+// Every load is unconditional from a clamped (valid) address and masked afterwards with a
+// select: a branch around a load makes hipcc wait vmcnt(0) per element.
+template <Kind K, int L, bool BF, bool PR>
+__device__ __forceinline__ float2 gather(const Ctx& x, int n) {
+  const FixedArgs& a = x.a;
+  float2 z;
+  if constexpr (K == Kind::C2C) {
+    if constexpr (PR) {
+      const int s = n < a.in_lo ? n : (n >= L - a.in_hi ? a.in_lo + (n - (L - a.in_hi)) : -1);
+      const bool ok = x.ok0 && s >= 0;
+      z = sel(ok, ld_c<BF>(x.in, x.cc * a.Si_in + (s < 0 ? 0 : s) * a.Sn_in));
+    } else {
+      z = sel(x.ok0, ld_c<BF>(x.in, x.cc * a.Si_in + n * a.Sn_in));
+    }
+    if (a.inverse) z.y = -z.y;
+  } else if constexpr (K == Kind::R2C) {
+    const float va = ld_r<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in);
+    const float vb = ld_r<BF>(x.in, x.i1c * a.Si_in + n * a.Sn_in);
+    z = make_float2(x.ok0 ? va : 0.f, x.ok1 ? vb : 0.f);
+  } else {
+    const bool upper = 2 * n > L;
+    const int kk = upper ? L - n : n;
+    const bool okk = kk < a.in_lo;
+    const int kc = okk ? kk : 0;
+    float2 A = sel(okk && x.ok0, ld_c<BF>(x.in, x.i0c * a.Si_in + kc * a.Sn_in));
+    float2 B = sel(okk && x.ok1, ld_c<BF>(x.in, x.i1c * a.Si_in + kc * a.Sn_in));
+    if (kk == 0 || 2 * kk == L) { A.y = 0.f; B.y = 0.f; }
+    if (upper) { A.y = -A.y; B.y = -B.y; }
+    z = make_float2(A.x - B.y, A.y + B.x);
+    if (a.inverse) z.y = -z.y;
+  }
+  return z;
+}
+
+// Last-pass element store (C2C / C2R), with output pruning and the fused scale.
+template <Kind K, int L, bool BF, bool PR>
+__device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v) {
+  const FixedArgs& a = x.a;
+  if constexpr (K == Kind::C2C) {
+    if (a.inverse) v.y = -v.y;
+    if constexpr (PR) {
+      const int s = n < a.out_lo ? n : (n >= L - a.out_hi ? a.out_lo + (n - (L - a.out_hi)) : -1);
+      if (x.ok0 && s >= 0) st_c<BF>(x.out, x.c * a.Si_out + s * a.Sn_out, make_float2(v.x * a.scale, v.y * a.scale));
+    } else {
+      if (x.ok0) st_c<BF>(x.out, x.c * a.Si_out + n * a.Sn_out, make_float2(v.x * a.scale, v.y * a.scale));
+    }
+  } else {
+    const float va = v.x * a.scale;
+    const float vb = (a.inverse ? -v.y : v.y) * a.scale;
+    const int32_t off = x.i0c * a.Si_out + n * a.Sn_out;
+    if (x.ok0) st_r<BF>(x.out, off, va);
+    if (x.ok1) st_r<BF>(x.out, off + a.Si_out, vb);
+  }
+}
+
+template <class F, int TP, int P>
+struct PassGeom {
+  static constexpr int R = F::r[P];
+  static constexpr int LR = F::L / R;
+  static constexpr int Q = (LR + TP - 1) / TP;
+  static constexpr int Ns = F::ns(P);
+  static constexpr bool EXACT = (LR % TP) == 0;
+  static constexpr int TWR = R > 1 ? R - 1 : 1;
+};
+
+// Twiddles of pass P for this thread's butterflies (global table, L1/L2 resident).
+template <class F, int TP, int P>
+__device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, TP, P>::Q][PassGeom<F, TP, P>::TWR]) {
+  using G = PassGeom<F, TP, P>;
+  if constexpr (G::Ns > 1) {
+#pragma unroll
+    for (int q = 0; q < G::Q; ++q) {
+      const int j = x.tp + q * TP;
+      if (G::EXACT || j < G::LR) {
+        const int k = j % G::Ns;
+#pragma unroll
+        for (int r = 1; r < G::R; ++r) tw[q][r - 1] = x.a.tw[F::goff(P) + (r - 1) * G::Ns + k];
+      }
+    }
+  }
+}
+
+template <Kind K, bool COLS, int TP, int T, class F, int P, bool BFI, bool BFO, bool PR>
+struct Step {
+  using G = PassGeom<F, TP, P>;
+  static constexpr int NP = F::N;
+  static constexpr int L = F::L;
+  static constexpr bool LAST = P == NP - 1;
+
+  __device__ __forceinline__ static void run(const Ctx& x, float2 (&tw)[G::Q][G::TWR]) {
+    constexpr int R = G::R, LR = G::LR, Q = G::Q, Ns = G::Ns;
+    // prefetch next pass' twiddles
+    if constexpr (!LAST) {
+      using GN = PassGeom<F, TP, P + 1>;
+      float2 twn[GN::Q][GN::TWR];
+      load_tw<F, TP, P + 1>(x, twn);
+      body(x, tw);
+      Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR>::run(x, twn);
+    } else {
+      body(x, tw);
+    }
+  }
+
+  __device__ __forceinline__ static void body(const Ctx& x, float2 (&tw)[G::Q][G::TWR]) {
+    constexpr int R = G::R, LR = G::LR, Q = G::Q, Ns = G::Ns;
+    float2 v[Q][R];
+    // ---- gather
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int j = x.tp + q * TP;
+      if (G::EXACT || j < LR) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if constexpr (P == 0) v[q][r] = gather<K, L, BFI, PR>(x, j + r * LR);
+          else v[q][r] = x.lds[lidx<COLS, T, L>(x, j + r * LR)];
+        }
+      }
+    }
+    if constexpr (P > 0) __syncthreads();  // all reads of the shared buffer done
+    // ---- twiddle + butterfly
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int j = x.tp + q * TP;
+      if (G::EXACT || j < LR) {
+        if constexpr (Ns > 1) {
+#pragma unroll
+          for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[q][r - 1]);
+        }
+        Dft<R>::run(v[q]);
+      }
+    }
+    // ---- scatter
+    if constexpr (LAST && K != Kind::R2C) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int j = x.tp + q * TP;
+        if (G::EXACT || j < LR) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) scatter<K, L, BFO, PR>(x, j + r * Ns, v[q][r]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int j = x.tp + q * TP;
+        if (G::EXACT || j < LR) {
+          const int k = j % Ns;
+          const int base = (j - k) * R + k;
+#pragma unroll
+          for (int r = 0; r < R; ++r) x.lds[lidx<COLS, T, L>(x, base + r * Ns)] = v[q][r];
+        }
+      }
+      __syncthreads();
+    }
+  }
+};
+
+template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR>
+__global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
+  constexpr int L = F::L;
+  constexpr int LDSN = COLS ? lds_pad(L * T) + 2 : T * (lds_pad(L) + 1);
+  __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
+  Ctx x;
+  x.a = a;
+  const int tid = threadIdx.x;
+  x.t = COLS ? tid % T : tid / TP;
+  x.tp = COLS ? tid / T : tid % TP;
+  const int32_t o = blockIdx.x / a.tiles_per_outer;
+  const int32_t tile = blockIdx.x - o * a.tiles_per_outer;
+  x.c = tile * T + x.t;
+  if constexpr (K == Kind::C2C) {
+    x.ok0 = x.c < a.I;
+    x.cc = x.ok0 ? x.c : a.I - 1;
+  } else {
+    x.ok0 = 2 * x.c < a.I;
+    x.ok1 = 2 * x.c + 1 < a.I;
+    x.i0c = x.ok0 ? 2 * x.c : a.I - 1;
+    x.i1c = x.ok1 ? 2 * x.c + 1 : a.I - 1;
+  }
+  x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
+  x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  x.lds = lds;
+  using G0 = PassGeom<F, TP, 0>;
+  float2 tw0[G0::Q][G0::TWR];
+  Step<K, COLS, TP, T, F, 0, BFI, BFO, PR>::run(x, tw0);
+  if constexpr (K == Kind::R2C) {
+    // Z (natural order) is in LDS: separate the two packed real signals' half spectra.
+    constexpr int KMAX = L / 2 + 1;
+    constexpr int Q2 = (KMAX + TP - 1) / TP;
+    const float h = 0.5f * a.scale;
+#pragma unroll
+    for (int q = 0; q < Q2; ++q) {
+      const int k = x.tp + q * TP;
+      if (k < a.out_lo) {
+        const float2 zk = lds[lidx<COLS, T, L>(x, k)];
+        const float2 zm = lds[lidx<COLS, T, L>(x, k == 0 ? 0 : L - k)];
+        float2 xa = make_float2((zk.x + zm.x) * h, (zk.y - zm.y) * h);
+        float2 xb = make_float2((zk.y + zm.y) * h, (zm.x - zk.x) * h);
+        if (a.inverse) { xa.y = -xa.y; xb.y = -xb.y; }
+        const int32_t off = x.i0c * a.Si_out + k * a.Sn_out;
+        if (x.ok0) st_c<BFO>(x.out, off, xa);
+        if (x.ok1) st_c<BFO>(x.out, off + a.Si_out, xb);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ config table
+#define AMD_DFT_FIXED_CONFIGS(X)          \
+  X(1440, false, 144, 1, 10, 12, 12)      \
+  X(720, false, 90, 2, 8, 9, 10)          \
+  X(1024, false, 128, 1, 8, 8, 16)        \
+  X(2048, false, 256, 1, 8, 16, 16)       \
+  X(512, false, 64, 2, 8, 8, 8)           \
+  X(256, false, 16, 4, 16, 16)            \
+  X(720, true, 90, 4, 8, 9, 10)           \
+  X(720, true, 90, 2, 8, 9, 10)           \
+  X(720, true, 45, 8, 8, 9, 10)           \
+  X(720, true, 45, 4, 8, 9, 10)           \
+  X(90, true, 10, 16, 9, 10)              \
+  X(180, true, 15, 16, 12, 15)
+
+template <Kind K, bool COLS, int TP, int T, class F, bool PR>
+void launch_dt(const FixedArgs& a, dim3 grid, hipStream_t st) {
+  const dim3 blk(TP * T);
+  if (a.bf16_in) {
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, PR>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, false, PR>), grid, blk, 0, st, a);
+  } else {
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, true, PR>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, PR>), grid, blk, 0, st, a);
+  }
+}
+
+template <Kind K, bool COLS, int TP, int T, class F>
+void launch_one(const FixedArgs& a, dim3 grid, hipStream_t st) {
+  // pruned C2C (FNO/AFNO mode windows) gets its own instantiation; R2C/C2R handle their
+  // (cheap, Hermitian) truncation in the common path.
+  const bool pr = K == Kind::C2C && (a.in_lo + a.in_hi != F::L || a.out_lo + a.out_hi != F::L);
+  if constexpr (K == Kind::C2C) {
+    if (pr) return launch_dt<K, COLS, TP, T, F, true>(a, grid, st);
+  }
+  launch_dt<K, COLS, TP, T, F, false>(a, grid, st);
+}
+
+using LaunchFn = void (*)(const FixedArgs&, dim3, hipStream_t);
+// per-kind launcher tables, index = position in AMD_DFT_FIXED_CONFIGS
+LaunchFn c2c_launcher(int idx);
+LaunchFn r2c_launcher(int idx);
+LaunchFn c2r_launcher(int idx);
+
+}  // namespace fixed_detail
+}  // namespace amd_dft

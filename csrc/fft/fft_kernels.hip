@@ -20,6 +20,7 @@
 #include <string>
 
 #include "fft_desc.h"
+#include "fft_fixed.h"
 #include "radix.h"
 
 namespace amd_dft {
@@ -155,7 +156,20 @@ __global__ void __launch_bounds__(256) fft_pass_kernel(const PassDesc d) {
   TO* __restrict__ out = static_cast<TO*>(d.out) + o * d.So_out;
   const float2* __restrict__ twg = static_cast<const float2*>(d.tw);
 
-  for (int i = tid; i < d.tw_count; i += nth) tw_s[i] = twg[i];
+  // Twiddles: 8 loads in flight per thread before the LDS writes.
+  for (int base = tid; base < d.tw_count; base += 8 * nth) {
+    float2 w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * nth;
+      w[u] = twg[i < d.tw_count ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * nth;
+      if (i < d.tw_count) tw_s[i] = w[u];
+    }
+  }
 
   // signals of this tile: complex index c = tile*T + t; logical signals for R2C/C2R are
   // (2c, 2c+1).
@@ -164,7 +178,19 @@ __global__ void __launch_bounds__(256) fft_pass_kernel(const PassDesc d) {
   const int nload = L << logT;
 
   // ------------------------------------------------------------ load (+ C2R assembly)
-  for (int idx = tid; idx < nload; idx += nth) {
+  // LOADU independent global loads are issued per thread before any LDS write so that the
+  // HBM/L2 latency is paid once per batch, not once per element.
+  constexpr int LOADU = 8;
+  for (int base = tid; base < nload; base += LOADU * nth) {
+  float2 zb[LOADU];
+  int lpos[LOADU];
+#pragma unroll
+  for (int u = 0; u < LOADU; ++u) {
+    // Unconditional loads from clamped addresses + selects: a branch around a load makes
+    // hipcc wait vmcnt(0) per element.
+    const int idx_raw = base + u * nth;
+    const bool in_range = idx_raw < nload;
+    const int idx = in_range ? idx_raw : 0;
     int t, n;
     if (nfast_in) {
       t = static_cast<int>(fdiv(static_cast<uint32_t>(idx), d.L_div));
@@ -173,37 +199,43 @@ __global__ void __launch_bounds__(256) fft_pass_kernel(const PassDesc d) {
       t = idx & (T - 1);
       n = idx >> logT;
     }
-    float2 z = make_float2(0.f, 0.f);
+    float2 z;
     if constexpr (K == Kind::C2C) {
       const int64_t i = c0 + t;
       const int s = stored_index(n, L, d.in_lo, d.in_hi);
-      if (i < d.I && s >= 0) z = IO<TI>::ld2(in + i * d.Si_in + s * d.Sn_in);
+      const bool ok = i < d.I && s >= 0;
+      const int64_t ic = i < d.I ? i : d.I - 1;
+      z = IO<TI>::ld2(in + ic * d.Si_in + (s < 0 ? 0 : s) * d.Sn_in);
+      z = make_float2(ok ? z.x : 0.f, ok ? z.y : 0.f);
       if (d.inverse) z.y = -z.y;
     } else if constexpr (K == Kind::R2C) {
       const int64_t i0 = 2 * (c0 + t);
-      const TI* p = in + i0 * d.Si_in + n * d.Sn_in;
-      if (d.vec_in && i0 + 1 < d.I) {
-        z = IO<TI>::ld2(p);
-      } else {
-        if (i0 < d.I) z.x = IO<TI>::ld(p);
-        if (i0 + 1 < d.I) z.y = IO<TI>::ld(p + d.Si_in);
-      }
+      const bool ok0 = i0 < d.I, ok1 = i0 + 1 < d.I;
+      const float va = IO<TI>::ld(in + (ok0 ? i0 : d.I - 1) * d.Si_in + n * d.Sn_in);
+      const float vb = IO<TI>::ld(in + (ok1 ? i0 + 1 : d.I - 1) * d.Si_in + n * d.Sn_in);
+      z = make_float2(ok0 ? va : 0.f, ok1 ? vb : 0.f);
     } else {  // C2R: z = A + iB with A, B the Hermitian extensions of the two half spectra
       const int64_t i0 = 2 * (c0 + t);
+      const bool ok0 = i0 < d.I, ok1 = i0 + 1 < d.I;
       const bool upper = 2 * n > L;
       const int kk = upper ? L - n : n;
-      float2 A = make_float2(0.f, 0.f), B = A;
-      if (kk < d.in_lo) {
-        const TI* p = in + i0 * d.Si_in + kk * d.Sn_in;
-        if (i0 < d.I) A = IO<TI>::ld2(p);
-        if (i0 + 1 < d.I) B = IO<TI>::ld2(p + d.Si_in);
-      }
+      const bool okk = kk < d.in_lo;
+      const int kc = okk ? kk : 0;
+      float2 A = IO<TI>::ld2(in + (ok0 ? i0 : d.I - 1) * d.Si_in + kc * d.Sn_in);
+      float2 B = IO<TI>::ld2(in + (ok1 ? i0 + 1 : d.I - 1) * d.Si_in + kc * d.Sn_in);
+      A = make_float2(okk && ok0 ? A.x : 0.f, okk && ok0 ? A.y : 0.f);
+      B = make_float2(okk && ok1 ? B.x : 0.f, okk && ok1 ? B.y : 0.f);
       if (kk == 0 || 2 * kk == L) { A.y = 0.f; B.y = 0.f; }
       if (upper) { A.y = -A.y; B.y = -B.y; }
       z = make_float2(A.x - B.y, A.y + B.x);
       if (d.inverse) z.y = -z.y;
     }
-    buf0[lds_ix((n << logT) + t)] = z;
+    zb[u] = z;
+    lpos[u] = in_range ? lds_ix((n << logT) + t) : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < LOADU; ++u)
+    if (lpos[u] >= 0) buf0[lpos[u]] = zb[u];
   }
   __syncthreads();
 
@@ -353,6 +385,7 @@ int64_t pass_lds_bytes(const PassDesc& d) {
 }
 
 void launch_fft_pass(const PassDesc& d, void* stream) {
+  if (launch_fft_fixed(d, stream)) return;
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (d.kind) {
     case Kind::C2C: return launch_k<Kind::C2C>(d, st);

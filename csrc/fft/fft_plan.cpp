@@ -1,7 +1,10 @@
 #include "fft_plan.h"
 
+#include "fft_fixed.h"
+
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <sstream>
 
@@ -80,6 +83,9 @@ bool radix_is_specialised(int r) {
 }
 
 std::vector<int32_t> factorize(int32_t L) {
+  // Lengths with a compile-time specialised kernel use that kernel's radix order.
+  std::vector<int32_t> fx = fixed_radices(L);
+  if (!fx.empty()) return fx;
   std::map<int32_t, Best> memo;
   std::vector<int32_t> f = search(L, memo).f;
   // Large radices first: later passes then write contiguous runs (Ns grows fast).
@@ -208,6 +214,11 @@ bool choose_tiling(PassDesc& d) {
     if (col_like && logT < 3 && next_wgs >= 128) { ++logT; continue; }
     break;
   }
+  // Tuning overrides (experiments only): MI_DFT_LOGT_ROW / MI_DFT_LOGT_COL force log2(T).
+  if (const char* e = std::getenv(col_like ? "MI_DFT_LOGT_COL" : "MI_DFT_LOGT_ROW")) {
+    const int f = std::atoi(e);
+    if (f >= 0 && f <= 6 && lds_of(f) <= kMaxLdsBytes) logT = f;
+  }
   d.logT = logT;
   d.T = 1 << logT;
   d.tiles_per_outer = static_cast<int32_t>((nsig + d.T - 1) / d.T);
@@ -215,6 +226,10 @@ bool choose_tiling(PassDesc& d) {
   for (int p = 0; p < d.npass; ++p) work = std::max<int64_t>(work, (static_cast<int64_t>(d.L) << logT) / d.radix[p]);
   int64_t nt = ((work + 63) / 64) * 64;
   d.nthreads = static_cast<int32_t>(std::min<int64_t>(256, std::max<int64_t>(64, nt)));
+  if (const char* e = std::getenv("MI_DFT_THREADS")) {
+    const int f = std::atoi(e);
+    if (f >= 64 && f <= 256 && f % 64 == 0) d.nthreads = f;
+  }
   const int32_t nout = d.kind == Kind::C2C ? d.out_lo + d.out_hi : (d.kind == Kind::R2C ? d.out_lo : d.L);
   d.out_div = FastDiv(static_cast<uint32_t>(std::max(nout, 1)));
   return true;

@@ -156,6 +156,12 @@ void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
   TORCH_CHECK(choose_tiling(d), "amd_dft: transform length ", L, " exceeds the LDS-resident limit (",
               max_lds_length(), ")");
   finalize_vec_flags(d, static_cast<int>(in.element_size()), static_cast<int>(out.element_size()));
+  // Timing-only ablations (results are WRONG): MI_DFT_ABLATE=nopass|notw|io
+  if (const char* ab = std::getenv("MI_DFT_ABLATE")) {
+    const std::string a(ab);
+    if (a == "nopass" || a == "io") d.npass = 0;
+    if (a == "notw" || a == "io") d.tw_count = 0;
+  }
   launch_fft_pass(d, c10::hip::getCurrentHIPStream(in.device().index()).stream());
 }
 
