@@ -1,0 +1,30 @@
+// Runtime helpers for the engine layer.
+//
+// wrap_device_ptr: view a raw device pointer as a tensor (no copy).  Used by
+// Engine.execute_v2(bindings), the TensorRT-style entry point that takes raw device
+// addresses (/root/reference/tests/test_dft.py:112-114: context.execute_v2([x_ptr, y_ptr])).
+#include <ATen/ATen.h>
+#include <torch/library.h>
+
+namespace amd_dft {
+namespace {
+
+at::Tensor wrap_device_ptr(int64_t ptr, at::IntArrayRef shape, at::ScalarType dtype, int64_t device_index) {
+  TORCH_CHECK(ptr != 0, "amd_dft.wrap_device_ptr: null pointer");
+  auto opts = at::TensorOptions().dtype(dtype).device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device_index)));
+  return at::from_blob(reinterpret_cast<void*>(ptr), shape, opts);
+}
+
+at::Tensor wrap_host_ptr(int64_t ptr, at::IntArrayRef shape, at::ScalarType dtype) {
+  TORCH_CHECK(ptr != 0, "amd_dft.wrap_host_ptr: null pointer");
+  return at::from_blob(reinterpret_cast<void*>(ptr), shape, at::TensorOptions().dtype(dtype));
+}
+
+}  // namespace
+}  // namespace amd_dft
+
+TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
+  m.def("wrap_device_ptr(int ptr, int[] shape, ScalarType dtype, int device_index) -> Tensor",
+        &amd_dft::wrap_device_ptr);
+  m.def("wrap_host_ptr(int ptr, int[] shape, ScalarType dtype) -> Tensor", &amd_dft::wrap_host_ptr);
+}

@@ -1,0 +1,274 @@
+"""Static-shape inference engine: ONNX graph -> hipGraph-captured executable.
+
+Replaces the reference's TensorRT build / serialize / deserialize / execute path
+(/root/reference/tests/test_dft.py:89-115; trtexec --saveEngine/--loadEngine,
+README.md:61-75).  An engine file holds a header (magic, format and plugin version "1",
+device arch, torch/HIP versions, I/O bindings) followed by the ONNX model bytes; the DFT plans
+(twiddle tables) are rebuilt and the per-step hipGraph is re-captured on load, exactly like
+the reference re-creates its cuFFT plan in configurePlugin (dft_plugins.cpp:131-178) after
+deserialising the plugin attributes (:61-71).  Shapes are static (dft_plugins.cpp:146-152).
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import struct
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import torch
+
+from .._loader import load_plugins
+from ..onnx import exporter as onnx_export
+from ..onnx import proto as P
+from ..onnx.runner import OnnxGraph
+
+ENGINE_MAGIC = b"AMDDFTENG\x00"
+ENGINE_FORMAT_VERSION = 1
+PLUGIN_VERSION = "1"
+
+
+@dataclass
+class Binding:
+    name: str
+    shape: List[int]
+    dtype: str
+    is_input: bool
+
+    def torch_dtype(self) -> torch.dtype:
+        return getattr(torch, self.dtype)
+
+
+@dataclass
+class EngineHeader:
+    format_version: int = ENGINE_FORMAT_VERSION
+    plugin_version: str = PLUGIN_VERSION
+    arch: str = ""
+    torch_version: str = torch.__version__
+    hip_version: str = str(torch.version.hip)
+    bindings: List[Binding] = field(default_factory=list)
+    use_graph: bool = True
+    created: float = field(default_factory=time.time)
+    extra: Dict[str, object] = field(default_factory=dict)
+
+    def to_json(self) -> bytes:
+        d = dict(self.__dict__)
+        d["bindings"] = [b.__dict__ for b in self.bindings]
+        return json.dumps(d).encode()
+
+    @classmethod
+    def from_json(cls, data: bytes) -> "EngineHeader":
+        d = json.loads(data.decode())
+        d["bindings"] = [Binding(**b) for b in d.get("bindings", [])]
+        return cls(**d)
+
+
+def _device_arch(device: torch.device) -> str:
+    if device.type == "cuda" and torch.cuda.is_available():
+        return getattr(torch.cuda.get_device_properties(device), "gcnArchName", "unknown")
+    return "cpu"
+
+
+def _dtype_name(dt: torch.dtype) -> str:
+    return str(dt).replace("torch.", "")
+
+
+class Engine:
+    """A built (static-shape) engine.  Use :meth:`build`, :meth:`load` or :meth:`deserialize`."""
+
+    def __init__(self, onnx_bytes: bytes, input_shapes: Sequence[Sequence[int]],
+                 input_dtypes: Optional[Sequence[torch.dtype]] = None, device: Optional[torch.device] = None,
+                 use_graph: bool = True, warmup: int = 2, header: Optional[EngineHeader] = None):
+        load_plugins()
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        self.onnx_bytes = onnx_bytes
+        self.graph = OnnxGraph(onnx_bytes, self.device)
+        if len(input_shapes) != len(self.graph.input_names):
+            raise ValueError(f"engine has {len(self.graph.input_names)} inputs, {len(input_shapes)} shapes given")
+        input_dtypes = list(input_dtypes) if input_dtypes is not None else list(self.graph.input_dtypes)
+        self.input_shapes = [list(map(int, s)) for s in input_shapes]
+        for s, ds in zip(self.input_shapes, self.graph.input_shapes):
+            if len(ds) == len(s) and any(d > 0 and d != v for d, v in zip(ds, s)):
+                raise ValueError(f"shape {s} does not match the model's static input shape {ds}")
+        self.static_inputs = [torch.zeros(s, dtype=dt, device=self.device)
+                              for s, dt in zip(self.input_shapes, input_dtypes)]
+        self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        self._cuda_graph = None
+        # warm-up: creates every FFT plan (twiddle upload) before capture and fixes output shapes
+        self.static_outputs = self._run_eager()
+        if self.use_graph:
+            self._capture(warmup)
+        self.header = header or EngineHeader()
+        self.header.arch = _device_arch(self.device)
+        self.header.use_graph = self.use_graph
+        self.header.bindings = (
+            [Binding(n, s, _dtype_name(t.dtype), True)
+             for n, s, t in zip(self.graph.input_names, self.input_shapes, self.static_inputs)]
+            + [Binding(n, list(t.shape), _dtype_name(t.dtype), False)
+               for n, t in zip(self.graph.output_names, self.static_outputs)])
+
+    # ------------------------------------------------------------------ build
+    @classmethod
+    def build(cls, source: Union[torch.nn.Module, bytes, str], inputs: Optional[Sequence[torch.Tensor]] = None,
+              shapes: Optional[Sequence[Sequence[int]]] = None, *, device=None, use_graph: bool = True,
+              opset_version: int = onnx_export.DEFAULT_OPSET, dtypes=None) -> "Engine":
+        """Build from an ``nn.Module`` (exported to ONNX with ``inputs``), ONNX bytes or a path."""
+        if isinstance(source, torch.nn.Module):
+            if inputs is None:
+                raise ValueError("building from a module needs example inputs")
+            ins = tuple(inputs) if isinstance(inputs, (list, tuple)) else (inputs,)
+            onnx_bytes = onnx_export.export(source, tuple(i.cpu() for i in ins), opset_version=opset_version)
+            shapes = shapes or [list(i.shape) for i in ins]
+            dtypes = dtypes or [i.dtype for i in ins]
+        else:
+            onnx_bytes = open(source, "rb").read() if isinstance(source, str) else bytes(source)
+            if shapes is None:
+                g = OnnxGraph(onnx_bytes, device="cpu")
+                shapes = g.input_shapes
+                if any(d < 0 for s in shapes for d in s):
+                    raise ValueError(f"model has dynamic input dims {shapes}: pass shapes= (trtexec --shapes)")
+        return cls(onnx_bytes, shapes, dtypes, device=device, use_graph=use_graph)
+
+    # ------------------------------------------------------------------ execution
+    def _run_eager(self) -> List[torch.Tensor]:
+        with torch.no_grad():
+            return list(self.graph.run(*self.static_inputs))
+
+    def _capture(self, warmup: int) -> None:
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(max(1, warmup)):
+                self._run_eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            outs = self._run_eager()
+        self._cuda_graph = g
+        self.static_outputs = outs
+
+    def enqueue(self) -> None:
+        """Run one step on the current stream with whatever is in ``static_inputs``."""
+        if self._cuda_graph is not None:
+            self._cuda_graph.replay()
+        else:
+            outs = self._run_eager()
+            for so, o in zip(self.static_outputs, outs):
+                so.copy_(o)
+
+    def infer(self, *inputs: torch.Tensor, copy_outputs: bool = True) -> List[torch.Tensor]:
+        for si, x in zip(self.static_inputs, inputs):
+            if list(x.shape) != list(si.shape):
+                raise ValueError(f"input shape {list(x.shape)} != engine binding {list(si.shape)} (static shapes)")
+            si.copy_(x, non_blocking=True)
+        self.enqueue()
+        return [o.clone() for o in self.static_outputs] if copy_outputs else list(self.static_outputs)
+
+    __call__ = infer
+
+    def execute_v2(self, bindings: Sequence[Union[int, torch.Tensor]]) -> bool:
+        """TensorRT-style synchronous execute: ``bindings`` = input then output device pointers
+        (ints) or tensors, in binding order (reference: test_dft.py:112-114)."""
+        n_in, n_out = len(self.static_inputs), len(self.static_outputs)
+        if len(bindings) != n_in + n_out:
+            raise ValueError(f"expected {n_in + n_out} bindings, got {len(bindings)}")
+        views = []
+        for b, t in zip(bindings, self.static_inputs + self.static_outputs):
+            if isinstance(b, torch.Tensor):
+                views.append(b)
+            elif self.device.type == "cuda":
+                views.append(torch.ops.amd_dft.wrap_device_ptr(int(b), list(t.shape), t.dtype, self.device.index or 0))
+            else:
+                views.append(torch.ops.amd_dft.wrap_host_ptr(int(b), list(t.shape), t.dtype))
+        for si, v in zip(self.static_inputs, views[:n_in]):
+            si.copy_(v)
+        self.enqueue()
+        for so, v in zip(self.static_outputs, views[n_in:]):
+            v.copy_(so)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return True
+
+    # ------------------------------------------------------------------ (de)serialisation
+    def serialize(self) -> bytes:
+        h = self.header.to_json()
+        return ENGINE_MAGIC + struct.pack("<I", len(h)) + h + struct.pack("<Q", len(self.onnx_bytes)) + self.onnx_bytes
+
+    def save(self, path: str) -> None:
+        with open(path, "wb") as f:
+            f.write(self.serialize())
+
+    @classmethod
+    def deserialize(cls, data: bytes, device=None, use_graph: Optional[bool] = None) -> "Engine":
+        if not data.startswith(ENGINE_MAGIC):
+            raise ValueError("not an amd_dft engine file (bad magic)")
+        off = len(ENGINE_MAGIC)
+        (hl,) = struct.unpack_from("<I", data, off)
+        off += 4
+        header = EngineHeader.from_json(data[off:off + hl])
+        off += hl
+        (ol,) = struct.unpack_from("<Q", data, off)
+        off += 8
+        onnx_bytes = data[off:off + ol]
+        if header.format_version != ENGINE_FORMAT_VERSION or header.plugin_version != PLUGIN_VERSION:
+            raise ValueError(f"engine format {header.format_version}/plugin {header.plugin_version} not supported")
+        ins = [b for b in header.bindings if b.is_input]
+        return cls(onnx_bytes, [b.shape for b in ins], [b.torch_dtype() for b in ins], device=device,
+                   use_graph=header.use_graph if use_graph is None else use_graph, header=header)
+
+    @classmethod
+    def load(cls, path: str, device=None, use_graph: Optional[bool] = None) -> "Engine":
+        with open(path, "rb") as f:
+            return cls.deserialize(f.read(), device=device, use_graph=use_graph)
+
+    # ------------------------------------------------------------------ introspection / timing
+    @property
+    def bindings(self) -> List[Binding]:
+        return self.header.bindings
+
+    @property
+    def input_names(self) -> List[str]:
+        return list(self.graph.input_names)
+
+    @property
+    def output_names(self) -> List[str]:
+        return list(self.graph.output_names)
+
+    def benchmark(self, iterations: int = 100, warmup: int = 10, fill_random: bool = True) -> Dict[str, float]:
+        """trtexec-style timing of ``iterations`` enqueues (GPU time per enqueue, ms)."""
+        if fill_random:
+            for si in self.static_inputs:
+                if si.is_floating_point():
+                    si.copy_(torch.randn_like(si))
+        for _ in range(warmup):
+            self.enqueue()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iterations)]
+            t0 = time.perf_counter()
+            for a, b in evs:
+                a.record()
+                self.enqueue()
+                b.record()
+            torch.cuda.synchronize(self.device)
+            wall = time.perf_counter() - t0
+            lat = sorted(a.elapsed_time(b) for a, b in evs)
+        else:
+            lat = []
+            t0 = time.perf_counter()
+            for _ in range(iterations):
+                t1 = time.perf_counter()
+                self.enqueue()
+                lat.append((time.perf_counter() - t1) * 1e3)
+            wall = time.perf_counter() - t0
+            lat.sort()
+        return {
+            "iterations": iterations, "throughput_qps": iterations / wall,
+            "latency_min_ms": lat[0], "latency_mean_ms": statistics.mean(lat),
+            "latency_median_ms": statistics.median(lat), "latency_p99_ms": lat[min(len(lat) - 1, int(0.99 * len(lat)))],
+            "latency_max_ms": lat[-1], "total_wall_s": wall,
+        }
