@@ -42,6 +42,8 @@ struct PassDesc {
   const void* in = nullptr;
   void* out = nullptr;
   const void* tw = nullptr;  // device float2 table: per-pass twiddles + generic radix roots
+  const void* add1 = nullptr;  // C2R epilogue addends (same layout and dtype as out), or null
+  const void* add2 = nullptr;
 
   int32_t L = 1;       // transform length
   int32_t npass = 0;   // number of Stockham passes (0 when L == 1)

@@ -87,6 +87,8 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
   a.scale = d.scale;
   a.inverse = d.inverse; a.vec_in = d.vec_in; a.vec_out = d.vec_out;
   a.bf16_in = d.tin == DType::BF16; a.bf16_out = d.tout == DType::BF16;
+  a.add1 = d.add1;
+  a.add2 = d.add2;
   const int64_t nblocks = d.O * a.tiles_per_outer;
   if (nblocks <= 0) return true;
   if (nblocks > 0x7fffffffLL) throw std::runtime_error("amd_dft: FFT grid too large");

@@ -30,6 +30,8 @@ struct FixedArgs {
   int32_t in_lo, in_hi, out_lo, out_hi, tiles_per_outer;
   float scale;
   int32_t inverse, vec_in, vec_out, bf16_in, bf16_out;
+  const void* add1;  // C2R epilogue: out = scale * irfft + add1 (+ add2); same layout/dtype as out
+  const void* add2;
 };
 
 template <int... Rs>
@@ -96,6 +98,8 @@ struct Ctx {
   FixedArgs a;
   const void* in;   // outer-offset applied
   void* out;
+  const void* add1;  // outer-offset applied
+  const void* add2;
   int32_t c;        // complex signal index
   int32_t cc;       // c clamped into [0, I) (C2C) -- loads are never predicated by branches
   int32_t i0c, i1c; // paired logical signals 2c, 2c+1 clamped into [0, I) (R2C / C2R)
@@ -147,7 +151,7 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
 }
 
 // Last-pass element store (C2C / C2R), with output pruning and the fused scale.
-template <Kind K, int L, bool BF, bool PR>
+template <Kind K, int L, bool BF, bool PR, int NADD>
 __device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v) {
   const FixedArgs& a = x.a;
   if constexpr (K == Kind::C2C) {
@@ -159,11 +163,20 @@ __device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v) {
       if (x.ok0) st_c<BF>(x.out, x.c * a.Si_out + n * a.Sn_out, make_float2(v.x * a.scale, v.y * a.scale));
     }
   } else {
-    const float va = v.x * a.scale;
-    const float vb = (a.inverse ? -v.y : v.y) * a.scale;
+    float va = v.x * a.scale;
+    float vb = (a.inverse ? -v.y : v.y) * a.scale;
     const int32_t off = x.i0c * a.Si_out + n * a.Sn_out;
+    const int32_t offb = x.i1c * a.Si_out + n * a.Sn_out;
+    if constexpr (NADD >= 1) {
+      va += ld_r<BF>(x.add1, off);
+      vb += ld_r<BF>(x.add1, offb);
+    }
+    if constexpr (NADD >= 2) {
+      va += ld_r<BF>(x.add2, off);
+      vb += ld_r<BF>(x.add2, offb);
+    }
     if (x.ok0) st_r<BF>(x.out, off, va);
-    if (x.ok1) st_r<BF>(x.out, off + a.Si_out, vb);
+    if (x.ok1) st_r<BF>(x.out, offb, vb);
   }
 }
 
@@ -194,7 +207,7 @@ __device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, T
   }
 }
 
-template <Kind K, bool COLS, int TP, int T, class F, int P, bool BFI, bool BFO, bool PR>
+template <Kind K, bool COLS, int TP, int T, class F, int P, bool BFI, bool BFO, bool PR, int NADD>
 struct Step {
   using G = PassGeom<F, TP, P>;
   static constexpr int NP = F::N;
@@ -209,7 +222,7 @@ struct Step {
       float2 twn[GN::Q][GN::TWR];
       load_tw<F, TP, P + 1>(x, twn);
       body(x, tw);
-      Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR>::run(x, twn);
+      Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR, NADD>::run(x, twn);
     } else {
       body(x, tw);
     }
@@ -250,7 +263,7 @@ struct Step {
         const int j = x.tp + q * TP;
         if (G::EXACT || j < LR) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) scatter<K, L, BFO, PR>(x, j + r * Ns, v[q][r]);
+          for (int r = 0; r < R; ++r) scatter<K, L, BFO, PR, NADD>(x, j + r * Ns, v[q][r]);
         }
       }
     } else {
@@ -269,7 +282,7 @@ struct Step {
   }
 };
 
-template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR>
+template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD>
 __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   constexpr int L = F::L;
   constexpr int LDSN = COLS ? lds_pad(L * T) + 2 : T * (lds_pad(L) + 1);
@@ -293,10 +306,12 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   }
   x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
   x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  if constexpr (NADD >= 1) x.add1 = static_cast<const char*>(a.add1) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  if constexpr (NADD >= 2) x.add2 = static_cast<const char*>(a.add2) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
   x.lds = lds;
   using G0 = PassGeom<F, TP, 0>;
   float2 tw0[G0::Q][G0::TWR];
-  Step<K, COLS, TP, T, F, 0, BFI, BFO, PR>::run(x, tw0);
+  Step<K, COLS, TP, T, F, 0, BFI, BFO, PR, NADD>::run(x, tw0);
   if constexpr (K == Kind::R2C) {
     // Z (natural order) is in LDS: separate the two packed real signals' half spectra.
     constexpr int KMAX = L / 2 + 1;
@@ -334,15 +349,15 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)
 
-template <Kind K, bool COLS, int TP, int T, class F, bool PR>
+template <Kind K, bool COLS, int TP, int T, class F, bool PR, int NADD>
 void launch_dt(const FixedArgs& a, dim3 grid, hipStream_t st) {
   const dim3 blk(TP * T);
   if (a.bf16_in) {
-    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, PR>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, false, PR>), grid, blk, 0, st, a);
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, PR, NADD>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, false, PR, NADD>), grid, blk, 0, st, a);
   } else {
-    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, true, PR>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, PR>), grid, blk, 0, st, a);
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, true, PR, NADD>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, PR, NADD>), grid, blk, 0, st, a);
   }
 }
 
@@ -352,9 +367,13 @@ void launch_one(const FixedArgs& a, dim3 grid, hipStream_t st) {
   // (cheap, Hermitian) truncation in the common path.
   const bool pr = K == Kind::C2C && (a.in_lo + a.in_hi != F::L || a.out_lo + a.out_hi != F::L);
   if constexpr (K == Kind::C2C) {
-    if (pr) return launch_dt<K, COLS, TP, T, F, true>(a, grid, st);
+    if (pr) return launch_dt<K, COLS, TP, T, F, true, 0>(a, grid, st);
   }
-  launch_dt<K, COLS, TP, T, F, false>(a, grid, st);
+  if constexpr (K == Kind::C2R) {
+    if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2>(a, grid, st);
+    if (a.add1) return launch_dt<K, COLS, TP, T, F, false, 1>(a, grid, st);
+  }
+  launch_dt<K, COLS, TP, T, F, false, 0>(a, grid, st);
 }
 
 using LaunchFn = void (*)(const FixedArgs&, dim3, hipStream_t);

@@ -337,9 +337,18 @@ __global__ void __launch_bounds__(256) fft_pass_kernel(const PassDesc d) {
       const int64_t i0 = 2 * (c0 + t);
       if (i0 >= d.I) continue;
       const float2 y = src[lds_ix((n << logT) + t)];
-      const float a = y.x * sc;
-      const float b = (d.inverse ? -y.y : y.y) * sc;
+      float a = y.x * sc;
+      float b = (d.inverse ? -y.y : y.y) * sc;
       TO* p = out + i0 * d.Si_out + n * d.Sn_out;
+      const int64_t poff = (p - static_cast<TO*>(d.out));
+      if (d.add1) {
+        a += IO<TO>::ld(static_cast<const TO*>(d.add1) + poff);
+        if (i0 + 1 < d.I) b += IO<TO>::ld(static_cast<const TO*>(d.add1) + poff + d.Si_out);
+      }
+      if (d.add2) {
+        a += IO<TO>::ld(static_cast<const TO*>(d.add2) + poff);
+        if (i0 + 1 < d.I) b += IO<TO>::ld(static_cast<const TO*>(d.add2) + poff + d.Si_out);
+      }
       if (d.vec_out && i0 + 1 < d.I) {
         IO<TO>::st2(p, make_float2(a, b));
       } else {

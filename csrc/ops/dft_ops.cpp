@@ -29,70 +29,10 @@
 #include <unordered_map>
 
 #include "../fft/fft_plan.h"
+#include "plan_cache.h"
 
 namespace amd_dft {
 namespace {
-
-// ------------------------------------------------------------------ plan cache
-struct DevPlan {
-  Plan1D plan;
-  at::Tensor tw;  // device float32 [2*tw_count]
-};
-
-class PlanCache {
- public:
-  std::shared_ptr<DevPlan> get(int64_t L, const at::Device& dev) {
-    const uint64_t key = (static_cast<uint64_t>(dev.index() + 1) << 40) | static_cast<uint64_t>(L);
-    std::lock_guard<std::mutex> g(mu_);
-    auto it = map_.find(key);
-    if (it != map_.end()) {
-      lru_.splice(lru_.begin(), lru_, it->second.second);
-      return it->second.first;
-    }
-    TORCH_CHECK(c10::hip::currentStreamCaptureStatusMayInitCtx() == c10::hip::CaptureStatus::None,
-                "amd_dft: FFT plan for length ", L,
-                " was not created before graph capture; run the model once (warm-up) before capturing");
-    auto dp = std::make_shared<DevPlan>();
-    dp->plan = make_plan_1d(static_cast<int32_t>(L));
-    auto host = at::from_blob(dp->plan.tw_host.data(), {static_cast<int64_t>(dp->plan.tw_host.size())},
-                              at::TensorOptions().dtype(at::kFloat));
-    dp->tw = host.to(dev);
-    lru_.push_front(key);
-    map_[key] = {dp, lru_.begin()};
-    while (map_.size() > capacity()) {
-      map_.erase(lru_.back());
-      lru_.pop_back();
-    }
-    return dp;
-  }
-  void clear() {
-    std::lock_guard<std::mutex> g(mu_);
-    map_.clear();
-    lru_.clear();
-  }
-  size_t size() {
-    std::lock_guard<std::mutex> g(mu_);
-    return map_.size();
-  }
-
- private:
-  static size_t capacity() {
-    static size_t cap = [] {
-      const char* e = std::getenv("MI_DFT_PLAN_CACHE_SIZE");
-      long v = e ? std::atol(e) : 256;
-      return static_cast<size_t>(v > 0 ? v : 256);
-    }();
-    return cap;
-  }
-  std::mutex mu_;
-  std::list<uint64_t> lru_;
-  std::unordered_map<uint64_t, std::pair<std::shared_ptr<DevPlan>, std::list<uint64_t>::iterator>> map_;
-};
-
-PlanCache& plan_cache() {
-  static PlanCache c;
-  return c;
-}
 
 // ------------------------------------------------------------------ helpers
 DType to_dtype(at::ScalarType t) {
@@ -136,8 +76,8 @@ at::Tensor alloc_complex(const std::vector<int64_t>& logical, const at::TensorOp
 
 void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
               const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
-              int out_hi, float scale, bool inverse) {
-  auto dp = plan_cache().get(L, in.device());
+              int out_hi, float scale, bool inverse, const void* add1 = nullptr, const void* add2 = nullptr) {
+  auto dp = get_plan(L, in.device());
   PassDesc d;
   d.kind = kind;
   apply_plan(d, dp->plan);
@@ -153,6 +93,8 @@ void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
   d.tout = to_dtype(out.scalar_type());
   d.in = in.data_ptr();
   d.out = out.data_ptr();
+  d.add1 = add1;
+  d.add2 = add2;
   TORCH_CHECK(choose_tiling(d), "amd_dft: transform length ", L, " exceeds the LDS-resident limit (",
               max_lds_length(), ")");
   finalize_vec_flags(d, static_cast<int>(in.element_size()), static_cast<int>(out.element_size()));
@@ -266,8 +208,9 @@ at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at:
   return cur_t;
 }
 
-at::Tensor c2r_cuda(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
-                    at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
+at::Tensor c2r_cuda_impl(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                         at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype,
+                         const std::optional<at::Tensor>& add1, const std::optional<at::Tensor>& add2) {
   const c10::DeviceGuard guard(x_.device());
   at::Tensor x = x_.contiguous();
   to_dtype(x.scalar_type());
@@ -288,11 +231,21 @@ at::Tensor c2r_cuda(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef o
     const float sc = final_pass ? static_cast<float>(scale) : 1.0f;
     if (final_pass) {
       at::Tensor out = at::empty(nxt, opts.dtype(odt));
+      const void* a1 = nullptr;
+      const void* a2 = nullptr;
+      for (int k = 0; k < 2; ++k) {
+        const auto& ad = k == 0 ? add1 : add2;
+        if (!ad.has_value()) continue;
+        TORCH_CHECK(ad->sizes() == out.sizes() && ad->scalar_type() == odt && ad->is_contiguous() &&
+                        ad->device() == out.device(),
+                    "amd_dft.c2r_add: addend must be contiguous with the output's shape, dtype and device");
+        (k == 0 ? a1 : a2) = ad->data_ptr();
+      }
       const int64_t half = s.n / 2 + 1;
       const int in_lo = static_cast<int>(std::min<int64_t>(s.lo, half));
       // When more modes are stored than the half spectrum, the extra ones are ignored; the
       // stored stride along the axis stays the stored size (geometry from `cur`).
-      run_pass(Kind::C2R, cur_t, out, cur, nxt, s.axis, s.n, in_lo, 0, static_cast<int>(s.n), 0, sc, true);
+      run_pass(Kind::C2R, cur_t, out, cur, nxt, s.axis, s.n, in_lo, 0, static_cast<int>(s.n), 0, sc, true, a1, a2);
       cur_t = out;
     } else {
       at::Tensor out = alloc_complex(nxt, opts, at::kFloat);
@@ -303,6 +256,17 @@ at::Tensor c2r_cuda(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef o
     cur = nxt;
   }
   return cur_t;
+}
+
+at::Tensor c2r_cuda(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                    at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
+  return c2r_cuda_impl(x, dim, out_size, scale, keep, out_dtype, std::nullopt, std::nullopt);
+}
+
+at::Tensor c2r_add_cuda(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                        at::IntArrayRef keep, const std::optional<at::Tensor>& add1,
+                        const std::optional<at::Tensor>& add2, std::optional<at::ScalarType> out_dtype) {
+  return c2r_cuda_impl(x, dim, out_size, scale, keep, out_dtype, add1, add2);
 }
 
 at::Tensor c2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, bool inverse, double scale,
@@ -383,6 +347,15 @@ at::Tensor c2r_cpu(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out
   return y.to(odt).contiguous();
 }
 
+at::Tensor c2r_add_cpu(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                       at::IntArrayRef keep, const std::optional<at::Tensor>& add1,
+                       const std::optional<at::Tensor>& add2, std::optional<at::ScalarType> out_dtype) {
+  at::Tensor y = c2r_cpu(x, dim, out_size, scale, keep, at::kFloat);
+  if (add1.has_value()) y = y + add1->to(at::kFloat);
+  if (add2.has_value()) y = y + add2->to(at::kFloat);
+  return y.to(out_dtype.value_or(x.scalar_type())).contiguous();
+}
+
 at::Tensor c2c_cpu(const at::Tensor& x, at::IntArrayRef dim, bool inverse, double scale,
                    std::optional<at::ScalarType> out_dtype) {
   TORCH_CHECK(x.dim() >= 2 && x.size(-1) == 2, "amd_dft: complex input must have a trailing dim of size 2");
@@ -406,6 +379,11 @@ at::Tensor c2r_meta(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef ou
                     at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype) {
   C2RShape sh = c2r_shape(x.sizes(), dim, out_size, keep);
   return at::empty(sh.out_real, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+}
+at::Tensor c2r_add_meta(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                        at::IntArrayRef keep, const std::optional<at::Tensor>&, const std::optional<at::Tensor>&,
+                        std::optional<at::ScalarType> out_dtype) {
+  return c2r_meta(x, dim, out_size, scale, keep, out_dtype);
 }
 at::Tensor c2c_meta(const at::Tensor& x, at::IntArrayRef, bool, double, std::optional<at::ScalarType> out_dtype) {
   return at::empty_like(x, x.options().dtype(out_dtype.value_or(x.scalar_type())));
@@ -472,8 +450,8 @@ std::string plugin_registry() {
          R"( {"name": "signal_ndim", "type": "INT32", "default": 1}]}])";
 }
 
-int64_t plan_cache_size() { return static_cast<int64_t>(plan_cache().size()); }
-void plan_cache_clear() { plan_cache().clear(); }
+int64_t plan_cache_size() { return static_cast<int64_t>(plan_cache_entries()); }
+void plan_cache_clear() { plan_cache_reset(); }
 
 }  // namespace
 }  // namespace amd_dft
@@ -482,6 +460,8 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("r2c(Tensor x, int[] dim, float scale=1.0, int[] keep=[], ScalarType? out_dtype=None) -> Tensor");
   m.def("c2r(Tensor x, int[] dim, int[] out_size, float scale=1.0, int[] keep=[], ScalarType? out_dtype=None) -> Tensor");
   m.def("c2c(Tensor x, int[] dim, bool inverse=False, float scale=1.0, ScalarType? out_dtype=None) -> Tensor");
+  m.def("c2r_add(Tensor x, int[] dim, int[] out_size, float scale=1.0, int[] keep=[], Tensor? add1=None, "
+        "Tensor? add2=None, ScalarType? out_dtype=None) -> Tensor");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("plan_info(int n) -> str", &amd_dft::plan_info);
@@ -494,18 +474,21 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("r2c", &amd_dft::r2c_cuda);
   m.impl("c2r", &amd_dft::c2r_cuda);
   m.impl("c2c", &amd_dft::c2c_cuda);
+  m.impl("c2r_add", &amd_dft::c2r_add_cuda);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("r2c", &amd_dft::r2c_cpu);
   m.impl("c2r", &amd_dft::c2r_cpu);
   m.impl("c2c", &amd_dft::c2c_cpu);
+  m.impl("c2r_add", &amd_dft::c2r_add_cpu);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("r2c", &amd_dft::r2c_meta);
   m.impl("c2r", &amd_dft::c2r_meta);
   m.impl("c2c", &amd_dft::c2c_meta);
+  m.impl("c2r_add", &amd_dft::c2r_add_meta);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {

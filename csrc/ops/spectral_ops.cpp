@@ -1,0 +1,155 @@
+// Torch op layer for the fused spectral-layer kernels (FourCastNet AFNO, FNO) and the
+// fused LayerNorm.  CPU implementations are plain ATen math (reference semantics); the
+// CUDA (HIP) implementations launch the hand-written gfx950 kernels.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "../spectral/spectral.h"
+#include "plan_cache.h"
+
+namespace amd_dft {
+namespace {
+
+// ------------------------------------------------------------------ AFNO spectral filter
+// xw [B, H, KM, C, 2] fp32 (W-direction half spectrum), w1t/w2t [NB, 2BS, 2BS] bf16 ([n][k]),
+// b1/b2 [NB, 2BS] fp32.  Returns [B, H, KM, C, 2] fp32:
+//   IFFT_H( softshrink( ReLU(FFT_H(x) W1' + b1') W2' + b2' ) )   (FFTs unnormalised)
+void check_afno(const at::Tensor& xw, const at::Tensor& w1t, const at::Tensor& w2t, const at::Tensor& b1,
+                const at::Tensor& b2) {
+  TORCH_CHECK(xw.dim() == 5 && xw.size(4) == 2 && xw.scalar_type() == at::kFloat,
+              "afno_spectral: x must be [B, H, KM, C, 2] float32");
+  const int64_t NB = w1t.size(0), K = w1t.size(1);
+  TORCH_CHECK(w1t.dim() == 3 && w1t.size(2) == K && w2t.sizes() == w1t.sizes(), "afno_spectral: bad weight shapes");
+  TORCH_CHECK(NB * K == 2 * xw.size(3), "afno_spectral: NB * 2 * block_size must equal 2 * C");
+  TORCH_CHECK(b1.sizes() == at::IntArrayRef({NB, K}) && b2.sizes() == b1.sizes(), "afno_spectral: bad bias shapes");
+}
+
+at::Tensor afno_spectral_cpu(const at::Tensor& xw, const at::Tensor& w1t, const at::Tensor& w2t, const at::Tensor& b1,
+                             const at::Tensor& b2, double lam) {
+  check_afno(xw, w1t, w2t, b1, b2);
+  const int64_t B = xw.size(0), H = xw.size(1), KM = xw.size(2), C = xw.size(3);
+  const int64_t NB = w1t.size(0), BS = C / NB;
+  at::Tensor X = at::fft_fft(at::view_as_complex(xw.contiguous()), std::nullopt, 1, "backward");
+  at::Tensor Xr = at::view_as_real(X).reshape({B, H, KM, NB, BS, 2});
+  at::Tensor A = at::cat({Xr.select(-1, 0), Xr.select(-1, 1)}, -1);  // [..., NB, 2BS]
+  at::Tensor W1 = w1t.to(at::kFloat).transpose(1, 2);                // [NB, k, n]
+  at::Tensor W2 = w2t.to(at::kFloat).transpose(1, 2);
+  at::Tensor H1 = at::relu(at::einsum("...bk,bkn->...bn", {A, W1}) + b1);
+  at::Tensor O = at::einsum("...bk,bkn->...bn", {H1, W2}) + b2;
+  O = at::softshrink(O, lam);
+  at::Tensor Oc = at::complex(O.narrow(-1, 0, BS), O.narrow(-1, BS, BS)).reshape({B, H, KM, C});
+  at::Tensor Y = at::fft_ifft(Oc, std::nullopt, 1, "forward");
+  return at::view_as_real(Y).contiguous();
+}
+
+at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, const at::Tensor& w2t_, const at::Tensor& b1_,
+                              const at::Tensor& b2_, double lam) {
+  check_afno(xw_, w1t_, w2t_, b1_, b2_);
+  const c10::DeviceGuard guard(xw_.device());
+  at::Tensor xw = xw_.contiguous();
+  at::Tensor w1t = w1t_.to(at::kBFloat16).contiguous(), w2t = w2t_.to(at::kBFloat16).contiguous();
+  at::Tensor b1 = b1_.to(at::kFloat).contiguous(), b2 = b2_.to(at::kFloat).contiguous();
+  const int64_t B = xw.size(0), H = xw.size(1), KM = xw.size(2), C = xw.size(3), NB = w1t.size(0);
+  TORCH_CHECK(afno_spectral_supported(static_cast<int>(H), static_cast<int>(C / NB)),
+              "afno_spectral: fused kernel supports H == 90 and block size 96 (use the generic path)");
+  at::Tensor y = at::empty_like(xw);
+  if (xw.numel() == 0) return y;
+  auto dp = get_plan(H, xw.device());
+  AfnoLaunch p;
+  p.x = xw.data_ptr<float>();
+  p.y = y.data_ptr<float>();
+  p.w1t = reinterpret_cast<const uint16_t*>(w1t.data_ptr());
+  p.w2t = reinterpret_cast<const uint16_t*>(w2t.data_ptr());
+  p.b1 = b1.data_ptr<float>();
+  p.b2 = b2.data_ptr<float>();
+  p.tw = dp->tw.data_ptr();
+  p.B = static_cast<int>(B);
+  p.H = static_cast<int>(H);
+  p.KM = static_cast<int>(KM);
+  p.C = static_cast<int>(C);
+  p.NB = static_cast<int>(NB);
+  p.lambda = static_cast<float>(lam);
+  launch_afno_spectral(p, c10::hip::getCurrentHIPStream(xw.device().index()).stream());
+  return y;
+}
+
+bool afno_spectral_ok(int64_t H, int64_t block_size) {
+  return afno_spectral_supported(static_cast<int>(H), static_cast<int>(block_size));
+}
+
+// ------------------------------------------------------------------ LayerNorm (+ residual)
+std::tuple<at::Tensor, at::Tensor> layer_norm_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                                  double eps, const std::optional<at::Tensor>& residual) {
+  at::Tensor xs = residual.has_value() ? (x.to(at::kFloat) + residual->to(at::kFloat)).to(x.scalar_type()) : x;
+  at::Tensor y = at::layer_norm(xs.to(at::kFloat), {x.size(-1)}, w.to(at::kFloat), b.to(at::kFloat), eps);
+  return {y.to(x.scalar_type()), xs};
+}
+
+std::tuple<at::Tensor, at::Tensor> layer_norm_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& b_,
+                                                   double eps, const std::optional<at::Tensor>& residual) {
+  const c10::DeviceGuard guard(x_.device());
+  if (x_.scalar_type() != at::kBFloat16 || x_.size(-1) % 8 != 0 || x_.size(-1) > 2048) {
+    return layer_norm_cpu(x_, w_, b_, eps, residual);  // ATen ops on the device tensors
+  }
+  at::Tensor x = x_.contiguous();
+  at::Tensor w = w_.to(at::kBFloat16).contiguous(), b = b_.to(at::kBFloat16).contiguous();
+  at::Tensor y = at::empty_like(x);
+  at::Tensor xs = x;
+  LayerNormLaunch p;
+  p.x = x.data_ptr();
+  p.y = y.data_ptr();
+  p.gamma = w.data_ptr();
+  p.beta = b.data_ptr();
+  p.residual = nullptr;
+  p.resid_out = nullptr;
+  at::Tensor r;
+  if (residual.has_value()) {
+    r = residual->to(at::kBFloat16).contiguous();
+    TORCH_CHECK(r.sizes() == x.sizes(), "layer_norm: residual shape mismatch");
+    xs = at::empty_like(x);
+    p.residual = r.data_ptr();
+    p.resid_out = xs.data_ptr();
+  }
+  p.cols = static_cast<int>(x.size(-1));
+  p.rows = x.numel() / p.cols;
+  p.eps = static_cast<float>(eps);
+  p.bf16 = 1;
+  if (p.rows > 0) launch_layernorm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return {y, xs};
+}
+
+std::tuple<at::Tensor, at::Tensor> layer_norm_meta(const at::Tensor& x, const at::Tensor&, const at::Tensor&, double,
+                                                   const std::optional<at::Tensor>&) {
+  return {at::empty_like(x), at::empty_like(x)};
+}
+
+at::Tensor afno_spectral_meta(const at::Tensor& xw, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                              const at::Tensor&, double) {
+  return at::empty_like(xw);
+}
+
+}  // namespace
+}  // namespace amd_dft
+
+TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
+  m.def("afno_spectral(Tensor x, Tensor w1t, Tensor w2t, Tensor b1, Tensor b2, float lam) -> Tensor");
+  m.def("afno_spectral_supported(int H, int block_size) -> bool", &amd_dft::afno_spectral_ok);
+  m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
+  m.impl("afno_spectral", &amd_dft::afno_spectral_cuda);
+  m.impl("layer_norm", &amd_dft::layer_norm_cuda);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
+  m.impl("afno_spectral", &amd_dft::afno_spectral_cpu);
+  m.impl("layer_norm", &amd_dft::layer_norm_cpu);
+}
+
+TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
+  m.impl("afno_spectral", &amd_dft::afno_spectral_meta);
+  m.impl("layer_norm", &amd_dft::layer_norm_meta);
+}

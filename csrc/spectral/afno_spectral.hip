@@ -1,0 +1,312 @@
+// Fused AFNO spectral filter along H (FourCastNet AFNO2D, K5 in SURVEY §2.5).
+//
+// One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H (=90),
+// c < 96, complex fp32, produced by the W-direction R2C pass.  In one launch it runs
+//   FFT_H (Stockham [9,10], register first pass)  ->
+//   O1 = ReLU([Xr|Xi] . W1' + b1')  (bf16 MFMA 16x16x32, fp32 accumulate)  ->
+//   O2 = O1 . W2' + b2'  -> softshrink(lambda)  ->
+//   IFFT_H (register last pass, stored straight to global)
+// where W' = [[W0, W1], [-W1, W0]] is the real 192x192 form of the complex 96x96 block weight
+// (pre-packed transposed, [n][k], so a lane's B fragment is 16 contiguous bytes).
+// Everything between the global load and the global store stays in 69 KB of LDS and in
+// registers (2 workgroups / CU); the reference FourCastNet path is ~10 separate kernels with
+// 4 spectrum round trips through HBM.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../fft/radix.h"
+#include "spectral.h"
+
+namespace amd_dft {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNT = 256;      // threads
+constexpr int kBS = 96;       // channels per AFNO block
+constexpr int kK = 2 * kBS;   // real-block GEMM K = N = 192
+constexpr int kAPitch = kK + 8;  // bf16 elements per A row (+16 B pad: ds_read_b128 spread)
+
+__device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+
+// Stockham pass over 96 interleaved signals in LDS (layout [n][96]) with register staging:
+// gather -> barrier -> twiddle/DFT -> scatter.  SRC_GLOBAL: pass 0 reads global memory.
+template <int R, int L, int Ns, int GOFF>
+struct HPass {
+  static constexpr int LR = L / R;
+  static constexpr int NB = LR * kBS;
+  static constexpr int Q = (NB + kNT - 1) / kNT;
+};
+
+template <int R, int L, int Ns, int GOFF, int Q>
+__device__ __forceinline__ void h_twiddle_dft(float2 (&v)[Q][R], const float2* __restrict__ tw) {
+  using P = HPass<R, L, Ns, GOFF>;
+  static_assert(P::Q == Q, "pass geometry");
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int b = threadIdx.x + q * kNT;
+    if (P::NB % kNT == 0 || b < P::NB) {
+      const int j = b / kBS;
+      if constexpr (Ns > 1) {
+        const int k = j % Ns;
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[GOFF + (r - 1) * Ns + k]);
+      }
+      Dft<R>::run(v[q]);
+    }
+  }
+}
+
+struct AfnoArgs {
+  const float* x;       // [B, H, KM, C, 2]
+  float* y;             // [B, H, KM, C, 2]
+  const uint16_t* w1t;  // [NB][192][192] bf16, [n][k]
+  const uint16_t* w2t;
+  const float* b1;      // [NB][192]
+  const float* b2;
+  const float2* tw;     // plan twiddles for length H ([9,10] order)
+  int KM, C, NB, H;
+  float lambda;
+};
+
+// GEMM [96 x 192] = A (LDS bf16, pitch kAPitch) x Bt^T (global bf16 [n][k]); wave w owns
+// N-tiles 3w..3w+2 for all 6 M-tiles.
+__device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                                            f32x4 (&acc)[6][3]) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bfr[6][3];
+#pragma unroll
+  for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+    for (int nj = 0; nj < 3; ++nj) {
+      const int n = (3 * w + nj) * 16 + r16;
+      bfr[ks][nj] = *reinterpret_cast<const bf16x8*>(Bt + n * kK + ks * 32 + kq * 8);
+    }
+#pragma unroll
+  for (int ks = 0; ks < 6; ++ks) {
+    bf16x8 afr[6];
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+      afr[mi] = *reinterpret_cast<const bf16x8*>(A + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj)
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bfr[ks][nj], acc[mi][nj], 0, 0, 0);
+  }
+}
+
+template <int L, int R0, int R1>
+__global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a) {
+  static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];  // [L][96] complex fp32 (69 KB at L=90)
+  uint16_t* A = reinterpret_cast<uint16_t*>(lds);               // aliases lds: [96][kAPitch] bf16
+  const int tid = threadIdx.x;
+  const int blk = blockIdx.x % a.NB;
+  const int bk = blockIdx.x / a.NB;  // b * KM + kw
+  const int kw = bk % a.KM;
+  const int b = bk / a.KM;
+  const int64_t row_stride = static_cast<int64_t>(a.KM) * a.C * 2;  // floats between consecutive h
+  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
+  const float* __restrict__ xin = a.x + base;
+  float* __restrict__ yout = a.y + base;
+  using P0 = HPass<R0, L, 1, 0>;
+  using P1 = HPass<R1, L, R0, 0>;
+
+  // ---------------- forward FFT_H: pass 0 straight from global
+  {
+    float2 v[P0::Q][R0];
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
+      const int bc = ok ? bb : 0;
+      const int t = bc % kBS, j = bc / kBS;
+#pragma unroll
+      for (int r = 0; r < R0; ++r) v[q][r] = *reinterpret_cast<const float2*>(xin + (j + r * P0::LR) * row_stride + 2 * t);
+    }
+    h_twiddle_dft<R0, L, 1, 0, P0::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) lds[(j * R0 + r) * kBS + t] = v[q][r];
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> A (bf16, [h][re 0..95 | im 96..191])
+  {
+    float2 v[P1::Q][R1];
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[q][r] = lds[(j + r * P1::LR) * kBS + t];
+      }
+    }
+    __syncthreads();
+    h_twiddle_dft<R1, L, R0, 0, P1::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int t = bb % kBS, j = bb / kBS;  // last pass: outputs at n = j + r * R0
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          const int n = j + r * R0;
+          A[n * kAPitch + t] = f2bf16(v[q][r].x);
+          A[n * kAPitch + kBS + t] = f2bf16(v[q][r].y);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- GEMM1 + bias + ReLU -> H1 (bf16, in place of A)
+  const int lane = tid & 63, w = tid >> 6;
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * kK * kK;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * kK * kK;
+  const float* b1 = a.b1 + blk * kK;
+  const float* b2 = a.b2 + blk * kK;
+  f32x4 acc[6][3];
+  gemm_96x192(A, w1t, acc);
+  __syncthreads();
+#pragma unroll
+  for (int nj = 0; nj < 3; ++nj) {
+    const int n = (3 * w + nj) * 16 + (lane & 15);
+    const float bias = b1[n];
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mi * 16 + 4 * (lane >> 4) + i;
+        A[m * kAPitch + n] = f2bf16(fmaxf(acc[mi][nj][i] + bias, 0.f));
+      }
+  }
+  __syncthreads();
+  // ---------------- GEMM2 + bias + softshrink -> X (fp32 complex, conjugated for the inverse)
+  gemm_96x192(A, w2t, acc);
+  __syncthreads();
+  float* X = reinterpret_cast<float*>(lds);
+  const float lam = a.lambda;
+#pragma unroll
+  for (int nj = 0; nj < 3; ++nj) {
+    const int n = (3 * w + nj) * 16 + (lane & 15);
+    const float bias = b2[n];
+    const int c = n < kBS ? n : n - kBS;
+    const int part = n < kBS ? 0 : 1;
+    const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mi * 16 + 4 * (lane >> 4) + i;
+        if (m < L) {
+          const float v = acc[mi][nj][i] + bias;
+          const float s = v > lam ? v - lam : (v < -lam ? v + lam : 0.f);
+          X[(m * kBS + c) * 2 + part] = sgn * s;
+        }
+      }
+  }
+  __syncthreads();
+  // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
+  {
+    float2 v[P0::Q][R0];
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) v[q][r] = lds[(j + r * P0::LR) * kBS + t];
+      }
+    }
+    __syncthreads();
+    h_twiddle_dft<R0, L, 1, 0, P0::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) lds[(j * R0 + r) * kBS + t] = v[q][r];
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> global (conj back)
+  {
+    float2 v[P1::Q][R1];
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[q][r] = lds[(j + r * P1::LR) * kBS + t];
+      }
+    }
+    h_twiddle_dft<R1, L, R0, 0, P1::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int t = bb % kBS, j = bb / kBS;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          const int n = j + r * R0;
+          *reinterpret_cast<float2*>(yout + n * row_stride + 2 * t) = make_float2(v[q][r].x, -v[q][r].y);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool afno_spectral_supported(int H, int block_size) { return H == 90 && block_size == kBS; }
+
+int64_t afno_spectral_lds_bytes(int H) { return static_cast<int64_t>(H) * kBS * sizeof(float2); }
+
+void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
+  if (!afno_spectral_supported(p.H, p.C / p.NB)) throw std::runtime_error("amd_dft: afno_spectral: unsupported shape");
+  AfnoArgs a;
+  a.x = p.x;
+  a.y = p.y;
+  a.w1t = p.w1t;
+  a.w2t = p.w2t;
+  a.b1 = p.b1;
+  a.b2 = p.b2;
+  a.tw = static_cast<const float2*>(p.tw);
+  a.KM = p.KM;
+  a.C = p.C;
+  a.NB = p.NB;
+  a.H = p.H;
+  a.lambda = p.lambda;
+  const int64_t nblocks = static_cast<int64_t>(p.B) * p.KM * p.NB;
+  if (nblocks <= 0) return;
+  const size_t lds = static_cast<size_t>(afno_spectral_lds_bytes(p.H));
+  auto kern = afno_spectral_kernel<90, 9, 10>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     static_cast<int>(lds));
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
+  hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), lds, static_cast<hipStream_t>(stream), a);
+  e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft

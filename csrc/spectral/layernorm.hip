@@ -1,0 +1,133 @@
+// Row LayerNorm (FourCastNet LN1/LN2 over 768 channels), one wave per row.
+//
+// bf16 or fp32 I/O, fp32 statistics (two-pass over registers: mean, then centred variance),
+// 16-byte vector loads/stores (Guideline 13), wave-level shuffle reductions (64 lanes).
+// Optional fused residual: x_out = x + residual is written and normalised in the same pass
+// (saves a separate elementwise kernel and one read of x).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "spectral.h"
+
+namespace amd_dft {
+namespace {
+
+constexpr int kWaves = 4;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void unpack8(uint4 u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint32_t bfpack(float a, float b) {
+  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<__bf16>(a))) |
+         (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<__bf16>(b))) << 16);
+}
+
+// NCH = 16-byte chunks (8 bf16) per lane, cols <= 64 * 8 * NCH
+template <int NCH, bool RES>
+__global__ void __launch_bounds__(64 * kWaves) ln_bf16_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                              const uint16_t* __restrict__ g, const uint16_t* __restrict__ b,
+                                                              const uint16_t* __restrict__ res, uint16_t* __restrict__ xo,
+                                                              int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nchunk = cols >> 3;
+  const uint16_t* xr = x + row * cols;
+  float v[NCH][8];
+  bool ok[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + 64 * c;
+    ok[c] = ch < nchunk;
+    const int chc = ok[c] ? ch : 0;
+    unpack8(*reinterpret_cast<const uint4*>(xr + chc * 8), v[c]);
+    if constexpr (RES) {
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(res + row * cols + chc * 8), r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] += r[i];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += ok[c] ? v[c][i] : 0.f;
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[c][i] - mean;
+      q += ok[c] ? d * d : 0.f;
+    }
+  const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+  float gg[NCH][8], bb[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int chc = ok[c] ? lane + 64 * c : 0;
+    unpack8(*reinterpret_cast<const uint4*>(g + chc * 8), gg[c]);
+    unpack8(*reinterpret_cast<const uint4*>(b + chc * 8), bb[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!ok[c]) continue;
+    const int ch = lane + 64 * c;
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * gg[c][i] + bb[c][i];
+    *reinterpret_cast<uint4*>(y + row * cols + ch * 8) =
+        make_uint4(bfpack(o[0], o[1]), bfpack(o[2], o[3]), bfpack(o[4], o[5]), bfpack(o[6], o[7]));
+    if constexpr (RES) {
+      *reinterpret_cast<uint4*>(xo + row * cols + ch * 8) = make_uint4(
+          bfpack(v[c][0], v[c][1]), bfpack(v[c][2], v[c][3]), bfpack(v[c][4], v[c][5]), bfpack(v[c][6], v[c][7]));
+    }
+  }
+}
+
+template <int NCH>
+void launch_bf16(const LayerNormLaunch& p, hipStream_t st) {
+  const dim3 grid(static_cast<uint32_t>((p.rows + kWaves - 1) / kWaves));
+  const auto* x = static_cast<const uint16_t*>(p.x);
+  auto* y = static_cast<uint16_t*>(p.y);
+  const auto* g = static_cast<const uint16_t*>(p.gamma);
+  const auto* b = static_cast<const uint16_t*>(p.beta);
+  if (p.residual)
+    hipLaunchKernelGGL((ln_bf16_kernel<NCH, true>), grid, dim3(64 * kWaves), 0, st, x, y, g, b,
+                       static_cast<const uint16_t*>(p.residual), static_cast<uint16_t*>(p.resid_out), p.rows, p.cols,
+                       p.eps);
+  else
+    hipLaunchKernelGGL((ln_bf16_kernel<NCH, false>), grid, dim3(64 * kWaves), 0, st, x, y, g, b, nullptr, nullptr,
+                       p.rows, p.cols, p.eps);
+}
+
+}  // namespace
+
+void launch_layernorm(const LayerNormLaunch& p, void* stream) {
+  if (!p.bf16 || p.cols % 8 != 0 || p.cols > 64 * 8 * 4)
+    throw std::runtime_error("amd_dft: layernorm kernel supports bf16 rows with cols % 8 == 0 and cols <= 2048");
+  if (p.rows > static_cast<int64_t>(0x7fffffff) * kWaves) throw std::runtime_error("amd_dft: layernorm: too many rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nch = (p.cols / 8 + 63) / 64;
+  if (nch <= 1) launch_bf16<1>(p, st);
+  else if (nch == 2) launch_bf16<2>(p, st);
+  else launch_bf16<4>(p, st);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: layernorm launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft

@@ -1,0 +1,48 @@
+// Host interfaces of the fused spectral-layer kernels (no torch dependency).
+#pragma once
+
+#include <cstdint>
+
+namespace amd_dft {
+
+// ---- AFNO: fused FFT_H -> block-diagonal complex MLP (MFMA) -> softshrink -> IFFT_H
+struct AfnoLaunch {
+  const float* x;       // [B, H, KM, C, 2] fp32 (W-direction half spectrum, KM kept modes)
+  float* y;             // same shape
+  const uint16_t* w1t;  // [NB][2*BS][2*BS] bf16, real-block weight transposed ([n][k])
+  const uint16_t* w2t;
+  const float* b1;      // [NB][2*BS] = [b_re | b_im]
+  const float* b2;
+  const void* tw;       // FFT plan twiddles for length H
+  int B, H, KM, C, NB;
+  float lambda;
+};
+bool afno_spectral_supported(int H, int block_size);
+int64_t afno_spectral_lds_bytes(int H);
+void launch_afno_spectral(const AfnoLaunch& p, void* stream);
+
+// ---- FNO: per-mode complex channel mixing out[b,o,m] = sum_i x[b,i,m] * w[i,o,m]
+struct FnoMixLaunch {
+  const float* x;   // [B, Cin, M, 2] fp32 (M = kept modes, flattened)
+  const float* w;   // [Cin, Cout, M, 2] fp32
+  float* y;         // [B, Cout, M, 2] fp32
+  int B, Cin, Cout, M;
+};
+void launch_fno_mix(const FnoMixLaunch& p, void* stream);
+
+// ---- LayerNorm over the last dim (bf16/fp32 I/O, fp32 statistics)
+struct LayerNormLaunch {
+  const void* x;
+  void* y;
+  const void* gamma;
+  const void* beta;
+  const void* residual;  // optional: y = LN(x) ; x_out = x + residual written to resid_out
+  void* resid_out;
+  int64_t rows;
+  int cols;
+  float eps;
+  int bf16;  // 1: bf16 tensors, 0: fp32
+};
+void launch_layernorm(const LayerNormLaunch& p, void* stream);
+
+}  // namespace amd_dft

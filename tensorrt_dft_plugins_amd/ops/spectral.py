@@ -1,0 +1,111 @@
+"""Fused spectral-layer ops (FourCastNet AFNO, FNO) and fused LayerNorm.
+
+``afno_spectral_h`` runs the K5 kernel of SURVEY §2.5: FFT along H -> block-diagonal complex
+MLP on MFMA (bf16 operands, fp32 accumulation) -> softshrink -> inverse FFT along H, one
+launch, spectrum kept in LDS.  ``c2r_w_add`` is the W-direction C2R pass with the AFNO
+filter bias (and the block residual) fused into its store.
+"""
+from __future__ import annotations
+
+import math
+import weakref
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .._loader import load_plugins
+from . import dft as D
+
+__all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
+           "afno_block_amd", "fno_spectral_mix"]
+
+
+def _ops():
+    load_plugins()
+    return torch.ops.amd_dft
+
+
+_pack_cache: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _real_block(w: torch.Tensor) -> torch.Tensor:
+    """[2, NB, bs, bs] complex-as-pair weight -> [NB, 2bs(k), 2bs(n)] real form [[W0, W1], [-W1, W0]]."""
+    top = torch.cat([w[0], w[1]], dim=2)
+    bot = torch.cat([-w[1], w[0]], dim=2)
+    return torch.cat([top, bot], dim=1)
+
+
+def pack_afno_weights(w1, b1, w2, b2) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Pack AFNO2D parameters for the fused kernel: transposed real-block bf16 weights ([n][k])
+    and concatenated fp32 biases.  Cached per parameter tensor version (graph-capture safe once
+    warmed up)."""
+    key = w1
+    ver = (w1._version, b1._version, w2._version, b2._version, w1.device, w1.data_ptr())
+    hit = _pack_cache.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    with torch.no_grad():
+        w1t = _real_block(w1.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
+        w2t = _real_block(w2.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
+        b1p = torch.cat([b1[0], b1[1]], dim=1).float().contiguous()
+        b2p = torch.cat([b2[0], b2[1]], dim=1).float().contiguous()
+    packed = (w1t, w2t, b1p, b2p)
+    _pack_cache[key] = (ver, packed)
+    return packed
+
+
+def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:
+    if not x.is_cuda:
+        return False
+    B, H, W, C = x.shape
+    return bool(_ops().afno_spectral_supported(H, C // num_blocks))
+
+
+def afno_spectral_h(xw: torch.Tensor, w1, b1, w2, b2, num_blocks: int, lam: float) -> torch.Tensor:
+    w1t, w2t, b1p, b2p = pack_afno_weights(w1, b1, w2, b2)
+    return _ops().afno_spectral(xw, w1t, w2t, b1p, b2p, float(lam))
+
+
+def c2r_w_add(yw: torch.Tensor, x: torch.Tensor, W: int, scale: float,
+              residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = scale * irfft_W(yw) + x (+ residual), with yw = [B, H, km, C, 2] (km stored modes)."""
+    km = yw.shape[2]
+    return _ops().c2r_add(yw, [2], [W], scale, [km, 0], x.contiguous(),
+                          None if residual is None else residual.contiguous(), x.dtype)
+
+
+def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm, residual: Optional[torch.Tensor] = None):
+    """Fused (x + residual) -> LayerNorm.  Returns (normed, x + residual)."""
+    return _ops().layer_norm(x, ln.weight, ln.bias, ln.eps, residual)
+
+
+def afno_block_amd(blk, x: torch.Tensor) -> torch.Tensor:
+    """One FourCastNet block on the MI355X path (bf16 activations)."""
+    from ..models.afno import afno2d_amd
+
+    f = blk.filter
+    c = f.cfg
+    h, _ = layer_norm(x, blk.norm1)
+    # filter(LN1(x)) + LN1(x) [AFNO bias] + x [double skip], all fused into the C2R store
+    x = afno2d_amd(h, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, c.hard_thresholding_fraction,
+                   residual=x)
+    y, _ = layer_norm(x, blk.norm2)
+    m = blk.mlp
+    B, H, W, C = y.shape
+    y2 = y.reshape(-1, C)
+    hid = F.gelu(F.linear(y2, m.fc1.weight, m.fc1.bias))
+    out = torch.addmm(x.reshape(-1, C), hid, m.fc2.weight.t()) if m.fc2.bias is None else \
+        torch.addmm(x.reshape(-1, C), hid, m.fc2.weight.t()).add_(m.fc2.bias)
+    return out.reshape(B, H, W, C)
+
+
+def fno_spectral_mix(xm: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """FNO mode mixing out[b,o,m] = sum_i x[b,i,m] w[i,o,m] on complex-as-pair tensors
+    xm [B, Cin, M, 2], w [Cin, Cout, M, 2] -> [B, Cout, M, 2] (fp32)."""
+    ops = _ops()
+    if xm.is_cuda and hasattr(ops, "fno_mix"):
+        return ops.fno_mix(xm.contiguous(), w.contiguous())
+    xc = torch.view_as_complex(xm.float().contiguous())
+    wc = torch.view_as_complex(w.float().contiguous())
+    return torch.view_as_real(torch.einsum("bim,iom->bom", xc, wc)).contiguous()

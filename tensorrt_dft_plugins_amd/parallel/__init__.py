@@ -1,0 +1,2 @@
+"""Parallelism: batch data-parallel inference over RCCL (xGMI) / Gloo."""
+from .dp import DataParallelInference, all_gather_batch, init_distributed, world_info  # noqa: F401

@@ -1,0 +1,120 @@
+"""Batch data-parallel inference over RCCL (torch.distributed backend "nccl") / Gloo.
+
+One process per GPU.  Each rank replays its own hipGraph-captured forward on
+its batch shard; the per-step outputs are all-gathered over xGMI (RCCL
+``all_gather_into_tensor``) on a dedicated communication stream, overlapped with the next
+step's compute: two captured graphs write two output buffers (shared memory pool), and a
+buffer is only overwritten after the collective that reads it has completed (stream-ordered
+``work.wait()``, no host sync).  The reference has no parallelism at all
+(/root/reference/src/dft_plugins/dft_plugins.cpp:341, "assuming single GPU").
+"""
+from __future__ import annotations
+
+import os
+from datetime import timedelta
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..engine.capture import CapturedModule
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> tuple[int, int, int]:
+    """Initialise the default process group from torchrun env vars; returns (rank, world, local_rank).
+
+    backend: "nccl" (= RCCL on ROCm) when a GPU is present, else "gloo".
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s), device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s))
+    return rank, world, local
+
+
+def world_info() -> tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False):
+    """Gather per-rank batch shards along dim 0 (RCCL all_gather_into_tensor; list form on Gloo)."""
+    rank, world = world_info()
+    if world == 1:
+        if out is not None:
+            out.copy_(x)
+            return out if not async_op else (out, None)
+        return (x, None) if async_op else x
+    if out is None:
+        out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    if dist.get_backend() == "gloo":
+        parts = list(out.chunk(world, 0))
+        w = dist.all_gather(parts, x.contiguous(), async_op=async_op)
+    else:
+        w = dist.all_gather_into_tensor(out, x.contiguous(), async_op=async_op)
+    return (out, w) if async_op else out
+
+
+class DataParallelInference:
+    """Overlapped batch-DP inference of a static-shape module (per-rank shard = ``example``)."""
+
+    def __init__(self, module: torch.nn.Module, example: torch.Tensor, *, gather: bool = True,
+                 use_graph: bool = True, warmup: int = 2):
+        self.rank, self.world = world_info()
+        self.gather = gather and self.world > 1
+        self.cap = CapturedModule(module, [example], warmup=warmup, n_graphs=2 if self.gather else 1,
+                                  use_graph=use_graph)
+        self.device = example.device
+        self.cuda = self.device.type == "cuda"
+        self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.full: List[Optional[torch.Tensor]] = [None, None]
+        self.works: List[Optional[object]] = [None, None]
+        self.events = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
+        if self.gather:
+            o = self.cap.outputs[0][0]
+            for i in range(2):
+                self.full[i] = torch.empty((self.world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
+                                           device=o.device)
+        self.k = 0
+
+    @property
+    def inputs(self) -> torch.Tensor:
+        return self.cap.inputs[0]
+
+    def step(self) -> torch.Tensor:
+        """Enqueue one step; returns the (eventually) gathered output buffer of this step."""
+        i = self.k % len(self.cap.outputs)
+        self.k += 1
+        if self.gather and self.works[i] is not None:
+            self.works[i].wait()  # stream-ordered: compute waits until the old gather read out[i]
+            self.works[i] = None
+        out = self.cap.replay(i)[0]
+        if not self.gather:
+            return out
+        if self.cuda:
+            self.events[i].record()
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(self.events[i])
+                _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
+        else:
+            _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
+        return self.full[i]
+
+    def drain(self) -> None:
+        """Make the current stream wait for all outstanding gathers."""
+        for i, w in enumerate(self.works):
+            if w is not None:
+                w.wait()
+                self.works[i] = None
+        if self.cuda:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)

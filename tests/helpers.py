@@ -1,12 +1,18 @@
 import torch
 
 
+def _as_f64(t: torch.Tensor) -> torch.Tensor:
+    t = t.detach().to("cpu")
+    if t.is_complex():
+        return torch.view_as_real(t.to(torch.complex128))
+    return t.to(torch.float64)
+
+
 def rel_l2(a: torch.Tensor, b: torch.Tensor) -> float:
-    a = a.detach().to("cpu", torch.float64)
-    b = b.detach().to("cpu", torch.float64)
-    if a.is_complex() or b.is_complex():
-        a = torch.view_as_real(a.to(torch.complex128)) if a.is_complex() else a
-        b = torch.view_as_real(b.to(torch.complex128)) if b.is_complex() else b
+    """Relative L2 error ||a - b|| / ||b|| (complex tensors compared as (re, im) pairs)."""
+    a, b = _as_f64(a), _as_f64(b)
+    if a.shape != b.shape and a.shape[:-1] == b.shape and a.shape[-1] == 2:
+        b = torch.stack([b, torch.zeros_like(b)], -1)
     den = b.norm().item()
     num = (a - b).norm().item()
     return num / den if den > 0 else num

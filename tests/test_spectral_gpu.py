@@ -1,0 +1,113 @@
+"""GPU tier: fused spectral kernels (AFNO K5, LayerNorm, C2R+add) vs PyTorch fp32 references,
+and the FourCastNet model on the MI355X path vs the FourCastNet reference forward."""
+import pytest
+import torch
+
+from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+from tensorrt_dft_plugins_amd.models.afno import afno2d_amd, afno2d_reference
+from tensorrt_dft_plugins_amd.ops import spectral as S
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _afno_params(nb, bs, scale=0.02, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    w1 = scale * torch.randn(2, nb, bs, bs, generator=g)
+    w2 = scale * torch.randn(2, nb, bs, bs, generator=g)
+    b1 = scale * torch.randn(2, nb, bs, generator=g)
+    b2 = scale * torch.randn(2, nb, bs, generator=g)
+    return w1, b1, w2, b2
+
+
+def test_afno_spectral_kernel_vs_cpu(device):
+    torch.manual_seed(0)
+    B, H, KM, C, nb = 2, 90, 46, 768, 8
+    xw = torch.randn(B, H, KM, C, 2)
+    w1, b1, w2, b2 = _afno_params(nb, C // nb, scale=0.05)
+    w1t, w2t, b1p, b2p = S.pack_afno_weights(w1, b1, w2, b2)
+    ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)  # CPU: fp32 math
+    out = torch.ops.amd_dft.afno_spectral(xw.to(device), w1t.to(device), w2t.to(device), b1p.to(device),
+                                          b2p.to(device), 0.01)
+    assert rel_l2(out, ref) < 1.5e-2  # bf16 MFMA operands, fp32 accumulation
+
+
+def test_afno_spectral_kernel_exact_weights(device):
+    """Identity-like weights (exact in bf16) + integer-valued spectra: the fused kernel must
+    reproduce FFT -> ReLU(x) -> IFFT structure up to fp32 rounding (layout check with asymmetric data)."""
+    B, H, KM, C, nb = 1, 90, 2, 768, 8
+    bs = C // nb
+    w1 = torch.zeros(2, nb, bs, bs)
+    w1[0] = torch.eye(bs)
+    w2 = torch.zeros(2, nb, bs, bs)
+    w2[0] = torch.eye(bs) * 0.5
+    w2[1, :, 0, 1] = 0.25  # asymmetric imaginary coupling
+    b1 = torch.zeros(2, nb, bs)
+    b2 = torch.zeros(2, nb, bs)
+    b2[0, :, 3] = 1.0
+    xw = torch.randint(-3, 4, (B, H, KM, C, 2)).float()
+    w1t, w2t, b1p, b2p = S.pack_afno_weights(w1, b1, w2, b2)
+    ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.0)
+    out = torch.ops.amd_dft.afno_spectral(xw.to(device), w1t.to(device), w2t.to(device), b1p.to(device),
+                                          b2p.to(device), 0.0)
+    assert rel_l2(out, ref) < 5e-3
+
+
+def test_afno2d_amd_fused_vs_reference(device):
+    torch.manual_seed(1)
+    B, H, W, C, nb = 2, 90, 180, 768, 8
+    x = torch.randn(B, H, W, C)
+    w1, b1, w2, b2 = _afno_params(nb, C // nb, scale=0.05)
+    ref = afno2d_reference(x, w1, b1, w2, b2, nb, 0.01, 1.0)
+    xd = x.to(device)
+    out = afno2d_amd(xd, w1.to(device), b1.to(device), w2.to(device), b2.to(device), nb, 0.01, 1.0)
+    assert S.afno_fused_available(xd, nb)
+    assert rel_l2(out, ref) < 1e-2
+    # bf16 activations (model dtype)
+    outb = afno2d_amd(xd.to(torch.bfloat16), w1.to(device), b1.to(device), w2.to(device), b2.to(device), nb, 0.01, 1.0)
+    assert outb.dtype == torch.bfloat16
+    assert rel_l2(outb.float(), ref) < 2e-2
+
+
+def test_layernorm_kernel(device):
+    torch.manual_seed(2)
+    x = torch.randn(1000, 768, device=device).to(torch.bfloat16)
+    r = torch.randn(1000, 768, device=device).to(torch.bfloat16)
+    ln = torch.nn.LayerNorm(768, eps=1e-6).to(device).to(torch.bfloat16)
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(768) * 0.5 + 1)
+        ln.bias.copy_(torch.randn(768) * 0.1)
+    y, xs = S.layer_norm(x, ln)
+    ref = torch.nn.functional.layer_norm(x.float(), (768,), ln.weight.float(), ln.bias.float(), 1e-6)
+    assert rel_l2(y.float(), ref) < 8e-3
+    y2, xs2 = S.layer_norm(x, ln, r)
+    s = (x.float() + r.float())
+    assert rel_l2(xs2.float(), s) < 4e-3
+    assert rel_l2(y2.float(), torch.nn.functional.layer_norm(s, (768,), ln.weight.float(), ln.bias.float(), 1e-6)) < 8e-3
+
+
+def test_c2r_add_kernel(device):
+    torch.manual_seed(3)
+    yw = torch.randn(2, 90, 46, 64, 2, device=device)
+    x = torch.randn(2, 90, 180, 64, device=device)
+    r = torch.randn(2, 90, 180, 64, device=device)
+    out = S.c2r_w_add(yw, x, 180, 0.5, r)
+    full = torch.zeros(2, 90, 91, 64, dtype=torch.complex128)
+    full[:, :, :46] = torch.view_as_complex(yw.cpu().double())
+    ref = 0.5 * torch.fft.irfft(full, n=180, dim=2, norm="forward") + x.cpu().double() + r.cpu().double()
+    assert rel_l2(out, ref) < 5e-6
+
+
+@pytest.mark.parametrize("depth", [2])
+def test_fourcastnet_amd_vs_reference(device, depth):
+    torch.manual_seed(4)
+    cfg = AFNOConfig(depth=depth)
+    m = AFNONet(cfg, backend="torch").to(device).eval()
+    x = torch.randn(1, cfg.in_chans, *cfg.img_size, device=device)
+    with torch.no_grad():
+        ref = m(x)
+        out = m.set_backend("amd")(x)
+        mb = m.to(torch.bfloat16)
+        outb = mb(x.to(torch.bfloat16))
+    assert rel_l2(out, ref) < 1e-2
+    assert rel_l2(outb.float(), ref) < 5e-2
