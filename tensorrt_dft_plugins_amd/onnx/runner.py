@@ -74,13 +74,32 @@ def _ints(x) -> List[int]:
     return [int(v) for v in x]
 
 
+_DEV_CONSTS: Dict[tuple, torch.Tensor] = {}
+
+
+def _to_dev(t: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """Host value -> device.  0-dim host tensors stay on the host (PyTorch treats them as
+    scalars, no copy); small host tensors are memoised by value so the copy happens during
+    warm-up and never inside hipGraph capture."""
+    if t.dim() == 0:
+        return t
+    if t.numel() <= 4096:
+        key = (str(device), t.dtype, tuple(t.shape), tuple(t.reshape(-1).tolist()))
+        v = _DEV_CONSTS.get(key)
+        if v is None:
+            v = t.to(device)
+            _DEV_CONSTS[key] = v
+        return v
+    return t.to(device)
+
+
 def _align(a, b):
     """Put host scalars/tensors next to device tensors for arithmetic."""
     if isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and a.device != b.device:
         if _is_host(a):
-            a = a.to(b.device)
+            a = _to_dev(a, b.device)
         else:
-            b = b.to(a.device)
+            b = _to_dev(b, a.device)
     return a, b
 
 
@@ -144,7 +163,7 @@ def _clip(attrs, x, lo=None, hi=None):
 def _where(attrs, c, a, b):
     dev = next((t.device for t in (c, a, b) if isinstance(t, torch.Tensor) and not _is_host(t)), None)
     if dev is not None:
-        c, a, b = (t.to(dev) if isinstance(t, torch.Tensor) else t for t in (c, a, b))
+        c, a, b = (_to_dev(t, dev) if isinstance(t, torch.Tensor) and _is_host(t) else t for t in (c, a, b))
     return torch.where(c, a, b)
 
 
@@ -309,7 +328,7 @@ def _concat(attrs, *xs):
     xs = [x for x in xs if not (isinstance(x, torch.Tensor) and x.numel() == 0 and x.dim() == 1)] or list(xs)
     dev = next((x.device for x in xs if not _is_host(x)), None)
     if dev is not None:
-        xs = [x.to(dev) for x in xs]
+        xs = [_to_dev(x, dev) if _is_host(x) else x for x in xs]
     return torch.cat(xs, attrs.get("axis", 0))
 
 
@@ -344,9 +363,9 @@ def _slice(attrs, x, starts=None, ends=None, axes=None, steps=None):
 def _gather(attrs, x, idx):
     axis = attrs.get("axis", 0) % x.dim()
     if _is_host(idx) and not _is_host(x):
-        idx = idx.to(x.device)
+        idx = _to_dev(idx, x.device) if idx.dim() else idx.reshape(1).to(x.device)
     if _is_host(x) and not _is_host(idx):
-        x = x.to(idx.device)
+        x = _to_dev(x, idx.device)
     n = x.shape[axis]
     idx = torch.where(idx < 0, idx + n, idx)
     out = torch.index_select(x, axis, idx.reshape(-1))
@@ -504,7 +523,7 @@ class OnnxGraph:
         for o in self.output_names:
             v = env[o]
             if _is_host(v) and self.device.type != "cpu":
-                v = v.to(self.device)
+                v = _to_dev(v, self.device) if v.dim() else _to_dev(v.reshape(1), self.device).reshape(())
             out.append(v)
         return out
 

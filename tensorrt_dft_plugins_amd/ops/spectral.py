@@ -8,7 +8,6 @@ filter bias (and the block residual) fused into its store.
 from __future__ import annotations
 
 import math
-import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -26,7 +25,7 @@ def _ops():
     return torch.ops.amd_dft
 
 
-_pack_cache: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_pack_cache: dict = {}
 
 
 def _real_block(w: torch.Tensor) -> torch.Tensor:
@@ -40,18 +39,19 @@ def pack_afno_weights(w1, b1, w2, b2) -> Tuple[torch.Tensor, torch.Tensor, torch
     """Pack AFNO2D parameters for the fused kernel: transposed real-block bf16 weights ([n][k])
     and concatenated fp32 biases.  Cached per parameter tensor version (graph-capture safe once
     warmed up)."""
-    key = w1
-    ver = (w1._version, b1._version, w2._version, b2._version, w1.device, w1.data_ptr())
+    key = tuple((id(t), t.data_ptr(), t._version, str(t.device), t.dtype) for t in (w1, b1, w2, b2))
     hit = _pack_cache.get(key)
-    if hit is not None and hit[0] == ver:
-        return hit[1]
+    if hit is not None:
+        return hit
     with torch.no_grad():
         w1t = _real_block(w1.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
         w2t = _real_block(w2.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
         b1p = torch.cat([b1[0], b1[1]], dim=1).float().contiguous()
         b2p = torch.cat([b2[0], b2[1]], dim=1).float().contiguous()
     packed = (w1t, w2t, b1p, b2p)
-    _pack_cache[key] = (ver, packed)
+    if len(_pack_cache) > 256:
+        _pack_cache.clear()
+    _pack_cache[key] = packed
     return packed
 
 
