@@ -89,6 +89,19 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
   a.bf16_in = d.tin == DType::BF16; a.bf16_out = d.tout == DType::BF16;
   a.add1 = d.add1;
   a.add2 = d.add2;
+  {
+    // paired-vector IO: the two real signals of a complex FFT are adjacent (and 2 scalars
+    // apart on the complex side), I even, and every pair offset suitably aligned
+    const int64_t rin = d.kind == Kind::R2C ? 1 : 2, rout = d.kind == Kind::C2R ? 1 : 2;
+    const int esi = a.bf16_in ? 2 : 4, eso = a.bf16_out ? 2 : 4;
+    const uintptr_t pin = reinterpret_cast<uintptr_t>(d.in), pout = reinterpret_cast<uintptr_t>(d.out);
+    bool pv = d.kind != Kind::C2C && d.I % 2 == 0 && d.Si_in == rin && d.Si_out == rout;
+    pv = pv && d.Sn_in % (2 * rin) == 0 && d.So_in % (2 * rin) == 0 && pin % (2 * rin * esi) == 0;
+    pv = pv && d.Sn_out % (2 * rout) == 0 && d.So_out % (2 * rout) == 0 && pout % (2 * rout * eso) == 0;
+    for (const void* ad : {d.add1, d.add2})
+      pv = pv && (ad == nullptr || reinterpret_cast<uintptr_t>(ad) % (2 * rout * eso) == 0);
+    a.pairvec = pv ? 1 : 0;
+  }
   const int64_t nblocks = d.O * a.tiles_per_outer;
   if (nblocks <= 0) return true;
   if (nblocks > 0x7fffffffLL) throw std::runtime_error("amd_dft: FFT grid too large");

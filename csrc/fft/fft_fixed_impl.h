@@ -32,6 +32,7 @@ struct FixedArgs {
   int32_t inverse, vec_in, vec_out, bf16_in, bf16_out;
   const void* add1;  // C2R epilogue: out = scale * irfft + add1 (+ add2); same layout/dtype as out
   const void* add2;
+  int32_t pairvec;   // paired real signals adjacent in memory (channel-last) and I even
 };
 
 template <int... Rs>
@@ -92,6 +93,16 @@ __device__ __forceinline__ void st_c2(void* p, int32_t off, float2 a, float2 b) 
     *reinterpret_cast<float4*>(static_cast<float*>(p) + off) = make_float4(a.x, a.y, b.x, b.y);
   }
 }
+template <bool BF>
+__device__ __forceinline__ float4 ld_c2(const void* p, int32_t off) {  // two adjacent complex values
+  if constexpr (BF) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + off);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + off);
+  }
+}
 __device__ __forceinline__ float2 sel(bool ok, float2 v) { return make_float2(ok ? v.x : 0.f, ok ? v.y : 0.f); }
 
 struct Ctx {
@@ -118,7 +129,7 @@ __device__ __forceinline__ int lidx(const Ctx& x, int n) {
 // First-pass element fetch (includes the C2R Hermitian assembly and input pruning).
 // Every load is unconditional from a clamped (valid) address and masked afterwards with a
 // select: a branch around a load makes hipcc wait vmcnt(0) per element.
-template <Kind K, int L, bool BF, bool PR>
+template <Kind K, int L, bool BF, bool PR, bool PV>
 __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
   const FixedArgs& a = x.a;
   float2 z;
@@ -132,16 +143,27 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
     }
     if (a.inverse) z.y = -z.y;
   } else if constexpr (K == Kind::R2C) {
-    const float va = ld_r<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in);
-    const float vb = ld_r<BF>(x.in, x.i1c * a.Si_in + n * a.Sn_in);
-    z = make_float2(x.ok0 ? va : 0.f, x.ok1 ? vb : 0.f);
+    if constexpr (PV) {  // the two packed real signals are adjacent: one vector load
+      z = sel(x.ok0, ld_c<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in));
+    } else {
+      const float va = ld_r<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in);
+      const float vb = ld_r<BF>(x.in, x.i1c * a.Si_in + n * a.Sn_in);
+      z = make_float2(x.ok0 ? va : 0.f, x.ok1 ? vb : 0.f);
+    }
   } else {
     const bool upper = 2 * n > L;
     const int kk = upper ? L - n : n;
     const bool okk = kk < a.in_lo;
     const int kc = okk ? kk : 0;
-    float2 A = sel(okk && x.ok0, ld_c<BF>(x.in, x.i0c * a.Si_in + kc * a.Sn_in));
-    float2 B = sel(okk && x.ok1, ld_c<BF>(x.in, x.i1c * a.Si_in + kc * a.Sn_in));
+    float2 A, B;
+    if constexpr (PV) {
+      const float4 ab = ld_c2<BF>(x.in, x.i0c * a.Si_in + kc * a.Sn_in);
+      A = sel(okk && x.ok0, make_float2(ab.x, ab.y));
+      B = sel(okk && x.ok0, make_float2(ab.z, ab.w));
+    } else {
+      A = sel(okk && x.ok0, ld_c<BF>(x.in, x.i0c * a.Si_in + kc * a.Sn_in));
+      B = sel(okk && x.ok1, ld_c<BF>(x.in, x.i1c * a.Si_in + kc * a.Sn_in));
+    }
     if (kk == 0 || 2 * kk == L) { A.y = 0.f; B.y = 0.f; }
     if (upper) { A.y = -A.y; B.y = -B.y; }
     z = make_float2(A.x - B.y, A.y + B.x);
@@ -151,8 +173,10 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
 }
 
 // Last-pass element store (C2C / C2R), with output pruning and the fused scale.
-template <Kind K, int L, bool BF, bool PR, int NADD>
-__device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v) {
+// Last-pass element store (C2C / C2R), with output pruning, the fused scale and (C2R) the
+// pre-loaded addend pair `ad` (add1 + add2 at this element, zero when NADD == 0).
+template <Kind K, int L, bool BF, bool PR, bool PV>
+__device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v, float2 ad) {
   const FixedArgs& a = x.a;
   if constexpr (K == Kind::C2C) {
     if (a.inverse) v.y = -v.y;
@@ -163,21 +187,42 @@ __device__ __forceinline__ void scatter(const Ctx& x, int n, float2 v) {
       if (x.ok0) st_c<BF>(x.out, x.c * a.Si_out + n * a.Sn_out, make_float2(v.x * a.scale, v.y * a.scale));
     }
   } else {
-    float va = v.x * a.scale;
-    float vb = (a.inverse ? -v.y : v.y) * a.scale;
+    const float va = v.x * a.scale + ad.x;
+    const float vb = (a.inverse ? -v.y : v.y) * a.scale + ad.y;
+    const int32_t off = x.i0c * a.Si_out + n * a.Sn_out;
+    if constexpr (PV) {
+      if (x.ok0) st_c<BF>(x.out, off, make_float2(va, vb));
+    } else {
+      if (x.ok0) st_r<BF>(x.out, off, va);
+      if (x.ok1) st_r<BF>(x.out, x.i1c * a.Si_out + n * a.Sn_out, vb);
+    }
+  }
+}
+
+// C2R addends of one output element (both packed signals), summed.
+template <int NADD, bool BF, bool PV>
+__device__ __forceinline__ float2 load_addend(const Ctx& x, int n) {
+  float2 r = make_float2(0.f, 0.f);
+  if constexpr (NADD > 0) {
+    const FixedArgs& a = x.a;
     const int32_t off = x.i0c * a.Si_out + n * a.Sn_out;
     const int32_t offb = x.i1c * a.Si_out + n * a.Sn_out;
-    if constexpr (NADD >= 1) {
-      va += ld_r<BF>(x.add1, off);
-      vb += ld_r<BF>(x.add1, offb);
+    if constexpr (PV) {
+      r = ld_c<BF>(x.add1, off);
+      if constexpr (NADD >= 2) {
+        const float2 t = ld_c<BF>(x.add2, off);
+        r.x += t.x;
+        r.y += t.y;
+      }
+    } else {
+      r = make_float2(ld_r<BF>(x.add1, off), ld_r<BF>(x.add1, offb));
+      if constexpr (NADD >= 2) {
+        r.x += ld_r<BF>(x.add2, off);
+        r.y += ld_r<BF>(x.add2, offb);
+      }
     }
-    if constexpr (NADD >= 2) {
-      va += ld_r<BF>(x.add2, off);
-      vb += ld_r<BF>(x.add2, offb);
-    }
-    if (x.ok0) st_r<BF>(x.out, off, va);
-    if (x.ok1) st_r<BF>(x.out, offb, vb);
   }
+  return r;
 }
 
 template <class F, int TP, int P>
@@ -207,7 +252,7 @@ __device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, T
   }
 }
 
-template <Kind K, bool COLS, int TP, int T, class F, int P, bool BFI, bool BFO, bool PR, int NADD>
+template <Kind K, bool COLS, int TP, int T, class F, int P, bool BFI, bool BFO, bool PR, int NADD, bool PV>
 struct Step {
   using G = PassGeom<F, TP, P>;
   static constexpr int NP = F::N;
@@ -222,7 +267,7 @@ struct Step {
       float2 twn[GN::Q][GN::TWR];
       load_tw<F, TP, P + 1>(x, twn);
       body(x, tw);
-      Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR, NADD>::run(x, twn);
+      Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR, NADD, PV>::run(x, twn);
     } else {
       body(x, tw);
     }
@@ -231,6 +276,18 @@ struct Step {
   __device__ __forceinline__ static void body(const Ctx& x, float2 (&tw)[G::Q][G::TWR]) {
     constexpr int R = G::R, LR = G::LR, Q = G::Q, Ns = G::Ns;
     float2 v[Q][R];
+    // C2R epilogue addends: issued before this pass' gather so their latency hides under it
+    constexpr bool ADDS = LAST && K == Kind::C2R && NADD > 0;
+    float2 addv[ADDS ? Q : 1][ADDS ? R : 1];
+    if constexpr (ADDS) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int jr = x.tp + q * TP;
+        const int j = (G::EXACT || jr < LR) ? jr : 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) addv[q][r] = load_addend<NADD, BFO, PV>(x, j + r * Ns);
+      }
+    }
     // ---- gather
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -238,7 +295,7 @@ struct Step {
       if (G::EXACT || j < LR) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if constexpr (P == 0) v[q][r] = gather<K, L, BFI, PR>(x, j + r * LR);
+          if constexpr (P == 0) v[q][r] = gather<K, L, BFI, PR, PV>(x, j + r * LR);
           else v[q][r] = x.lds[lidx<COLS, T, L>(x, j + r * LR)];
         }
       }
@@ -263,7 +320,10 @@ struct Step {
         const int j = x.tp + q * TP;
         if (G::EXACT || j < LR) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) scatter<K, L, BFO, PR, NADD>(x, j + r * Ns, v[q][r]);
+          for (int r = 0; r < R; ++r) {
+            if constexpr (ADDS) scatter<K, L, BFO, PR, PV>(x, j + r * Ns, v[q][r], addv[q][r]);
+            else scatter<K, L, BFO, PR, PV>(x, j + r * Ns, v[q][r], make_float2(0.f, 0.f));
+          }
         }
       }
     } else {
@@ -282,7 +342,7 @@ struct Step {
   }
 };
 
-template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD>
+template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>
 __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   constexpr int L = F::L;
   constexpr int LDSN = COLS ? lds_pad(L * T) + 2 : T * (lds_pad(L) + 1);
@@ -301,8 +361,13 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   } else {
     x.ok0 = 2 * x.c < a.I;
     x.ok1 = 2 * x.c + 1 < a.I;
-    x.i0c = x.ok0 ? 2 * x.c : a.I - 1;
-    x.i1c = x.ok1 ? 2 * x.c + 1 : a.I - 1;
+    if constexpr (PV) {  // I even (host-checked): clamp to the last complete pair
+      x.i0c = x.ok0 ? 2 * x.c : a.I - 2;
+      x.i1c = x.i0c + 1;
+    } else {
+      x.i0c = x.ok0 ? 2 * x.c : a.I - 1;
+      x.i1c = x.ok1 ? 2 * x.c + 1 : a.I - 1;
+    }
   }
   x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
   x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
@@ -311,7 +376,7 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   x.lds = lds;
   using G0 = PassGeom<F, TP, 0>;
   float2 tw0[G0::Q][G0::TWR];
-  Step<K, COLS, TP, T, F, 0, BFI, BFO, PR, NADD>::run(x, tw0);
+  Step<K, COLS, TP, T, F, 0, BFI, BFO, PR, NADD, PV>::run(x, tw0);
   if constexpr (K == Kind::R2C) {
     // Z (natural order) is in LDS: separate the two packed real signals' half spectra.
     constexpr int KMAX = L / 2 + 1;
@@ -327,8 +392,12 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
         float2 xb = make_float2((zk.y + zm.y) * h, (zm.x - zk.x) * h);
         if (a.inverse) { xa.y = -xa.y; xb.y = -xb.y; }
         const int32_t off = x.i0c * a.Si_out + k * a.Sn_out;
-        if (x.ok0) st_c<BFO>(x.out, off, xa);
-        if (x.ok1) st_c<BFO>(x.out, off + a.Si_out, xb);
+        if constexpr (PV) {
+          if (x.ok0) st_c2<BFO>(x.out, off, xa, xb);
+        } else {
+          if (x.ok0) st_c<BFO>(x.out, off, xa);
+          if (x.ok1) st_c<BFO>(x.out, x.i1c * a.Si_out + k * a.Sn_out, xb);
+        }
       }
     }
   }
@@ -349,31 +418,45 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)
 
-template <Kind K, bool COLS, int TP, int T, class F, bool PR, int NADD>
+template <Kind K, bool COLS, int TP, int T, class F, bool PR, int NADD, bool PV>
 void launch_dt(const FixedArgs& a, dim3 grid, hipStream_t st) {
   const dim3 blk(TP * T);
   if (a.bf16_in) {
-    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, PR, NADD>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, false, PR, NADD>), grid, blk, 0, st, a);
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, PR, NADD, PV>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, false, PR, NADD, PV>), grid, blk, 0, st, a);
   } else {
-    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, true, PR, NADD>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, PR, NADD>), grid, blk, 0, st, a);
+    if (a.bf16_out) hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, true, PR, NADD, PV>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, PR, NADD, PV>), grid, blk, 0, st, a);
   }
 }
 
 template <Kind K, bool COLS, int TP, int T, class F>
 void launch_one(const FixedArgs& a, dim3 grid, hipStream_t st) {
   // pruned C2C (FNO/AFNO mode windows) gets its own instantiation; R2C/C2R handle their
-  // (cheap, Hermitian) truncation in the common path.
+  // (cheap, Hermitian) truncation in the common path.  Column layouts (channel-last) get the
+  // paired-vector variant (PV) and the C2R addend epilogue (NADD).
   const bool pr = K == Kind::C2C && (a.in_lo + a.in_hi != F::L || a.out_lo + a.out_hi != F::L);
   if constexpr (K == Kind::C2C) {
-    if (pr) return launch_dt<K, COLS, TP, T, F, true, 0>(a, grid, st);
+    if (pr) return launch_dt<K, COLS, TP, T, F, true, 0, false>(a, grid, st);
   }
-  if constexpr (K == Kind::C2R) {
-    if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2>(a, grid, st);
-    if (a.add1) return launch_dt<K, COLS, TP, T, F, false, 1>(a, grid, st);
+  if constexpr (COLS && K != Kind::C2C) {
+    if (a.pairvec) {
+      if constexpr (K == Kind::C2R) {
+        if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2, true>(a, grid, st);
+        if (a.add1) return launch_dt<K, COLS, TP, T, F, false, 1, true>(a, grid, st);
+      }
+      return launch_dt<K, COLS, TP, T, F, false, 0, true>(a, grid, st);
+    }
+    if constexpr (K == Kind::C2R) {
+      if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2, false>(a, grid, st);
+      if (a.add1) return launch_dt<K, COLS, TP, T, F, false, 1, false>(a, grid, st);
+    }
   }
-  launch_dt<K, COLS, TP, T, F, false, 0>(a, grid, st);
+  if constexpr (!COLS && K == Kind::C2R) {
+    if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2, false>(a, grid, st);
+    if (a.add1) return launch_dt<K, COLS, TP, T, F, false, 1, false>(a, grid, st);
+  }
+  launch_dt<K, COLS, TP, T, F, false, 0, false>(a, grid, st);
 }
 
 using LaunchFn = void (*)(const FixedArgs&, dim3, hipStream_t);

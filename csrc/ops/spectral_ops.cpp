@@ -18,8 +18,9 @@ namespace {
 //   IFFT_H( softshrink( ReLU(FFT_H(x) W1' + b1') W2' + b2' ) )   (FFTs unnormalised)
 void check_afno(const at::Tensor& xw, const at::Tensor& w1t, const at::Tensor& w2t, const at::Tensor& b1,
                 const at::Tensor& b2) {
-  TORCH_CHECK(xw.dim() == 5 && xw.size(4) == 2 && xw.scalar_type() == at::kFloat,
-              "afno_spectral: x must be [B, H, KM, C, 2] float32");
+  TORCH_CHECK(xw.dim() == 5 && xw.size(4) == 2 &&
+                  (xw.scalar_type() == at::kFloat || xw.scalar_type() == at::kBFloat16),
+              "afno_spectral: x must be [B, H, KM, C, 2] float32 or bfloat16");
   const int64_t NB = w1t.size(0), K = w1t.size(1);
   TORCH_CHECK(w1t.dim() == 3 && w1t.size(2) == K && w2t.sizes() == w1t.sizes(), "afno_spectral: bad weight shapes");
   TORCH_CHECK(NB * K == 2 * xw.size(3), "afno_spectral: NB * 2 * block_size must equal 2 * C");
@@ -31,7 +32,7 @@ at::Tensor afno_spectral_cpu(const at::Tensor& xw, const at::Tensor& w1t, const 
   check_afno(xw, w1t, w2t, b1, b2);
   const int64_t B = xw.size(0), H = xw.size(1), KM = xw.size(2), C = xw.size(3);
   const int64_t NB = w1t.size(0), BS = C / NB;
-  at::Tensor X = at::fft_fft(at::view_as_complex(xw.contiguous()), std::nullopt, 1, "backward");
+  at::Tensor X = at::fft_fft(at::view_as_complex(xw.to(at::kFloat).contiguous()), std::nullopt, 1, "backward");
   at::Tensor Xr = at::view_as_real(X).reshape({B, H, KM, NB, BS, 2});
   at::Tensor A = at::cat({Xr.select(-1, 0), Xr.select(-1, 1)}, -1);  // [..., NB, 2BS]
   at::Tensor W1 = w1t.to(at::kFloat).transpose(1, 2);                // [NB, k, n]
@@ -41,7 +42,7 @@ at::Tensor afno_spectral_cpu(const at::Tensor& xw, const at::Tensor& w1t, const 
   O = at::softshrink(O, lam);
   at::Tensor Oc = at::complex(O.narrow(-1, 0, BS), O.narrow(-1, BS, BS)).reshape({B, H, KM, C});
   at::Tensor Y = at::fft_ifft(Oc, std::nullopt, 1, "forward");
-  return at::view_as_real(Y).contiguous();
+  return at::view_as_real(Y).to(xw.scalar_type()).contiguous();
 }
 
 at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, const at::Tensor& w2t_, const at::Tensor& b1_,
@@ -58,8 +59,9 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   if (xw.numel() == 0) return y;
   auto dp = get_plan(H, xw.device());
   AfnoLaunch p;
-  p.x = xw.data_ptr<float>();
-  p.y = y.data_ptr<float>();
+  p.x = xw.data_ptr();
+  p.y = y.data_ptr();
+  p.bf16_in = p.bf16_out = xw.scalar_type() == at::kBFloat16;
   p.w1t = reinterpret_cast<const uint16_t*>(w1t.data_ptr());
   p.w2t = reinterpret_cast<const uint16_t*>(w2t.data_ptr());
   p.b1 = b1.data_ptr<float>();

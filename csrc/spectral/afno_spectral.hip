@@ -33,6 +33,25 @@ constexpr int kAPitch = kK + 8;  // bf16 elements per A row (+16 B pad: ds_read_
 
 __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 
+template <bool BF>
+__device__ __forceinline__ float2 ldc(const void* p, int64_t off) {  // off in scalars
+  if constexpr (BF) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(p) + off);
+    return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float2*>(static_cast<const float*>(p) + off);
+  }
+}
+template <bool BF>
+__device__ __forceinline__ void stc(void* p, int64_t off, float2 v) {
+  if constexpr (BF) {
+    *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(p) + off) =
+        static_cast<uint32_t>(f2bf16(v.x)) | (static_cast<uint32_t>(f2bf16(v.y)) << 16);
+  } else {
+    *reinterpret_cast<float2*>(static_cast<float*>(p) + off) = v;
+  }
+}
+
 // Stockham pass over 96 interleaved signals in LDS (layout [n][96]) with register staging:
 // gather -> barrier -> twiddle/DFT -> scatter.  SRC_GLOBAL: pass 0 reads global memory.
 template <int R, int L, int Ns, int GOFF>
@@ -62,8 +81,8 @@ __device__ __forceinline__ void h_twiddle_dft(float2 (&v)[Q][R], const float2* _
 }
 
 struct AfnoArgs {
-  const float* x;       // [B, H, KM, C, 2]
-  float* y;             // [B, H, KM, C, 2]
+  const void* x;        // [B, H, KM, C, 2] fp32 or bf16
+  void* y;              // [B, H, KM, C, 2] fp32 or bf16
   const uint16_t* w1t;  // [NB][192][192] bf16, [n][k]
   const uint16_t* w2t;
   const float* b1;      // [NB][192]
@@ -106,7 +125,7 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
   }
 }
 
-template <int L, int R0, int R1>
+template <int L, int R0, int R1, bool BFI, bool BFO>
 __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a) {
   static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
   extern __shared__ __attribute__((aligned(16))) float2 lds[];  // [L][96] complex fp32 (69 KB at L=90)
@@ -118,8 +137,8 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
   const int b = bk / a.KM;
   const int64_t row_stride = static_cast<int64_t>(a.KM) * a.C * 2;  // floats between consecutive h
   const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
-  const float* __restrict__ xin = a.x + base;
-  float* __restrict__ yout = a.y + base;
+  const void* xin = static_cast<const char*>(a.x) + base * (BFI ? 2 : 4);
+  void* yout = static_cast<char*>(a.y) + base * (BFO ? 2 : 4);
   using P0 = HPass<R0, L, 1, 0>;
   using P1 = HPass<R1, L, R0, 0>;
 
@@ -133,7 +152,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       const int bc = ok ? bb : 0;
       const int t = bc % kBS, j = bc / kBS;
 #pragma unroll
-      for (int r = 0; r < R0; ++r) v[q][r] = *reinterpret_cast<const float2*>(xin + (j + r * P0::LR) * row_stride + 2 * t);
+      for (int r = 0; r < R0; ++r) v[q][r] = ldc<BFI>(xin, (j + r * P0::LR) * row_stride + 2 * t);
     }
     h_twiddle_dft<R0, L, 1, 0, P0::Q>(v, a.tw);
 #pragma unroll
@@ -269,7 +288,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          *reinterpret_cast<float2*>(yout + n * row_stride + 2 * t) = make_float2(v[q][r].x, -v[q][r].y);
+          stc<BFO>(yout, n * row_stride + 2 * t, make_float2(v[q][r].x, -v[q][r].y));
         }
       }
     }
@@ -300,7 +319,8 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   const int64_t nblocks = static_cast<int64_t>(p.B) * p.KM * p.NB;
   if (nblocks <= 0) return;
   const size_t lds = static_cast<size_t>(afno_spectral_lds_bytes(p.H));
-  auto kern = afno_spectral_kernel<90, 9, 10>;
+  auto kern = p.bf16_in ? (p.bf16_out ? afno_spectral_kernel<90, 9, 10, true, true> : afno_spectral_kernel<90, 9, 10, true, false>)
+                        : (p.bf16_out ? afno_spectral_kernel<90, 9, 10, false, true> : afno_spectral_kernel<90, 9, 10, false, false>);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(lds));
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));

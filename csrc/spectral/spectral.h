@@ -7,8 +7,9 @@ namespace amd_dft {
 
 // ---- AFNO: fused FFT_H -> block-diagonal complex MLP (MFMA) -> softshrink -> IFFT_H
 struct AfnoLaunch {
-  const float* x;       // [B, H, KM, C, 2] fp32 (W-direction half spectrum, KM kept modes)
-  float* y;             // same shape
+  const void* x;        // [B, H, KM, C, 2] fp32/bf16 (W-direction half spectrum, KM kept modes)
+  void* y;              // same shape (fp32/bf16)
+  int bf16_in = 0, bf16_out = 0;
   const uint16_t* w1t;  // [NB][2*BS][2*BS] bf16, real-block weight transposed ([n][k])
   const uint16_t* w2t;
   const float* b1;      // [NB][2*BS] = [b_re | b_im]

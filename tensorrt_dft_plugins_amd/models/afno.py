@@ -122,8 +122,11 @@ def afno2d_amd(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_threshold
     r0, r1, km = kept_window(H, W, hard_thresholding_fraction)
     scale_f = 1.0 / math.sqrt(H * W)
     if S.afno_fused_available(x, num_blocks) and r0 == 0 and r1 == H:
-        # W-direction R2C keeping km modes: [B, H, km, C, 2] fp32
-        xw = D._ops().r2c(x, [2], scale_f, [km, 0], torch.float32)
+        # W-direction R2C keeping km modes: [B, H, km, C, 2] (bf16 for bf16 models: halves the
+        # spectrum traffic; the spectral MLP consumes bf16 MFMA operands anyway; FFTs are fp32
+        # in registers/LDS)
+        sdt = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
+        xw = D._ops().r2c(x, [2], scale_f, [km, 0], sdt)
         yw = S.afno_spectral_h(xw, w1, b1, w2, b2, num_blocks, sparsity_threshold)
         # C2R along W from km stored modes, + bias (filter input) fused
         return S.c2r_w_add(yw, x, W, 1.0 / math.sqrt(H * W), residual)
@@ -172,7 +175,8 @@ class Block(nn.Module):
         if self.backend == "amd":
             from ..ops import spectral as S
 
-            return S.afno_block_amd(self, x)
+            x, y = S.afno_block_amd(self, x)
+            return x + y
         residual = x
         x = self.filter(self.norm1(x))
         x = x + residual  # double skip
@@ -206,19 +210,44 @@ class AFNONet(nn.Module):
         B = x.shape[0]
         p = cfg.patch_size
         if self.backend == "amd":
-            # conv with kernel == stride is a GEMM over non-overlapping patches
-            xp = x.reshape(B, cfg.in_chans, cfg.h, p, cfg.w, p).permute(0, 2, 4, 1, 3, 5)
-            xp = xp.reshape(B * cfg.h * cfg.w, cfg.in_chans * p * p)
+            # conv with kernel == stride is a GEMM over non-overlapping patches (vectorised
+            # patchify kernel instead of a strided permute copy)
+            xp = torch.ops.amd_dft.patchify(x, p)
             wmat = self.patch_embed.weight.reshape(cfg.embed_dim, -1)
             t = F.linear(xp, wmat, self.patch_embed.bias).reshape(B, cfg.h * cfg.w, cfg.embed_dim)
         else:
             t = self.patch_embed(x).flatten(2).transpose(1, 2)
         t = (t + self.pos_embed).reshape(B, cfg.h, cfg.w, cfg.embed_dim)
-        for blk in self.blocks:
-            t = blk(t)
-        t = self.head(t)  # [B, h, w, out*p*p]
+        if self.backend == "amd":
+            from ..ops import spectral as S
+
+            pending = None
+            for blk in self.blocks:
+                t, pending = S.afno_block_amd(blk, t, pending)
+            if pending is not None:
+                t = t + pending
+        else:
+            for blk in self.blocks:
+                t = blk(t)
+        if self.backend == "amd":
+            # head GEMM with its output features permuted to (c_out, p1, p2) so the un-patchify
+            # is a vectorised 16-byte remap
+            t = F.linear(t, self._head_weight_cpp())
+            return torch.ops.amd_dft.unpatchify(t, cfg.out_chans, cfg.h, cfg.w, p)
+        t = self.head(t)  # [B, h, w, out*p*p], feature order (p1, p2, c_out) as FourCastNet
         t = t.reshape(B, cfg.h, cfg.w, p, p, cfg.out_chans).permute(0, 5, 1, 3, 2, 4)
         return t.reshape(B, cfg.out_chans, cfg.h * p, cfg.w * p)
+
+    def _head_weight_cpp(self) -> torch.Tensor:
+        """Head weight with rows reordered from (p1, p2, c_out) to (c_out, p1, p2); cached."""
+        w = self.head.weight
+        key = (w.data_ptr(), w._version, w.dtype, w.device)
+        if getattr(self, "_hw_key", None) != key:
+            p, co = self.cfg.patch_size, self.cfg.out_chans
+            with torch.no_grad():
+                self._hw = w.reshape(p, p, co, -1).permute(2, 0, 1, 3).reshape(co * p * p, -1).contiguous()
+            self._hw_key = key
+        return self._hw
 
 
 def flops_per_sample(cfg: AFNOConfig) -> float:

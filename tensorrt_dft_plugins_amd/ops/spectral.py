@@ -80,24 +80,35 @@ def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm, residual: Optional[torch
     return _ops().layer_norm(x, ln.weight, ln.bias, ln.eps, residual)
 
 
-def afno_block_amd(blk, x: torch.Tensor) -> torch.Tensor:
-    """One FourCastNet block on the MI355X path (bf16 activations)."""
+def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
+    """fc + GELU with the activation fused into the GEMM epilogue (hipBLASLt) when available."""
+    if y2.is_cuda and fc.bias is not None and hasattr(torch, "_addmm_activation"):
+        return torch._addmm_activation(fc.bias, y2, fc.weight.t(), use_gelu=True)
+    return F.gelu(F.linear(y2, fc.weight, fc.bias))
+
+
+def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
+    """One FourCastNet block on the MI355X path (bf16 activations).
+
+    Residual-stream fusion: the block returns ``(x, y)`` with the true block output being
+    ``x + y`` (``y`` = fc2 output incl. bias).  The addition is fused into the next block's
+    LN1 (which also writes the summed residual stream), so fc2 needs no residual GEMM input
+    (hipBLASLt would copy it into the output first) and no separate bias/residual kernels.
+    """
     from ..models.afno import afno2d_amd
 
     f = blk.filter
     c = f.cfg
-    h, _ = layer_norm(x, blk.norm1)
-    # filter(LN1(x)) + LN1(x) [AFNO bias] + x [double skip], all fused into the C2R store
+    h, x = _ops().layer_norm(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, pending)
+    # filter(LN1(x)) + LN1(x) [AFNO bias] + x [double skip], fused into the C2R store
     x = afno2d_amd(h, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, c.hard_thresholding_fraction,
                    residual=x)
-    y, _ = layer_norm(x, blk.norm2)
+    yn, _ = layer_norm(x, blk.norm2)
     m = blk.mlp
-    B, H, W, C = y.shape
-    y2 = y.reshape(-1, C)
-    hid = F.gelu(F.linear(y2, m.fc1.weight, m.fc1.bias))
-    out = torch.addmm(x.reshape(-1, C), hid, m.fc2.weight.t()) if m.fc2.bias is None else \
-        torch.addmm(x.reshape(-1, C), hid, m.fc2.weight.t()).add_(m.fc2.bias)
-    return out.reshape(B, H, W, C)
+    B, H, W, C = yn.shape
+    hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
+    y = F.linear(hid, m.fc2.weight, m.fc2.bias)
+    return x, y.reshape(B, H, W, C)
 
 
 def fno_spectral_mix(xm: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -111,3 +111,13 @@ def test_fourcastnet_amd_vs_reference(device, depth):
         outb = mb(x.to(torch.bfloat16))
     assert rel_l2(out, ref) < 1e-2
     assert rel_l2(outb.float(), ref) < 5e-2
+
+
+def test_patchify_kernels(device):
+    torch.manual_seed(5)
+    x = torch.randn(2, 20, 720, 1440, device=device).to(torch.bfloat16)
+    t = torch.ops.amd_dft.patchify(x, 8)
+    ref = torch.ops.amd_dft.patchify(x.cpu(), 8)
+    assert torch.equal(t.cpu(), ref)
+    back = torch.ops.amd_dft.unpatchify(t, 20, 90, 180, 8)
+    assert torch.equal(back, x)
