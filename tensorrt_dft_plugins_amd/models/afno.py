@@ -210,6 +210,9 @@ class AFNONet(nn.Module):
         B = x.shape[0]
         p = cfg.patch_size
         if self.backend == "amd":
+            from .._loader import load_plugins
+
+            load_plugins()
             # conv with kernel == stride is a GEMM over non-overlapping patches (vectorised
             # patchify kernel instead of a strided permute copy)
             xp = torch.ops.amd_dft.patchify(x, p)

@@ -1,0 +1,94 @@
+"""Distributed tier (CPU, Gloo, world_size 2): batch-DP inference with overlapped all-gather
+equals the single-process result; bench.py harness under torch.distributed.run."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    try:
+        _worker_body(rank, world, port, q)
+    except BaseException as e:  # surface failures instead of a queue timeout
+        q.put((rank, repr(e), None))
+        raise
+
+
+def _worker_body(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+    from tensorrt_dft_plugins_amd.parallel import DataParallelInference, init_distributed
+
+    init_distributed("gloo")
+    torch.manual_seed(0)  # same weights on every rank
+    cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
+    model = AFNONet(cfg, backend="amd").eval()
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(2, cfg.in_chans, *cfg.img_size, generator=g)
+    dp = DataParallelInference(model, x, gather=True, use_graph=False)
+    outs = []
+    for _ in range(3):
+        outs.append(dp.step())
+    dp.drain()
+    full = outs[-1].clone()
+    with torch.no_grad():
+        local = model(x)
+    q.put((rank, full, local))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_allgather_gloo_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, full, local = q.get(timeout=300)
+        assert local is not None, f"rank {r} failed: {full}"
+        res[r] = (full, local)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expected = torch.cat([res[r][1] for r in range(world)], 0)
+    for r in range(world):
+        assert res[r][0].shape == expected.shape
+        assert torch.allclose(res[r][0], expected, atol=1e-5)
+
+
+def test_bench_harness_torchrun_gloo():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--tiny", "--gpus", "2",
+           "--steps", "2", "--warmup", "1"]
+    env = dict(os.environ)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["parallelism"] == "dp2"
+    assert d["value"] > 0 and d["higher_is_better"] is True
