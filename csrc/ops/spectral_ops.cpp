@@ -81,6 +81,113 @@ bool afno_spectral_ok(int64_t H, int64_t block_size) {
   return afno_spectral_supported(static_cast<int>(H), static_cast<int>(block_size));
 }
 
+// ------------------------------------------------------------------ FNO mode mixing
+// x [B, Cin, M, 2] fp32, w [Cin, Cout, M, 2] fp32 -> y [B, Cout, M, 2] fp32
+at::Tensor fno_mix_cpu(const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 2 && w.dim() == 4 && w.size(3) == 2 && w.size(0) == x.size(1) &&
+                  w.size(2) == x.size(2),
+              "fno_mix: x [B, Cin, M, 2], w [Cin, Cout, M, 2]");
+  at::Tensor xc = at::view_as_complex(x.to(at::kFloat).contiguous());
+  at::Tensor wc = at::view_as_complex(w.to(at::kFloat).contiguous());
+  return at::view_as_real(at::einsum("bim,iom->bom", {xc, wc})).contiguous();
+}
+
+bool fno_mix_fits(int64_t B, int64_t Cin, int64_t Cout) {
+  const int64_t K = 2 * Cin, N = 2 * Cout, Kp = (K + 3) & ~3, Bp = (B + 15) & ~15, Np = (N + 15) & ~15;
+  return 4 * 8 * (Bp * Kp + Kp * Np + Bp * Np) <= 160 * 1024;
+}
+
+at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() == 4 && x_.size(3) == 2 && w_.dim() == 4 && w_.size(3) == 2 && w_.size(0) == x_.size(1) &&
+                  w_.size(2) == x_.size(2),
+              "fno_mix: x [B, Cin, M, 2], w [Cin, Cout, M, 2]");
+  const int64_t B = x_.size(0), Cin = x_.size(1), M = x_.size(2), Cout = w_.size(1);
+  if (!fno_mix_fits(B, Cin, Cout)) return fno_mix_cpu(x_, w_);  // ATen on the device tensors
+  at::Tensor x = x_.to(at::kFloat).contiguous(), w = w_.to(at::kFloat).contiguous();
+  at::Tensor y = at::empty({B, Cout, M, 2}, x.options());
+  FnoMixLaunch p;
+  p.x = x.data_ptr<float>();
+  p.w = w.data_ptr<float>();
+  p.y = y.data_ptr<float>();
+  p.B = static_cast<int>(B);
+  p.Cin = static_cast<int>(Cin);
+  p.Cout = static_cast<int>(Cout);
+  p.M = static_cast<int>(M);
+  launch_fno_mix(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor fno_mix_meta(const at::Tensor& x, const at::Tensor& w) {
+  return at::empty({x.size(0), w.size(1), x.size(2), 2}, x.options().dtype(at::kFloat));
+}
+
+// ------------------------------------------------------------------ FNO pointwise epilogue
+// y = act(spec + conv1x1(x, w) + bias); x [B, Cin, *S], spec [B, Cout, *S] (or None), w [Cout, Cin(,1,1)]
+at::Tensor fno_pointwise_cpu(const c10::optional<at::Tensor>& spec, const at::Tensor& x, const at::Tensor& w,
+                             const c10::optional<at::Tensor>& bias, bool gelu) {
+  TORCH_CHECK(x.dim() >= 2, "fno_pointwise: x [B, Cin, ...]");
+  const int64_t B = x.size(0), Cin = x.size(1);
+  at::Tensor w2 = w.reshape({w.size(0), -1}).to(at::kFloat);
+  TORCH_CHECK(w2.size(1) == Cin, "fno_pointwise: weight must be [Cout, Cin]");
+  at::Tensor xf = x.to(at::kFloat).reshape({B, Cin, -1});
+  at::Tensor y = at::einsum("oi,bip->bop", {w2, xf});
+  if (bias.has_value() && bias->defined()) y = y + bias->to(at::kFloat).reshape({1, -1, 1});
+  if (spec.has_value() && spec->defined()) y = y + spec->to(at::kFloat).reshape({B, w2.size(0), -1});
+  if (gelu) y = at::gelu(y);
+  std::vector<int64_t> shape = x.sizes().vec();
+  shape[1] = w2.size(0);
+  return y.reshape(shape).to(x.scalar_type());
+}
+
+at::Tensor fno_pointwise_cuda(const c10::optional<at::Tensor>& spec_, const at::Tensor& x_, const at::Tensor& w,
+                              const c10::optional<at::Tensor>& bias, bool gelu) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() >= 2, "fno_pointwise: x [B, Cin, ...]");
+  TORCH_CHECK(x_.scalar_type() == at::kFloat || x_.scalar_type() == at::kBFloat16,
+              "fno_pointwise: x must be float32 or bfloat16");
+  const int64_t B = x_.size(0), Cin = x_.size(1);
+  const int64_t P = x_.numel() / std::max<int64_t>(B * Cin, 1);
+  at::Tensor w2 = w.reshape({w.size(0), -1}).to(at::kFloat).contiguous();
+  TORCH_CHECK(w2.size(1) == Cin, "fno_pointwise: weight must be [Cout, Cin]");
+  const int64_t Cout = w2.size(0);
+  TORCH_CHECK(fno_pointwise_supported(static_cast<int>(Cin)), "fno_pointwise: unsupported channel count ", Cin,
+              " (kernel instances: 4, 8, 16, 20, 32, 64, 128)");
+  TORCH_CHECK(P < (int64_t(1) << 31) / 4 && B <= 65535, "fno_pointwise: tensor too large");
+  at::Tensor x = x_.contiguous();
+  at::Tensor spec;
+  if (spec_.has_value() && spec_->defined()) {
+    TORCH_CHECK(spec_->numel() == B * Cout * P, "fno_pointwise: spec must be [B, Cout, ...] like the output");
+    spec = spec_->to(x.scalar_type()).contiguous();
+  }
+  at::Tensor bf;
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  std::vector<int64_t> shape = x.sizes().vec();
+  shape[1] = Cout;
+  at::Tensor y = at::empty(shape, x.options());
+  FnoPointwiseLaunch p;
+  p.spec = spec.defined() ? spec.data_ptr() : nullptr;
+  p.x = x.data_ptr();
+  p.w = w2.data_ptr<float>();
+  p.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  p.y = y.data_ptr();
+  p.B = static_cast<int>(B);
+  p.Cin = static_cast<int>(Cin);
+  p.Cout = static_cast<int>(Cout);
+  p.P = static_cast<int>(P);
+  p.bf16 = x.scalar_type() == at::kBFloat16;
+  p.gelu = gelu;
+  launch_fno_pointwise(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor fno_pointwise_meta(const c10::optional<at::Tensor>& spec, const at::Tensor& x, const at::Tensor& w,
+                              const c10::optional<at::Tensor>& bias, bool gelu) {
+  std::vector<int64_t> shape = x.sizes().vec();
+  shape[1] = w.size(0);
+  return at::empty(shape, x.options());
+}
+
 // ------------------------------------------------------------------ LayerNorm (+ residual)
 std::tuple<at::Tensor, at::Tensor> layer_norm_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                   double eps, const std::optional<at::Tensor>& residual) {
@@ -139,19 +246,27 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral(Tensor x, Tensor w1t, Tensor w2t, Tensor b1, Tensor b2, float lam) -> Tensor");
   m.def("afno_spectral_supported(int H, int block_size) -> bool", &amd_dft::afno_spectral_ok);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
+  m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
+  m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_cuda);
   m.impl("layer_norm", &amd_dft::layer_norm_cuda);
+  m.impl("fno_mix", &amd_dft::fno_mix_cuda);
+  m.impl("fno_pointwise", &amd_dft::fno_pointwise_cuda);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_cpu);
   m.impl("layer_norm", &amd_dft::layer_norm_cpu);
+  m.impl("fno_mix", &amd_dft::fno_mix_cpu);
+  m.impl("fno_pointwise", &amd_dft::fno_pointwise_cpu);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_meta);
   m.impl("layer_norm", &amd_dft::layer_norm_meta);
+  m.impl("fno_mix", &amd_dft::fno_mix_meta);
+  m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);
 }

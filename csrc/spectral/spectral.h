@@ -31,6 +31,19 @@ struct FnoMixLaunch {
 };
 void launch_fno_mix(const FnoMixLaunch& p, void* stream);
 
+// ---- FNO pointwise epilogue: y[b,o,p] = act(spec[b,o,p] + sum_i w[o,i] x[b,i,p] + bias[o])
+struct FnoPointwiseLaunch {
+  const void* spec;    // [B, Cout, P] (same dtype as x) or nullptr
+  const void* x;       // [B, Cin, P]
+  const float* w;      // [Cout, Cin] fp32
+  const float* bias;   // [Cout] fp32 or nullptr
+  void* y;             // [B, Cout, P]
+  int B, Cin, Cout, P;
+  int bf16 = 0, gelu = 1;
+};
+bool fno_pointwise_supported(int cin);
+void launch_fno_pointwise(const FnoPointwiseLaunch& p, void* stream);
+
 // ---- LayerNorm over the last dim (bf16/fp32 I/O, fp32 statistics)
 struct LayerNormLaunch {
   const void* x;

@@ -1,0 +1,163 @@
+"""Fourier Neural Operator (FNO, Li et al. 2021) on the MI355X DFT ops, random-initialised.
+
+The reference's motivating workload is FNO-family models (/root/reference/README.md:3); its
+TensorRT plugins supply the two FFT ends of every spectral layer
+(/root/reference/src/dft_plugins.cpp:171-195 R2C/C2R exec), and the per-mode complex multiply
+and the pointwise path run as ordinary TensorRT layers.  Here a spectral layer is three native
+kernels and nothing else:
+
+  1. pruned R2C over (H, W) -- only the kept ``[0, m1) u [H-m1, H)`` x ``[0, m2)`` modes are
+     produced (rows the mixer never reads are never transformed along H);
+  2. ``fno_mix``  -- the per-mode complex channel mixing on MFMA (``csrc/spectral/fno_mix.hip``);
+  3. pruned C2R back to ``H x W`` (the zero modes are never materialised),
+followed by ``fno_pointwise`` (1x1 conv + spectral add + bias + GELU in one HBM pass,
+``csrc/spectral/fno_pointwise.hip``).
+
+Backends: ``"torch"`` (torch.fft + einsum + conv2d, the numerics oracle) and ``"amd"``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import dft as D
+from ..ops import spectral as S
+
+__all__ = ["FNOConfig", "SpectralConv2d", "FNOBlock", "FNO2d", "spectral_conv2d_reference"]
+
+
+@dataclass
+class FNOConfig:
+    img_size: Tuple[int, int] = (720, 1440)
+    in_chans: int = 20
+    out_chans: int = 20
+    width: int = 20
+    modes1: int = 32  # kept H modes on each side (low and high)
+    modes2: int = 32  # kept W modes (one-sided)
+    n_layers: int = 4
+    proj_hidden: int = 128
+
+
+def spectral_conv2d_reference(x: torch.Tensor, weight: torch.Tensor, m1: int, m2: int) -> torch.Tensor:
+    """Classic FNO SpectralConv2d in plain PyTorch (fp32 FFT).
+
+    ``weight``: [Cin, Cout, 2*m1, m2, 2] real, rows ``[0, m1)`` act on the low H modes and rows
+    ``[m1, 2*m1)`` on the high (negative-frequency) H modes (the classic ``weights1/weights2``).
+    """
+    B, _, H, W = x.shape
+    cout = weight.shape[1]
+    wc = torch.view_as_complex(weight.float().contiguous())
+    xf = torch.fft.rfft2(x.float())
+    out = torch.zeros(B, cout, H, W // 2 + 1, dtype=torch.complex64, device=x.device)
+    out[:, :, :m1, :m2] = torch.einsum("bixy,ioxy->boxy", xf[:, :, :m1, :m2], wc[:, :, :m1])
+    out[:, :, H - m1:, :m2] = torch.einsum("bixy,ioxy->boxy", xf[:, :, H - m1:, :m2], wc[:, :, m1:])
+    return torch.fft.irfft2(out, s=(H, W))
+
+
+class SpectralConv2d(nn.Module):
+    def __init__(self, in_ch: int, out_ch: int, modes1: int, modes2: int, backend: str = "torch"):
+        super().__init__()
+        self.in_ch, self.out_ch, self.modes1, self.modes2 = in_ch, out_ch, modes1, modes2
+        self.backend = backend
+        scale = 1.0 / (in_ch * out_ch)
+        self.weight = nn.Parameter(scale * torch.rand(in_ch, out_ch, 2 * modes1, modes2, 2))
+
+    def _check(self, H: int, W: int):
+        if 2 * self.modes1 > H or self.modes2 > W // 2 + 1:
+            raise ValueError(f"modes ({self.modes1}, {self.modes2}) do not fit a {H}x{W} grid")
+
+    def spectrum(self, x: torch.Tensor) -> torch.Tensor:
+        """Spectral path only: irfft2(mix(rfft2(x)))  ->  [B, Cout, H, W] in x.dtype (amd) / fp32 (torch)."""
+        B, C, H, W = x.shape
+        self._check(H, W)
+        m1, m2 = self.modes1, self.modes2
+        if self.backend == "torch":
+            return spectral_conv2d_reference(x, self.weight, m1, m2)
+        keep = [(m1, m1), (m2, 0)]
+        xm = D.rfftn_pruned(x, [2, 3], keep)  # [B, Cin, 2*m1, m2, 2] fp32
+        ym = S.fno_spectral_mix(xm.reshape(B, C, 2 * m1 * m2, 2), self._packed_weight())
+        return D.irfftn_pruned(ym.reshape(B, self.out_ch, 2 * m1, m2, 2), [2, 3], [H, W], keep,
+                               out_dtype=x.dtype)
+
+    def _packed_weight(self) -> torch.Tensor:
+        w = self.weight
+        if w.dtype != torch.float32:
+            w = w.float()
+        return w.reshape(self.in_ch, self.out_ch, 2 * self.modes1 * self.modes2, 2)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.spectrum(x)
+
+
+class FNOBlock(nn.Module):
+    """One FNO layer: ``act(SpectralConv2d(x) + Conv1x1(x))`` -- the "FNO SpectralConv2d block"."""
+
+    def __init__(self, width: int, modes1: int, modes2: int, activation: bool = True, backend: str = "torch"):
+        super().__init__()
+        self.spectral = SpectralConv2d(width, width, modes1, modes2, backend)
+        self.w = nn.Conv2d(width, width, 1)
+        self.activation = activation
+        self.backend = backend
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.backend == "amd":
+            spec = self.spectral.spectrum(x)
+            return torch.ops.amd_dft.fno_pointwise(spec, x, self.w.weight.float(), self.w.bias.float(),
+                                                   self.activation)
+        y = self.spectral(x).to(x.dtype) + self.w(x)
+        return F.gelu(y) if self.activation else y
+
+
+class FNO2d(nn.Module):
+    """Lifting (1x1, in -> width) -> n_layers FNO blocks (last without activation) ->
+    projection (1x1 width -> proj_hidden, GELU, 1x1 -> out)."""
+
+    def __init__(self, cfg: Optional[FNOConfig] = None, backend: str = "torch"):
+        super().__init__()
+        self.cfg = cfg = cfg or FNOConfig()
+        self.lift = nn.Conv2d(cfg.in_chans, cfg.width, 1)
+        self.blocks = nn.ModuleList(
+            [FNOBlock(cfg.width, cfg.modes1, cfg.modes2, activation=i < cfg.n_layers - 1, backend=backend)
+             for i in range(cfg.n_layers)])
+        self.proj1 = nn.Conv2d(cfg.width, cfg.proj_hidden, 1)
+        self.proj2 = nn.Conv2d(cfg.proj_hidden, cfg.out_chans, 1)
+        self.set_backend(backend)
+
+    def set_backend(self, backend: str) -> "FNO2d":
+        self.backend = backend
+        for b in self.blocks:
+            b.backend = backend
+            b.spectral.backend = backend
+        return self
+
+    def _pw(self, conv: nn.Conv2d, x: torch.Tensor, gelu: bool) -> torch.Tensor:
+        if self.backend == "amd":
+            return torch.ops.amd_dft.fno_pointwise(None, x, conv.weight.float(), conv.bias.float(), gelu)
+        y = conv(x)
+        return F.gelu(y) if gelu else y
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.backend == "amd":
+            from .._loader import load_plugins
+
+            load_plugins()
+        x = self._pw(self.lift, x, False)
+        for b in self.blocks:
+            x = b(x)
+        return self._pw(self.proj2, self._pw(self.proj1, x, True), False)
+
+
+def fno_block_flops(B: int, width: int, H: int, W: int, m1: int, m2: int) -> float:
+    """Useful FLOPs of one FNO block (5 N log2 N per complex FFT-equivalent; real transforms
+    counted at half; pointwise 2*C^2 per pixel; mixing 8*C^2 per kept mode)."""
+    import math
+
+    n = H * W
+    fft = 2 * 0.5 * 5 * n * math.log2(n) * B * width
+    mix = 8 * width * width * 2 * m1 * m2 * B
+    pw = 2 * width * width * n * B
+    return fft + mix + pw

@@ -1,0 +1,160 @@
+"""FNO model family: SpectralConv2d / FNO block / FNO2d on the amd ops vs the torch.fft oracle
+(CPU tier here; the GPU tier runs the same checks on the native kernels)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorrt_dft_plugins_amd.models import FNO2d, FNOBlock, FNOConfig, spectral_conv2d_reference
+from tensorrt_dft_plugins_amd.ops import spectral as S
+from helpers import rel_l2
+
+
+def _block(width, m1, m2, seed=0):
+    torch.manual_seed(seed)
+    return FNOBlock(width, m1, m2, backend="torch")
+
+
+def test_spectral_conv_reference_matches_dense_definition():
+    """The oracle against a dense complex-DFT formulation (independent of slicing conventions)."""
+    torch.manual_seed(0)
+    B, C, H, W, m1, m2 = 1, 3, 8, 10, 2, 3
+    x = torch.randn(B, C, H, W, dtype=torch.float64)
+    wt = torch.randn(C, C, 2 * m1, m2, 2, dtype=torch.float64)
+    xf = torch.fft.fft2(x)
+    wc = torch.view_as_complex(wt)
+    out = torch.zeros(B, C, H, W, dtype=torch.complex128)
+    for kx in list(range(m1)) + list(range(H - m1, H)):
+        r = kx if kx < m1 else kx - (H - m1) + m1
+        for ky in range(m2):
+            v = torch.einsum("bi,io->bo", xf[:, :, kx, ky], wc[:, :, r, ky])
+            out[:, :, kx, ky] = v
+    ref = spectral_conv2d_reference(x.float(), wt.float(), m1, m2)
+    half = torch.zeros(B, C, H, W // 2 + 1, dtype=torch.complex128)
+    half[..., :m2] = out[..., :m2]
+    assert rel_l2(ref, torch.fft.irfft2(half, s=(H, W))) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 16, 24, 3, 5), (1, 20, 36, 40, 6, 8)])
+def test_spectral_conv_amd_cpu(shape):
+    B, C, H, W, m1, m2 = shape
+    torch.manual_seed(1)
+    blk = _block(C, m1, m2)
+    x = torch.randn(B, C, H, W)
+    ref = blk.spectral(x)
+    blk.spectral.backend = "amd"
+    out = blk.spectral(x)
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_fno_mix_op_cpu():
+    torch.manual_seed(2)
+    xm = torch.randn(3, 5, 7, 2)
+    w = torch.randn(5, 4, 7, 2)
+    y = torch.ops.amd_dft.fno_mix(xm, w)
+    ref = torch.einsum("bim,iom->bom", torch.view_as_complex(xm), torch.view_as_complex(w))
+    assert rel_l2(torch.view_as_complex(y.contiguous()), ref) < 1e-6
+
+
+def test_fno_pointwise_op_cpu():
+    torch.manual_seed(3)
+    x = torch.randn(2, 20, 6, 8)
+    s = torch.randn(2, 20, 6, 8)
+    w = torch.randn(20, 20)
+    b = torch.randn(20)
+    y = torch.ops.amd_dft.fno_pointwise(s, x, w, b, True)
+    assert rel_l2(y, F.gelu(F.conv2d(x, w[:, :, None, None], b) + s)) < 1e-6
+    y2 = torch.ops.amd_dft.fno_pointwise(None, x, w[:8], b[:8], False)
+    assert y2.shape == (2, 8, 6, 8)
+    assert rel_l2(y2, F.conv2d(x, w[:8, :, None, None], b[:8])) < 1e-6
+
+
+def test_fno_block_amd_cpu():
+    torch.manual_seed(4)
+    blk = _block(20, 4, 5)
+    x = torch.randn(2, 20, 24, 32)
+    with torch.no_grad():
+        ref = blk(x)
+        blk.backend = blk.spectral.backend = "amd"
+        out = blk(x)
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_fno2d_amd_cpu():
+    torch.manual_seed(5)
+    cfg = FNOConfig(img_size=(32, 48), in_chans=4, out_chans=3, width=16, modes1=5, modes2=7, n_layers=3,
+                    proj_hidden=32)
+    m = FNO2d(cfg, backend="torch").eval()
+    x = torch.randn(2, 4, 32, 48)
+    with torch.no_grad():
+        ref = m(x)
+        out = m.set_backend("amd")(x)
+    assert out.shape == (2, 3, 32, 48)
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_spectral_mix_fallback_matches():
+    torch.manual_seed(6)
+    xm = torch.randn(2, 3, 10, 2)
+    w = torch.randn(3, 3, 10, 2)
+    assert rel_l2(S.fno_spectral_mix(xm, w), torch.ops.amd_dft.fno_mix(xm, w)) < 1e-6
+
+
+def test_modes_too_large():
+    blk = _block(4, 20, 5)
+    blk.backend = blk.spectral.backend = "amd"
+    with pytest.raises(ValueError):
+        blk(torch.randn(1, 4, 16, 16))
+
+
+@pytest.mark.gpu
+def test_fno_mix_kernel_gpu(device):
+    torch.manual_seed(7)
+    for B, Ci, Co, M in [(1, 20, 20, 2048), (4, 20, 20, 100), (32, 20, 20, 37), (3, 7, 5, 19), (2, 32, 16, 64)]:
+        xm = torch.randn(B, Ci, M, 2)
+        w = torch.randn(Ci, Co, M, 2)
+        ref = torch.ops.amd_dft.fno_mix(xm, w)
+        out = torch.ops.amd_dft.fno_mix(xm.to(device), w.to(device))
+        assert rel_l2(out, ref) < 1e-5, (B, Ci, Co, M)
+
+
+@pytest.mark.gpu
+def test_fno_pointwise_kernel_gpu(device):
+    torch.manual_seed(8)
+    for dt in (torch.float32, torch.bfloat16):
+        for (B, Ci, Co, H, W) in [(2, 20, 20, 72, 144), (1, 20, 128, 9, 7), (1, 128, 20, 8, 8), (3, 4, 6, 5, 3)]:
+            x = torch.randn(B, Ci, H, W).to(dt)
+            s = torch.randn(B, Co, H, W).to(dt)
+            w = torch.randn(Co, Ci) / Ci ** 0.5
+            b = torch.randn(Co)
+            ref = torch.ops.amd_dft.fno_pointwise(s.float(), x.float(), w, b, True)
+            out = torch.ops.amd_dft.fno_pointwise(s.to(device), x.to(device), w.to(device), b.to(device), True)
+            assert out.dtype == dt
+            assert rel_l2(out.float(), ref) < (1e-5 if dt == torch.float32 else 1e-2), (dt, B, Ci, Co, H, W)
+
+
+@pytest.mark.gpu
+def test_fno_block_gpu_full_grid(device):
+    """BASELINE config 3: FNO SpectralConv2d block, 20 ch, 720x1440, bf16 (and fp32)."""
+    torch.manual_seed(9)
+    blk = _block(20, 32, 32).to(device)
+    x = torch.randn(1, 20, 720, 1440, device=device)
+    with torch.no_grad():
+        ref = blk(x)
+        blk.backend = blk.spectral.backend = "amd"
+        out = blk(x)
+        assert rel_l2(out, ref) < 1e-4
+        outb = blk(x.to(torch.bfloat16))
+    assert outb.dtype == torch.bfloat16
+    assert rel_l2(outb.float(), ref) < 2e-2
+
+
+@pytest.mark.gpu
+def test_fno2d_gpu(device):
+    torch.manual_seed(10)
+    cfg = FNOConfig(img_size=(90, 180), modes1=12, modes2=12, n_layers=2)
+    m = FNO2d(cfg, backend="torch").to(device).eval()
+    x = torch.randn(2, 20, 90, 180, device=device)
+    with torch.no_grad():
+        ref = m(x)
+        out = m.set_backend("amd")(x)
+    assert rel_l2(out, ref) < 1e-4
