@@ -31,6 +31,7 @@ def main(argv=None):
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--amd-only", action="store_true", help="skip the torch comparator (profiling)")
     a = ap.parse_args(argv)
     tdp.load_plugins()
     dev = torch.device("cuda:0")
@@ -53,11 +54,13 @@ def main(argv=None):
             for _ in range(a.rounds):
                 samples["amd_eager"].append(time_eager(lambda: amd(x), a.iters))
                 samples["amd_graph"].append(time_graph(lambda: amd(x), a.iters))
-                samples["torch_eager"].append(time_eager(lambda: blk_t(x), a.iters))
-                samples["torch_graph"].append(time_graph(lambda: blk_t(x), a.iters))
-        r = {k: {"median_us": statistics.median(v), "min_us": min(v)} for k, v in samples.items()}
+                if not a.amd_only:
+                    samples["torch_eager"].append(time_eager(lambda: blk_t(x), a.iters))
+                    samples["torch_graph"].append(time_graph(lambda: blk_t(x), a.iters))
+        r = {k: {"median_us": statistics.median(v), "min_us": min(v)} for k, v in samples.items() if v}
         r["rel_l2_vs_fp32_torch"] = err
-        r["speedup_graph_vs_torch"] = r["torch_graph"]["median_us"] / r["amd_graph"]["median_us"]
+        if not a.amd_only:
+            r["speedup_graph_vs_torch"] = r["torch_graph"]["median_us"] / r["amd_graph"]["median_us"]
         fl = fno_block_flops(a.batch, a.width, H, W, *a.modes)
         r["block_gflops_amd_graph"] = fl / (r["amd_graph"]["median_us"] * 1e3)
         nbytes = x.element_size() * x.numel()

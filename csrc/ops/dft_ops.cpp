@@ -26,9 +26,11 @@
 #include <memory>
 #include <mutex>
 #include <sstream>
+#include <string>
 #include <unordered_map>
 
 #include "../fft/fft_plan.h"
+#include "../spectral/dft_gemm.h"
 #include "plan_cache.h"
 
 namespace amd_dft {
@@ -173,6 +175,77 @@ C2RShape c2r_shape(at::IntArrayRef sizes_with_2, at::IntArrayRef dim, at::IntArr
   return r;
 }
 
+// ------------------------------------------------------------------ DFT-as-GEMM (pruned R2C)
+// A pruned R2C along the innermost, contiguous axis that keeps few modes runs as an MFMA GEMM
+// (csrc/spectral/dft_gemm.hip) instead of a full Stockham FFT.  MI_DFT_GEMM=0 disables it.
+bool use_dftw(const at::Tensor& in, const DimSpec& s, at::ScalarType out_t) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("MI_DFT_GEMM");
+    return !(e && std::string(e) == "0");
+  }();
+  if (!enabled || out_t != at::kFloat || !in.is_contiguous()) return false;
+  if (s.axis != in.dim() - 1 || s.hi != 0) return false;
+  // fp32 inputs stay on the Stockham kernels (~1e-7): the GEMM's bf16x3 split of fp32 data is
+  // good to ~4e-6 relative; bf16 inputs are exact operands and get fp32-grade results.
+  if (in.scalar_type() != at::kBFloat16) return false;
+  if (s.lo < 1 || s.lo > 64 || s.n % 8 != 0 || s.n < 64 || 8 * s.lo > s.n) return false;
+  return in.numel() < (int64_t(1) << 31);
+}
+
+void run_dftw(const at::Tensor& in, const at::Tensor& out, const DimSpec& s, float scale) {
+  auto tabs = get_dft_gemm_tables(DftTable::R2C, static_cast<int>(s.n), static_cast<int>(s.lo), in.device());
+  DftwR2CLaunch p;
+  p.x = in.data_ptr();
+  p.out = out.data_ptr();
+  p.b0 = tabs.first.data_ptr();
+  p.phase = tabs.second.data_ptr();
+  p.R = static_cast<int>(in.numel() / s.n);
+  p.W = static_cast<int>(s.n);
+  p.m = static_cast<int>(s.lo);
+  p.scale = scale;
+  p.bf16 = in.scalar_type() == at::kBFloat16;
+  launch_dftw_r2c(p, c10::hip::getCurrentHIPStream(in.device().index()).stream());
+}
+
+at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
+                    std::optional<at::ScalarType> out_dtype);
+
+// Explicit DFT-GEMM R2C along the last dim (any supported dtype): [..., W] -> [..., m, 2] fp32.
+at::Tensor dftw_r2c_cuda(const at::Tensor& x_, int64_t m, double scale) {
+  const c10::DeviceGuard guard(x_.device());
+  at::Tensor x = x_.contiguous();
+  TORCH_CHECK(x.dim() >= 1 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "amd_dft.dftw_r2c: x must be float32 or bfloat16");
+  const int64_t W = x.size(-1);
+  TORCH_CHECK(m >= 1 && m <= W / 2 + 1, "amd_dft.dftw_r2c: needs 1 <= m <= W/2+1");
+  if (m > 64 || W % 8 != 0)  // outside the GEMM kernel: pruned Stockham R2C
+  {
+    const std::vector<int64_t> d{x.dim() - 1}, k{m, 0};
+    return r2c_cuda(x, d, scale, k, at::kFloat);
+  }
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "amd_dft.dftw_r2c: tensor too large");
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = m;
+  os.push_back(2);
+  at::Tensor out = at::empty(os, x.options().dtype(at::kFloat));
+  if (x.numel() == 0) return out;
+  DimSpec s{static_cast<int>(x.dim() - 1), W, m, 0};
+  run_dftw(x, out, s, static_cast<float>(scale));
+  return out;
+}
+
+at::Tensor dftw_r2c_cpu(const at::Tensor& x, int64_t m, double scale) {
+  at::Tensor y = at::fft_rfft(x.to(at::kDouble), c10::nullopt, -1).narrow(-1, 0, m) * scale;
+  return at::view_as_real(y.to(at::kComplexFloat).contiguous()).contiguous();
+}
+
+at::Tensor dftw_r2c_meta(const at::Tensor& x, int64_t m, double) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = m;
+  os.push_back(2);
+  return at::empty(os, x.options().dtype(at::kFloat));
+}
+
 // ------------------------------------------------------------------ CUDA (HIP) impls
 at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
                     std::optional<at::ScalarType> out_dtype) {
@@ -195,7 +268,9 @@ at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at:
     const bool final_pass = i == 0;
     at::Tensor out = alloc_complex(nxt, opts, final_pass ? odt : at::kFloat);
     const float sc = final_pass ? static_cast<float>(scale) : 1.0f;
-    if (i == ns - 1) {
+    if (i == ns - 1 && use_dftw(cur_t, s, out.scalar_type())) {
+      run_dftw(cur_t, out, s, sc);
+    } else if (i == ns - 1) {
       run_pass(Kind::R2C, cur_t, out, cur, nxt, s.axis, s.n, static_cast<int>(s.n), 0, static_cast<int>(s.lo), 0,
                sc, false);
     } else {
@@ -292,6 +367,65 @@ at::Tensor c2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, bool inverse, dou
     cur_t = out;
   }
   return cur_t;
+}
+
+// Pruned C2C along one axis: input stores modes [0, in_lo) u [n - in_hi, n) of a length-n
+// transform, output keeps [0, out_lo) u [n - out_hi, n).  Unnormalised, times `scale`.
+void check_c2c_axis(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,
+                    int64_t out_hi) {
+  TORCH_CHECK(x.dim() >= 2 && x.size(-1) == 2, "amd_dft.c2c_axis: complex input needs a trailing dim of size 2");
+  TORCH_CHECK(n >= 1 && in_lo >= 0 && in_hi >= 0 && out_lo >= 0 && out_hi >= 0 && in_lo + in_hi <= n &&
+                  out_lo + out_hi <= n && in_lo + in_hi >= 1,
+              "amd_dft.c2c_axis: bad mode windows");
+  TORCH_CHECK(x.size(dim) == in_lo + in_hi, "amd_dft.c2c_axis: dim ", dim, " stores ", x.size(dim),
+              " modes, expected in_lo + in_hi = ", in_lo + in_hi);
+}
+
+at::Tensor c2c_axis_cuda(const at::Tensor& x_, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,
+                         int64_t out_hi, bool inverse, double scale) {
+  const c10::DeviceGuard guard(x_.device());
+  at::Tensor x = x_.contiguous();
+  to_dtype(x.scalar_type());
+  const int64_t nd = x.dim() - 1;
+  dim = dim < 0 ? dim + nd : dim;
+  TORCH_CHECK(dim >= 0 && dim < nd, "amd_dft.c2c_axis: dim out of range");
+  check_c2c_axis(x, dim, n, in_lo, in_hi, out_lo, out_hi);
+  std::vector<int64_t> cur(x.sizes().begin(), x.sizes().end() - 1);
+  std::vector<int64_t> nxt = cur;
+  nxt[dim] = out_lo + out_hi;
+  at::Tensor out = alloc_complex(nxt, x.options(), at::kFloat);
+  if (out.numel() == 0) return out;
+  run_pass(Kind::C2C, x, out, cur, nxt, static_cast<int>(dim), n, static_cast<int>(in_lo), static_cast<int>(in_hi),
+           static_cast<int>(out_lo), static_cast<int>(out_hi), static_cast<float>(scale), inverse);
+  return out;
+}
+
+at::Tensor c2c_axis_cpu(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,
+                        int64_t out_hi, bool inverse, double scale) {
+  const int64_t nd = x.dim() - 1;
+  dim = dim < 0 ? dim + nd : dim;
+  check_c2c_axis(x, dim, n, in_lo, in_hi, out_lo, out_hi);
+  at::Tensor xc = at::view_as_complex(x.to(at::kDouble).contiguous());
+  std::vector<int64_t> full_shape(xc.sizes().begin(), xc.sizes().end());
+  full_shape[dim] = n;
+  at::Tensor full = at::zeros(full_shape, xc.options());
+  if (in_lo) full.narrow(dim, 0, in_lo).copy_(xc.narrow(dim, 0, in_lo));
+  if (in_hi) full.narrow(dim, n - in_hi, in_hi).copy_(xc.narrow(dim, in_lo, in_hi));
+  at::Tensor y = inverse ? at::fft_ifft(full, n, dim, "forward") : at::fft_fft(full, n, dim, "backward");
+  y = y * scale;
+  std::vector<at::Tensor> parts;
+  if (out_lo) parts.push_back(y.narrow(dim, 0, out_lo));
+  if (out_hi) parts.push_back(y.narrow(dim, n - out_hi, out_hi));
+  at::Tensor r = parts.size() == 1 ? parts[0] : at::cat(parts, dim);
+  return at::view_as_real(r.to(at::kComplexFloat).contiguous()).contiguous();
+}
+
+at::Tensor c2c_axis_meta(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,
+                         int64_t out_hi, bool, double) {
+  std::vector<int64_t> s(x.sizes().begin(), x.sizes().end());
+  const int64_t nd = x.dim() - 1;
+  s[dim < 0 ? dim + nd : dim] = out_lo + out_hi;
+  return at::empty(s, x.options().dtype(at::kFloat));
 }
 
 // ------------------------------------------------------------------ CPU impls (torch.fft)
@@ -462,6 +596,9 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("c2c(Tensor x, int[] dim, bool inverse=False, float scale=1.0, ScalarType? out_dtype=None) -> Tensor");
   m.def("c2r_add(Tensor x, int[] dim, int[] out_size, float scale=1.0, int[] keep=[], Tensor? add1=None, "
         "Tensor? add2=None, ScalarType? out_dtype=None) -> Tensor");
+  m.def("c2c_axis(Tensor x, int dim, int n, int in_lo, int in_hi, int out_lo, int out_hi, bool inverse=False, "
+        "float scale=1.0) -> Tensor");
+  m.def("dftw_r2c(Tensor x, int m, float scale=1.0) -> Tensor");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("plan_info(int n) -> str", &amd_dft::plan_info);
@@ -475,6 +612,8 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("c2r", &amd_dft::c2r_cuda);
   m.impl("c2c", &amd_dft::c2c_cuda);
   m.impl("c2r_add", &amd_dft::c2r_add_cuda);
+  m.impl("c2c_axis", &amd_dft::c2c_axis_cuda);
+  m.impl("dftw_r2c", &amd_dft::dftw_r2c_cuda);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -482,6 +621,8 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("c2r", &amd_dft::c2r_cpu);
   m.impl("c2c", &amd_dft::c2c_cpu);
   m.impl("c2r_add", &amd_dft::c2r_add_cpu);
+  m.impl("c2c_axis", &amd_dft::c2c_axis_cpu);
+  m.impl("dftw_r2c", &amd_dft::dftw_r2c_cpu);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -489,6 +630,8 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("c2r", &amd_dft::c2r_meta);
   m.impl("c2c", &amd_dft::c2c_meta);
   m.impl("c2r_add", &amd_dft::c2r_add_meta);
+  m.impl("c2c_axis", &amd_dft::c2c_axis_meta);
+  m.impl("dftw_r2c", &amd_dft::dftw_r2c_meta);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {

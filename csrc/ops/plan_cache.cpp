@@ -5,7 +5,11 @@
 #include <cstdlib>
 #include <list>
 #include <mutex>
+#include <map>
+#include <tuple>
 #include <unordered_map>
+
+#include "../spectral/dft_gemm.h"
 
 namespace amd_dft {
 namespace {
@@ -69,6 +73,27 @@ PlanCache& plan_cache() {
 }  // namespace
 
 std::shared_ptr<DevPlan> get_plan(int64_t L, const at::Device& dev) { return plan_cache().get(L, dev); }
+
+std::pair<at::Tensor, at::Tensor> get_dft_gemm_tables(DftTable kind, int W, int m, const at::Device& dev) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int>, std::pair<at::Tensor, at::Tensor>> cache;
+  const auto key = std::make_tuple(static_cast<int>(kind), W, m, static_cast<int>(dev.index()));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  TORCH_CHECK(c10::hip::currentStreamCaptureStatusMayInitCtx() == c10::hip::CaptureStatus::None,
+              "amd_dft: DFT-GEMM tables for length ", W, " were not created before graph capture; run the model "
+              "once (warm-up) before capturing");
+  std::vector<uint16_t> frag;
+  std::vector<float> ph;
+  if (kind == DftTable::R2C) dftw_r2c_tables(W, m, frag, ph);
+  else fno_c2r_tables(W, m, kind == DftTable::C2R_BF16 ? kFnoChunkBF : kFnoChunkF32, frag, ph);
+  auto f = at::from_blob(frag.data(), {static_cast<int64_t>(frag.size())}, at::TensorOptions().dtype(at::kShort))
+               .to(dev);
+  auto p = at::from_blob(ph.data(), {static_cast<int64_t>(ph.size())}, at::TensorOptions().dtype(at::kFloat)).to(dev);
+  // Never evicted: captured graphs keep raw pointers to these tables.
+  return cache[key] = {f, p};
+}
 size_t plan_cache_entries() { return plan_cache().size(); }
 void plan_cache_reset() { plan_cache().clear(); }
 

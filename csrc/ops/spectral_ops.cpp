@@ -4,8 +4,10 @@
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <ATen/core/dispatch/Dispatcher.h>
 #include <torch/library.h>
 
+#include "../spectral/dft_gemm.h"
 #include "../spectral/spectral.h"
 #include "plan_cache.h"
 
@@ -188,6 +190,80 @@ at::Tensor fno_pointwise_meta(const c10::optional<at::Tensor>& spec, const at::T
   return at::empty(shape, x.options());
 }
 
+// ------------------------------------------------------------------ FNO layer tail (C2R-W + pointwise)
+// yw [B, Cout, H, m, 2] fp32 (inverse-H-transformed kept modes, carrying the 1/(H W) scale),
+// x [B, Cin, H, W] -> y [B, Cout, H, W] = act(irfft_W(yw) + conv1x1(x, wc) + bias), dtype of x.
+void check_fno_c2r(const at::Tensor& yw, const at::Tensor& x, const at::Tensor& wc) {
+  TORCH_CHECK(x.dim() == 4 && yw.dim() == 5 && yw.size(4) == 2, "fno_c2r_pw: yw [B, Cout, H, m, 2], x [B, Cin, H, W]");
+  TORCH_CHECK(yw.size(0) == x.size(0) && yw.size(2) == x.size(2), "fno_c2r_pw: batch / H mismatch");
+  TORCH_CHECK(wc.numel() == yw.size(1) * x.size(1), "fno_c2r_pw: wc must be [Cout, Cin]");
+  TORCH_CHECK(2 * (yw.size(3) - 1) <= x.size(3), "fno_c2r_pw: more modes than the half spectrum");
+}
+
+at::Tensor fno_c2r_pw_cpu(const at::Tensor& yw, const at::Tensor& x, const at::Tensor& wc,
+                          const c10::optional<at::Tensor>& bias, bool gelu) {
+  check_fno_c2r(yw, x, wc);
+  const int64_t W = x.size(3), m = yw.size(3);
+  at::Tensor full = at::zeros({yw.size(0), yw.size(1), yw.size(2), W / 2 + 1}, yw.options().dtype(at::kComplexDouble));
+  full.narrow(3, 0, m).copy_(at::view_as_complex(yw.to(at::kDouble).contiguous()));
+  at::Tensor spec = at::fft_irfft(full, W, 3, "forward").to(at::kFloat);
+  return fno_pointwise_cpu(spec, x, wc.reshape({yw.size(1), x.size(1)}), bias, gelu);
+}
+
+at::Tensor fno_c2r_pw_cuda(const at::Tensor& yw_, const at::Tensor& x_, const at::Tensor& wc_,
+                           const c10::optional<at::Tensor>& bias, bool gelu) {
+  const c10::DeviceGuard guard(x_.device());
+  check_fno_c2r(yw_, x_, wc_);
+  TORCH_CHECK(x_.scalar_type() == at::kFloat || x_.scalar_type() == at::kBFloat16,
+              "fno_c2r_pw: x must be float32 or bfloat16");
+  const int64_t B = x_.size(0), Cin = x_.size(1), H = x_.size(2), W = x_.size(3), Cout = yw_.size(1),
+                m = yw_.size(3);
+  if (!fno_c2r_pw_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(m),
+                            static_cast<int>(W))) {
+    // shapes outside the fused kernel: C2R on the FFT kernels + the pointwise kernel
+    static auto c2r = c10::Dispatcher::singleton()
+                          .findSchemaOrThrow("amd_dft::c2r", "")
+                          .typed<at::Tensor(const at::Tensor&, at::IntArrayRef, at::IntArrayRef, double,
+                                            at::IntArrayRef, std::optional<at::ScalarType>)>();
+    const std::vector<int64_t> dim{3}, out_size{W};
+    at::Tensor spec = c2r.call(yw_.to(at::kFloat).contiguous(), dim, out_size, 1.0, {}, x_.scalar_type());
+    return fno_pointwise_cuda(spec, x_, wc_.reshape({Cout, Cin}), bias, gelu);
+  }
+  TORCH_CHECK(B * Cin * H * W < (int64_t(1) << 31) && B * Cout * H * W < (int64_t(1) << 31),
+              "fno_c2r_pw: tensor too large");
+  at::Tensor x = x_.contiguous();
+  at::Tensor yw = yw_.to(at::kFloat).contiguous();
+  at::Tensor wc = wc_.to(at::kFloat).reshape({Cout, Cin}).contiguous();
+  at::Tensor bf;
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  at::Tensor y = at::empty({B, Cout, H, W}, x.options());
+  auto tabs = get_dft_gemm_tables(x.scalar_type() == at::kBFloat16 ? DftTable::C2R_BF16 : DftTable::C2R_F32,
+                                  static_cast<int>(W), static_cast<int>(m), x.device());
+  FnoC2RPwLaunch p;
+  p.yw = yw.data_ptr();
+  p.x = x.data_ptr();
+  p.wc = wc.data_ptr<float>();
+  p.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  p.y = y.data_ptr();
+  p.g0 = tabs.first.data_ptr();
+  p.rot = tabs.second.data_ptr();
+  p.B = static_cast<int>(B);
+  p.Cin = static_cast<int>(Cin);
+  p.Cout = static_cast<int>(Cout);
+  p.H = static_cast<int>(H);
+  p.W = static_cast<int>(W);
+  p.m = static_cast<int>(m);
+  p.bf16 = x.scalar_type() == at::kBFloat16;
+  p.gelu = gelu;
+  launch_fno_c2r_pw(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor fno_c2r_pw_meta(const at::Tensor& yw, const at::Tensor& x, const at::Tensor& wc,
+                           const c10::optional<at::Tensor>&, bool) {
+  return at::empty({x.size(0), yw.size(1), x.size(2), x.size(3)}, x.options());
+}
+
 // ------------------------------------------------------------------ LayerNorm (+ residual)
 std::tuple<at::Tensor, at::Tensor> layer_norm_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                   double eps, const std::optional<at::Tensor>& residual) {
@@ -248,6 +324,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
+  m.def("fno_c2r_pw(Tensor yw, Tensor x, Tensor wc, Tensor? bias=None, bool gelu=True) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
@@ -255,6 +332,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("layer_norm", &amd_dft::layer_norm_cuda);
   m.impl("fno_mix", &amd_dft::fno_mix_cuda);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_cuda);
+  m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cuda);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -262,6 +340,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("layer_norm", &amd_dft::layer_norm_cpu);
   m.impl("fno_mix", &amd_dft::fno_mix_cpu);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_cpu);
+  m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cpu);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -269,4 +348,5 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("layer_norm", &amd_dft::layer_norm_meta);
   m.impl("fno_mix", &amd_dft::fno_mix_meta);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);
+  m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_meta);
 }

@@ -1,0 +1,214 @@
+// Pruned real DFTs along the innermost axis as MFMA GEMMs (FNO path).
+//
+// When only the first m <= 64 of the W/2+1 half-spectrum modes are kept (FNO keeps 16-32 of
+// 721), a Stockham FFT computes ~20x more outputs than are used and is bound by its LDS passes.
+// A truncated DFT is a tall-skinny GEMM  X[r, n] = sum_k x[r, k] e^{-2 pi i n k / W}  that the
+// matrix cores finish far below the HBM time of reading x once.  The twiddle operand would
+// have to be re-read for every row tile (W x 2m complex, 368 KB for 1440 x 32 -- more L2
+// traffic than x itself), so it is factored instead:
+//   k = KB*s + k',   e^{-2 pi i n k/W} = e^{-2 pi i n KB s/W} * e^{-2 pi i n k'/W}
+// The KB x 16G block B0[k'][n] (bf16 hi/lo split, so the twiddles are exact to ~2^-17) lives
+// in registers for the whole kernel; each KB-block of x contributes  ph_s[n] * (x_s . B0)  with
+// one complex scale of the MFMA accumulator per block and mode.
+//
+//   x:   [R, W] bf16 or fp32 rows (contiguous)     out: [R, m] complex fp32 (re, im)
+//   A fragment (16x32 bf16): lane l holds x[row0 + (l&15)][k0 + 8(l>>4) + j], j < 8 -- one
+//   16-byte load per lane straight from HBM (no LDS); fp32 input is split hi + lo on the fly.
+// A workgroup (4 waves) owns 16 rows; the waves take interleaved KB-blocks (split-K) and are
+// summed through LDS, so a 20x720-row FNO input still launches 900 workgroups.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+#include "dft_gemm.h"
+
+namespace amd_dft {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNKS = kDftGemmKB / 32;  // 32-deep MFMA k-steps per block
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = static_cast<__bf16>(v[j]);
+    hi[j] = h;
+    lo[j] = static_cast<__bf16>(v[j] - static_cast<float>(h));
+  }
+}
+
+template <bool BF, int G>
+__global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
+                                                       const bf16x8* __restrict__ b0, const float2* __restrict__ ph,
+                                                       int R, int W, int m, float scale, int nblk) {
+  __shared__ f32x4 red[3][G][2][64];
+  // block phases in LDS: read once per block and mode right before use, so an L2 round trip
+  // there would sit on every block's critical path
+  constexpr int kPhMax = 2048;
+  __shared__ float2 phs[kPhMax];
+  const int nph = nblk * 16 * G;
+  const bool ph_lds = nph <= kPhMax;
+  if (ph_lds)
+    for (int t = threadIdx.x; t < nph; t += 256) phs[t] = ph[t];
+  __syncthreads();
+  const float2* pht = ph_lds ? static_cast<const float2*>(phs) : ph;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * 16;
+  const int rowA = min(row0 + (lane & 15), R - 1);
+  const int kq = 8 * (lane >> 4);
+  // twiddle block, fragment order [kk][g][re/im][hi/lo][lane]
+  bf16x8 bfr[kNKS][G][2][2];
+#pragma unroll
+  for (int kk = 0; kk < kNKS; ++kk)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bfr[kk][g][c][h] = b0[(((kk * G + g) * 2 + c) * 2 + h) * 64 + lane];
+  f32x4 are[G], aim[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) are[g] = aim[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A operand: one 16-byte (bf16) / two 16-byte (fp32) loads per lane and k-step.
+  using Raw = typename std::conditional<BF, uint4, float4>::type;
+  constexpr int NR = BF ? 1 : 2;
+  const char* xrow = static_cast<const char*>(x) + static_cast<int64_t>(rowA) * W * (BF ? 2 : 4);
+  auto load = [&](int s, Raw (&r)[kNKS][NR]) {
+#pragma unroll
+    for (int kk = 0; kk < kNKS; ++kk) {
+      const int k0 = s * kDftGemmKB + 32 * kk + kq;
+      const bool ok = k0 < W;  // W % 8 == 0: a lane's 8 samples are all in or all out
+      const Raw* p = reinterpret_cast<const Raw*>(xrow + static_cast<int64_t>(ok ? k0 : 0) * (BF ? 2 : 4));
+#pragma unroll
+      for (int t = 0; t < NR; ++t) {
+        r[kk][t] = p[t];
+        if (!ok) r[kk][t] = Raw{};
+      }
+    }
+  };
+  // Batches of PF blocks per wave are loaded before any is consumed: 6 x 1 KB per wave in
+  // flight (one batch covers W <= 1536), enough to cover HBM latency at ~3 waves per SIMD.
+  constexpr int PF = 6;
+  for (int s0 = wv; s0 < nblk; s0 += 4 * PF) {
+    Raw buf[PF][kNKS][NR];
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      if (s0 + 4 * j < nblk) load(s0 + 4 * j, buf[j]);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int s = s0 + 4 * j;
+      if (s >= nblk) break;
+      f32x4 tr[G], ti[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) tr[g] = ti[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < kNKS; ++kk) {
+        if constexpr (BF) {
+          const bf16x8 a = __builtin_bit_cast(bf16x8, buf[j][kk][0]);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][0][0], tr[g], 0, 0, 0);
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][0][1], tr[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][0], ti[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][1], ti[g], 0, 0, 0);
+          }
+        } else {
+          const float4 f0 = buf[j][kk][0], f1 = buf[j][kk][NR - 1];
+          const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+          bf16x8 ah, al;
+          split8(v, ah, al);
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[kk][g][0][0], tr[g], 0, 0, 0);
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[kk][g][0][1], tr[g], 0, 0, 0);
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bfr[kk][g][0][0], tr[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[kk][g][1][0], ti[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bfr[kk][g][1][1], ti[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bfr[kk][g][1][0], ti[g], 0, 0, 0);
+          }
+        }
+      }
+      // block phase e^{-2 pi i n KB s / W}: one complex scale per accumulator column (mode n)
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float2 p = pht[s * 16 * G + 16 * g + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          are[g][i] = fmaf(p.x, tr[g][i], fmaf(-p.y, ti[g][i], are[g][i]));
+          aim[g][i] = fmaf(p.x, ti[g][i], fmaf(p.y, tr[g][i], aim[g][i]));
+        }
+      }
+    }
+  }
+  // split-K reduction of the 4 waves
+  if (wv > 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      red[wv - 1][g][0][lane] = are[g];
+      red[wv - 1][g][1][lane] = aim[g];
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      are[g] += red[w][g][0][lane];
+      aim[g] += red[w][g][1][lane];
+    }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int n = 16 * g + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + 4 * (lane >> 4) + i;
+      if (row < R && n < m)
+        out[static_cast<int64_t>(row) * m + n] = make_float2(are[g][i] * scale, aim[g][i] * scale);
+    }
+  }
+}
+
+template <bool BF>
+void launch_g(const DftwR2CLaunch& p, hipStream_t st) {
+  const int G = (p.m + 15) / 16;
+  const dim3 grid((p.R + 15) / 16);
+  const int nblk = (p.W + kDftGemmKB - 1) / kDftGemmKB;
+  const bf16x8* b0 = static_cast<const bf16x8*>(p.b0);
+  float2* out = static_cast<float2*>(p.out);
+  const float2* ph = static_cast<const float2*>(p.phase);
+#define L_(GG)                                                                                                    \
+  hipLaunchKernelGGL((dftw_r2c_kernel<BF, GG>), grid, dim3(256), 0, st, p.x, out, b0, ph, p.R, p.W, p.m, p.scale, \
+                     nblk)
+  switch (G) {
+    case 1: L_(1); break;
+    case 2: L_(2); break;
+    case 3: L_(3); break;
+    case 4: L_(4); break;
+    default: throw std::runtime_error("amd_dft: dftw_r2c: m must be in [1, 64]");
+  }
+#undef L_
+}
+
+}  // namespace
+
+void launch_dftw_r2c(const DftwR2CLaunch& p, void* stream) {
+  if (p.R == 0) return;
+  if (p.m < 1 || p.m > 64 || p.W % 8 != 0 || p.W < 8)
+    throw std::runtime_error("amd_dft: dftw_r2c needs 1 <= m <= 64 and W % 8 == 0");
+  if (static_cast<int64_t>(p.R) * p.W >= (int64_t(1) << 31))
+    throw std::runtime_error("amd_dft: dftw_r2c: tensor too large for 32-bit row offsets");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (p.bf16) launch_g<true>(p, st);
+  else launch_g<false>(p, st);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: dftw_r2c launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft

@@ -1,0 +1,390 @@
+// FNO layer tail in one kernel: inverse real DFT along W of the kept modes (as an MFMA GEMM),
+// + the 1x1 convolution of the layer input (MFMA), + bias, + GELU, one store of the output.
+//
+//   y[b,o,h,w] = act( sum_{k<m} s_k Re(Y[b,o,h,k] e^{2 pi i k w/W}) + sum_i Wc[o,i] x[b,i,h,w] + bias[o] )
+//
+// Replaces C2R-along-W (writes the full-resolution spectral output) + a pointwise kernel
+// (reads it back): the only HBM traffic left is reading x and writing y.
+//
+// GEMM orientation: C[m = pixel][n = out channel] so a lane's accumulator holds 4 consecutive
+// pixels of one channel (8/16-byte stores).  Per CH-pixel chunk starting at w0:
+//   spec:  A = G[k'][px]  (bf16 hi/lo fragments of s_k cos / -s_k sin, identical for every chunk,
+//          staged once per workgroup in LDS),  B = Y rotated by e^{2 pi i k w0/W} (fp32 in
+//          registers, split hi/lo per chunk) -- the same phase factorisation as dft_gemm.hip;
+//   conv:  A = x[i][px] from a per-wave LDS tile of the channel-planar input, read transposed by
+//          ds_read_b64_tr_b16 (bf16; two reads give a lane its 8 channels of one pixel),
+//          B = Wc^T (hi/lo split once).
+// Scheduling: the (row, chunk) units of the whole tensor are split into equal contiguous ranges,
+// one per wave (persistent-style), so no tail of half-empty rows; Y is reloaded on row change.
+// GELU: exact-erf form (A&S 7.1.26, |err| < 1.5e-7) for fp32 output; for bf16 output the tanh
+// form (|err| < 5e-4 absolute, 1/8 of a bf16 ulp at |y| ~ 1) at ~half the instruction cost.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+#include "dft_gemm.h"
+
+namespace amd_dft {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+__device__ __forceinline__ void split1(float v, __bf16& hi, __bf16& lo) {
+  hi = static_cast<__bf16>(v);
+  lo = static_cast<__bf16>(v - static_cast<float>(hi));
+}
+
+__device__ __forceinline__ float gelu_erf(float v) {
+  const float z = fabsf(v) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = fmaf(-p, __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z), 1.f);  // erf(|v|/sqrt2)
+  return 0.5f * v * (1.f + copysignf(e, v));
+}
+
+__device__ __forceinline__ float gelu_tanh(float v) {
+  // x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)) = x / (1 + 2^(v (c1 + c2 v^2)))
+  constexpr float c1 = -1.5957691216057308f * 1.4426950408889634f;
+  constexpr float c2 = c1 * 0.044715f;
+  const float z = v * fmaf(c2, v * v, c1);
+  return v * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool BF>
+struct Geo {
+  static constexpr int CH = BF ? kFnoChunkBF : kFnoChunkF32;  // pixels per chunk
+  static constexpr int PT = CH / 16;                           // MFMA pixel tiles per chunk
+  static constexpr int XP = BF ? CH + 16 : CH + 4;             // LDS row pitch (elements) of the x tile
+  static constexpr int ES = BF ? 2 : 4;
+};
+
+// two floats -> packed bf16x2 (v_cvt_pk_bf16_f32, round-to-nearest-even)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 v;
+  v[0] = static_cast<__bf16>(a);
+  v[1] = static_cast<__bf16>(b);
+  return __builtin_bit_cast(uint32_t, v);
+}
+// hi = bf16(a, b); lo = bf16(a - hi.a, b - hi.b)
+__device__ __forceinline__ void split_pk(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pk_bf16(a, b);
+  lo = pk_bf16(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+
+template <int ACT>
+__device__ __forceinline__ float act(float v) {
+  if constexpr (ACT == 1) return gelu_erf(v);
+  if constexpr (ACT == 2) return gelu_tanh(v);
+  return v;
+}
+
+// row_ror:n inside 16-lane rows: lane i receives lane (i - n) mod 16 of its row
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xf, 0xf, false));
+}
+
+template <bool BF>
+__device__ __forceinline__ void store4(char* dst, const float (&v)[4]) {
+  if constexpr (BF) *reinterpret_cast<uint2*>(dst) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+  else *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <bool BF, int KS, int CO, int ACT>
+__global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restrict__ yw, const void* __restrict__ x,
+                                                         const float* __restrict__ wc, const float* __restrict__ bias,
+                                                         void* __restrict__ y, const bf16x8* __restrict__ g0,
+                                                         const float2* __restrict__ rot, int Cin, int Cout, int H,
+                                                         int W, int m, int nch, int64_t units) {
+  using GG = Geo<BF>;
+  constexpr int PT = GG::PT, XP = GG::XP, ES = GG::ES, CH = GG::CH;
+  constexpr bool PREC3 = !BF;  // fp32 output: also the G_lo * Y_hi term (twiddles exact to ~2^-17)
+  constexpr int NG = PREC3 ? 2 : 1;
+  __shared__ bf16x8 g0s[KS][PT][NG][64];
+  __shared__ __attribute__((aligned(16))) char xs_raw[4][32 * XP * ES];
+  // chunk rotations in LDS (needed right before each chunk's MFMAs; an L2 round trip there
+  // stalled every chunk)
+  constexpr int kRotMax = 2048;
+  __shared__ float2 rots[kRotMax];
+  const int nrot = nch * 16 * KS;
+  const bool rot_lds = nrot <= kRotMax;
+  if (rot_lds)
+    for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
+  const float2* rtab = rot_lds ? static_cast<const float2*>(rots) : rot;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l15 = lane & 15, lq = lane >> 4;
+
+  for (int t = threadIdx.x; t < KS * PT * NG * 64; t += 256) {
+    const int ln = t & 63, r = t >> 6;
+    const int hl = r % NG, f = r / NG;  // f = ks * PT + pt
+    (&g0s[0][0][0][0])[t] = g0[(f * 2 + hl) * 64 + ln];
+  }
+  // conv B operand: Wc^T[i][o], lane holds i = 8lq + j of channel 16ot + l15
+  bf16x8 Wh[CO], Wl[CO];
+  float bo[CO];
+#pragma unroll
+  for (int ot = 0; ot < CO; ++ot) {
+    const int o = 16 * ot + l15;
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 8 * lq + 2 * j;
+      const float v0 = (o < Cout && i < Cin) ? wc[o * Cin + i] : 0.f;
+      const float v1 = (o < Cout && i + 1 < Cin) ? wc[o * Cin + i + 1] : 0.f;
+      split_pk(v0, v1, hi[j], lo[j]);
+    }
+    Wh[ot] = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+    Wl[ot] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
+    bo[ot] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+  }
+  // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not)
+  for (int t = threadIdx.x; t < 4 * 32 * XP * ES / 16; t += 256)
+    reinterpret_cast<uint4*>(&xs_raw[0][0])[t] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+  const int64_t u0 = gw * units / nw, u1 = (gw + 1) * units / nw;
+  if (u0 >= u1) return;  // no barriers below this point
+
+  char* xs = xs_raw[wv];
+  lds_v4s* xs_tr = (lds_v4s*)(xs_raw[wv]);
+  const int64_t plane = static_cast<int64_t>(H) * W * ES;  // bytes between channel planes
+  // the sparse second channel tile (Cout in (16, 20]) is packed 4 pixel tiles per lane-row
+  const bool pack = CO == 2 && Cout <= 20;
+  constexpr int LPR = CH / 8;    // lanes per staged channel row (8 pixels each)
+  constexpr int RPI = 64 / LPR;  // channel rows per wave instruction
+  const int st_ch = lane / LPR, st_px = (lane % LPR) * 8;  // staging role of this lane
+  float2 Yv[CO][KS][4];
+  int64_t cur_row = -1;
+  char* yrow = nullptr;  // &y[b][0][h][4 lq]
+
+  // x staging: this lane's 8-pixel pieces of channel rows st_ch + RPI*q of unit u, kept in
+  // registers one unit ahead so the loads are in flight while the previous chunk computes.
+  constexpr int NQ = 32 / RPI;
+  using Raw = typename std::conditional<BF, uint4, float4>::type;
+  constexpr int NR = BF ? 1 : 2;
+  Raw xr[NQ][NR];
+  auto load_x = [&](int64_t uu) {
+    const int64_t rr = uu / nch;
+    const int cw = static_cast<int>(uu - rr * nch) * CH + st_px;
+    const int64_t bb = rr / H, hh = rr - bb * H;
+    const char* src = static_cast<const char*>(x) + (((bb * Cin + st_ch) * H + hh) * W + cw) * ES;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (RPI * q >= Cin) break;  // wave-uniform
+      const bool ok = cw < W && st_ch + RPI * q < Cin;
+      const Raw* sp = reinterpret_cast<const Raw*>(ok ? src + RPI * q * plane : static_cast<const char*>(x));
+#pragma unroll
+      for (int t = 0; t < NR; ++t) {
+        xr[q][t] = sp[t];
+        if (!ok) xr[q][t] = Raw{};
+      }
+    }
+  };
+  load_x(u0);
+
+  for (int64_t u = u0; u < u1; ++u) {
+    const int64_t row = u / nch;
+    const int c = static_cast<int>(u - row * nch);
+    if (row != cur_row) {
+      cur_row = row;
+      const int64_t b = row / H, h = row - b * H;
+#pragma unroll
+      for (int ot = 0; ot < CO; ++ot)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
+            Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
+          }
+      yrow = static_cast<char*>(y) + ((b * Cout * H + h) * W + 4 * lq) * ES;
+    }
+    const int w0 = c * CH;
+    // ---- x chunk (channels x pixels) into this wave's LDS tile, then prefetch the next one
+    wave_lds_fence();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (RPI * q >= Cin) break;
+      const int ch = st_ch + RPI * q;
+      if (ch < Cin) {
+        Raw* dst = reinterpret_cast<Raw*>(xs + (ch * XP + st_px) * ES);
+#pragma unroll
+        for (int t = 0; t < NR; ++t) dst[t] = xr[q][t];
+      }
+    }
+    if (u + 1 < u1) load_x(u + 1);
+    // ---- rotate + split the spectral operand for this chunk
+    bf16x8 Bh[CO][KS], Bl[CO][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint32_t hi[CO][4], lo[CO][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float2 r = rtab[c * 16 * KS + 16 * ks + 4 * lq + q];
+#pragma unroll
+        for (int ot = 0; ot < CO; ++ot) {
+          const float2 v = Yv[ot][ks][q];
+          split_pk(v.x * r.x - v.y * r.y, v.x * r.y + v.y * r.x, hi[ot][q], lo[ot][q]);
+        }
+      }
+#pragma unroll
+      for (int ot = 0; ot < CO; ++ot) {
+        Bh[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(hi[ot][0], hi[ot][1], hi[ot][2], hi[ot][3]));
+        Bl[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(lo[ot][0], lo[ot][1], lo[ot][2], lo[ot][3]));
+      }
+    }
+    wave_lds_fence();
+    // ---- MFMA, 4 pixel tiles at a time: conv + spectral into bias-initialised accumulators
+    char* ychunk = yrow + static_cast<int64_t>(w0) * ES;
+#pragma unroll
+    for (int pg = 0; pg < PT / 4; ++pg) {
+      f32x4 acc[4][CO];
+#pragma unroll
+      for (int p4 = 0; p4 < 4; ++p4) {
+        const int pt = 4 * pg + p4;
+#pragma unroll
+        for (int ot = 0; ot < CO; ++ot) acc[p4][ot] = f32x4{bo[ot], bo[ot], bo[ot], bo[ot]};
+        bf16x8 ax, axl;
+        if constexpr (BF) {
+          // rows 8lq + (0..3) and 8lq + (4..7), cols 16pt..16pt+15: lane 4q'+p addresses row q', cols 4p..4p+3
+          const int e0 = (8 * lq + (l15 >> 2)) * XP + 16 * pt + 4 * (l15 & 3);
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(xs_tr + e0 / 4);
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(xs_tr + (e0 + 4 * XP) / 4);
+          const uint2 u0v = __builtin_bit_cast(uint2, a0), u1v = __builtin_bit_cast(uint2, a1);
+          ax = __builtin_bit_cast(bf16x8, make_uint4(u0v.x, u0v.y, u1v.x, u1v.y));
+        } else {
+          uint32_t hi[4], lo[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float* rp = reinterpret_cast<const float*>(xs) + (8 * lq + 2 * j) * XP + 16 * pt + l15;
+            split_pk(rp[0], rp[XP], hi[j], lo[j]);
+          }
+          ax = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+          axl = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
+        }
+#pragma unroll
+        for (int ot = 0; ot < CO; ++ot) {
+          acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wh[ot], acc[p4][ot], 0, 0, 0);
+          acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wl[ot], acc[p4][ot], 0, 0, 0);
+          if constexpr (!BF) acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(axl, Wh[ot], acc[p4][ot], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 gh = g0s[ks][pt][0][lane];
+#pragma unroll
+          for (int ot = 0; ot < CO; ++ot) {
+            acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, Bh[ot][ks], acc[p4][ot], 0, 0, 0);
+            acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, Bl[ot][ks], acc[p4][ot], 0, 0, 0);
+          }
+          if constexpr (PREC3) {
+            const bf16x8 gl = g0s[ks][pt][NG - 1][lane];
+#pragma unroll
+            for (int ot = 0; ot < CO; ++ot)
+              acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, Bh[ot][ks], acc[p4][ot], 0, 0, 0);
+          }
+        }
+      }
+      // ---- epilogue: activation + store, 4 consecutive pixels of one channel per lane
+      const int pxg = w0 + 64 * pg + 4 * lq;  // pixel of row i = 0 in tile p4 = 0
+#pragma unroll
+      for (int ot = 0; ot < CO; ++ot) {
+        if (ot == 1 && pack) break;
+        const int o = 16 * ot + l15;
+#pragma unroll
+        for (int p4 = 0; p4 < 4; ++p4) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
+          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(ychunk + o * plane + (64 * pg + 16 * p4) * ES, v);
+        }
+      }
+      if (CO == 2 && pack) {
+        // channel tile 1 holds <= 4 live columns: gather tiles p4 = 0..3 into lane groups l15 / 4
+        const int s = l15 >> 2, cc = l15 & 3;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a0 = acc[0][CO - 1][i], a1 = row_ror<4>(acc[1][CO - 1][i]), a2 = row_ror<8>(acc[2][CO - 1][i]),
+                      a3 = row_ror<12>(acc[3][CO - 1][i]);
+          v[i] = act<ACT>(s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3);
+        }
+        const int o = 16 + cc;
+        if (o < Cout && pxg + 16 * s < W) store4<BF>(ychunk + o * plane + (64 * pg + 16 * s) * ES, v);
+      }
+    }
+  }
+}
+
+template <bool BF, int KS, int CO>
+void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
+  constexpr int CH = Geo<BF>::CH;
+  const int nch = (p.W + CH - 1) / CH;
+  const int64_t units = static_cast<int64_t>(p.B) * p.H * nch;
+  // ~4 chunks per wave; every wave of the grid is resident at once for the FNO shapes
+  const int64_t nwg = std::min<int64_t>(std::max<int64_t>((units + 15) / 16, 1), 1 << 20);
+  const dim3 grid(static_cast<uint32_t>(nwg));
+  const float2* yw = static_cast<const float2*>(p.yw);
+  const bf16x8* g0 = static_cast<const bf16x8*>(p.g0);
+  const float2* rot = static_cast<const float2*>(p.rot);
+#define L_(A)                                                                                                     \
+  hipLaunchKernelGGL((fno_c2r_pw_kernel<BF, KS, CO, A>), grid, dim3(256), 0, st, yw, p.x, p.wc, p.bias, p.y, g0, rot, \
+                     p.Cin, p.Cout, p.H, p.W, p.m, nch, units)
+  if (!p.gelu) L_(0);
+  else if (BF) L_(2);
+  else L_(1);
+#undef L_
+}
+
+template <bool BF, int KS>
+void launch_co(const FnoC2RPwLaunch& p, hipStream_t st) {
+  if (p.Cout <= 16) launch_g<BF, KS, 1>(p, st);
+  else launch_g<BF, KS, 2>(p, st);
+}
+
+template <bool BF>
+void launch_ks(const FnoC2RPwLaunch& p, hipStream_t st) {
+  switch ((p.m + 15) / 16) {
+    case 1: launch_co<BF, 1>(p, st); break;
+    case 2: launch_co<BF, 2>(p, st); break;
+    case 3: launch_co<BF, 3>(p, st); break;
+    default: launch_co<BF, 4>(p, st); break;
+  }
+}
+
+}  // namespace
+
+bool fno_c2r_pw_supported(int cin, int cout, int m, int W) {
+  return cin >= 1 && cin <= 32 && cout >= 1 && cout <= 32 && m >= 1 && m <= 64 && 2 * (m - 1) <= W && W % 8 == 0;
+}
+
+void launch_fno_c2r_pw(const FnoC2RPwLaunch& p, void* stream) {
+  if (p.B == 0 || p.H == 0) return;
+  if (!fno_c2r_pw_supported(p.Cin, p.Cout, p.m, p.W))
+    throw std::runtime_error("amd_dft: fno_c2r_pw: needs Cin, Cout <= 32, m <= 64, W % 8 == 0");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (p.bf16) launch_ks<true>(p, st);
+  else launch_ks<false>(p, st);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: fno_c2r_pw launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft

@@ -7,6 +7,7 @@
 // GEMMs of its modes straight out of LDS.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <stdexcept>
 #include <string>
 
@@ -94,10 +95,55 @@ __global__ void __launch_bounds__(kNT) fno_mix_kernel(const float* __restrict__ 
   }
 }
 
+// Small batch (B <= 8): the MFMA M dimension (batch) would be >= 50% padding and the op is
+// a pure stream over the per-mode weights (Cin*Cout*M complex, 6.5 MB for 20x20x2048), so one
+// thread per (o, m) reads its Cin weights exactly once (coalesced along m) and keeps the B
+// accumulators in registers.
+template <int NB>
+__global__ void __launch_bounds__(256) fno_mix_small_kernel(const float2* __restrict__ x, const float2* __restrict__ w,
+                                                            float2* __restrict__ y, int B, int Cin, int Cout, int M) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(Cout) * M) return;
+  const int o = static_cast<int>(t / M), mm = static_cast<int>(t - static_cast<int64_t>(o) * M);
+  float2 acc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b] = make_float2(0.f, 0.f);
+#pragma unroll 8
+  for (int i = 0; i < Cin; ++i) {
+    const float2 wv = w[(static_cast<int64_t>(i) * Cout + o) * M + mm];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b < B) {
+        const float2 xv = x[(static_cast<int64_t>(b) * Cin + i) * M + mm];
+        acc[b].x = fmaf(xv.x, wv.x, fmaf(-xv.y, wv.y, acc[b].x));
+        acc[b].y = fmaf(xv.x, wv.y, fmaf(xv.y, wv.x, acc[b].y));
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    if (b < B) y[(static_cast<int64_t>(b) * Cout + o) * M + mm] = acc[b];
+}
+
 }  // namespace
 
 void launch_fno_mix(const FnoMixLaunch& p, void* stream) {
   if (p.B <= 0 || p.M <= 0) return;
+  if (p.B <= 8) {
+    const int64_t n = static_cast<int64_t>(p.Cout) * p.M;
+    const dim3 grid(static_cast<uint32_t>((n + 255) / 256));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const float2* xx = reinterpret_cast<const float2*>(p.x);
+    const float2* ww = reinterpret_cast<const float2*>(p.w);
+    float2* yy = reinterpret_cast<float2*>(p.y);
+    if (p.B <= 1) hipLaunchKernelGGL(fno_mix_small_kernel<1>, grid, dim3(256), 0, st, xx, ww, yy, p.B, p.Cin, p.Cout, p.M);
+    else if (p.B <= 2) hipLaunchKernelGGL(fno_mix_small_kernel<2>, grid, dim3(256), 0, st, xx, ww, yy, p.B, p.Cin, p.Cout, p.M);
+    else if (p.B <= 4) hipLaunchKernelGGL(fno_mix_small_kernel<4>, grid, dim3(256), 0, st, xx, ww, yy, p.B, p.Cin, p.Cout, p.M);
+    else hipLaunchKernelGGL(fno_mix_small_kernel<8>, grid, dim3(256), 0, st, xx, ww, yy, p.B, p.Cin, p.Cout, p.M);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: fno_mix launch: ") + hipGetErrorString(e));
+    return;
+  }
   const int K = 2 * p.Cin, N = 2 * p.Cout;
   const int Kp = (K + 3) & ~3, Bp = (p.B + 15) & ~15, Np = (N + 15) & ~15;
   const size_t lds = sizeof(float) * kMT * (static_cast<size_t>(Bp) * Kp + static_cast<size_t>(Kp) * Np +

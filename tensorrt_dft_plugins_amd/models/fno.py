@@ -4,14 +4,15 @@ The reference's motivating workload is FNO-family models (/root/reference/README
 TensorRT plugins supply the two FFT ends of every spectral layer
 (/root/reference/src/dft_plugins.cpp:171-195 R2C/C2R exec), and the per-mode complex multiply
 and the pointwise path run as ordinary TensorRT layers.  Here a spectral layer is three native
-kernels and nothing else:
+kernels per stage, and the full-resolution spectral output is never written to HBM:
 
-  1. pruned R2C over (H, W) -- only the kept ``[0, m1) u [H-m1, H)`` x ``[0, m2)`` modes are
-     produced (rows the mixer never reads are never transformed along H);
+  1. pruned R2C over (H, W): along W a truncated DFT on MFMA (``csrc/spectral/dft_gemm.hip``,
+     only the kept ``[0, m2)`` modes), then a pruned Stockham FFT along H keeping
+     ``[0, m1) u [H-m1, H)``;
   2. ``fno_mix``  -- the per-mode complex channel mixing on MFMA (``csrc/spectral/fno_mix.hip``);
-  3. pruned C2R back to ``H x W`` (the zero modes are never materialised),
-followed by ``fno_pointwise`` (1x1 conv + spectral add + bias + GELU in one HBM pass,
-``csrc/spectral/fno_pointwise.hip``).
+  3. pruned inverse FFT along H (``c2c_axis``), then ``fno_c2r_pw``: the inverse truncated DFT
+     along W on MFMA fused with the 1x1 convolution, bias and GELU
+     (``csrc/spectral/fno_c2r_pw.hip``) -- reads x, writes y, nothing else.
 
 Backends: ``"torch"`` (torch.fft + einsum + conv2d, the numerics oracle) and ``"amd"``.
 """
@@ -105,11 +106,25 @@ class FNOBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.backend == "amd":
-            spec = self.spectral.spectrum(x)
-            return torch.ops.amd_dft.fno_pointwise(spec, x, self.w.weight.float(), self.w.bias.float(),
-                                                   self.activation)
+            return self._forward_amd(x)
         y = self.spectral(x).to(x.dtype) + self.w(x)
         return F.gelu(y) if self.activation else y
+
+    def _forward_amd(self, x: torch.Tensor) -> torch.Tensor:
+        """pruned R2C (MFMA DFT-GEMM along W + pruned FFT along H) -> MFMA mode mixing ->
+        pruned inverse FFT along H -> fused [inverse DFT-GEMM along W + 1x1 conv + bias + GELU]."""
+        sp = self.spectral
+        B, C, H, W = x.shape
+        sp._check(H, W)
+        m1, m2 = sp.modes1, sp.modes2
+        ops = torch.ops.amd_dft
+        xw = ops.dftw_r2c(x, m2, 1.0)  # [B, Cin, H, m2, 2]  truncated DFT along W on MFMA
+        xm = ops.c2c_axis(xw, 2, H, H, 0, m1, m1, False, 1.0)  # [B, Cin, 2*m1, m2, 2]
+        ym = S.fno_spectral_mix(xm.reshape(B, C, 2 * m1 * m2, 2), sp._packed_weight())
+        ym = ym.reshape(B, sp.out_ch, 2 * m1, m2, 2)
+        yw = ops.c2c_axis(ym, 2, H, m1, m1, H, 0, True, 1.0 / (H * W))  # [B, Cout, H, m2, 2]
+        return ops.fno_c2r_pw(yw, x, self.w.weight.reshape(self.w.out_channels, -1).float(), self.w.bias.float(),
+                              self.activation)
 
 
 class FNO2d(nn.Module):

@@ -109,7 +109,8 @@ def test_modes_too_large():
 @pytest.mark.gpu
 def test_fno_mix_kernel_gpu(device):
     torch.manual_seed(7)
-    for B, Ci, Co, M in [(1, 20, 20, 2048), (4, 20, 20, 100), (32, 20, 20, 37), (3, 7, 5, 19), (2, 32, 16, 64)]:
+    for B, Ci, Co, M in [(1, 20, 20, 2048), (4, 20, 20, 100), (32, 20, 20, 37), (3, 7, 5, 19), (2, 32, 16, 64),
+                         (12, 20, 20, 64), (8, 20, 20, 2048)]:
         xm = torch.randn(B, Ci, M, 2)
         w = torch.randn(Ci, Co, M, 2)
         ref = torch.ops.amd_dft.fno_mix(xm, w)
@@ -158,3 +159,75 @@ def test_fno2d_gpu(device):
         ref = m(x)
         out = m.set_backend("amd")(x)
     assert rel_l2(out, ref) < 1e-4
+
+
+def test_c2c_axis_cpu():
+    torch.manual_seed(11)
+    x = torch.randn(2, 3, 10, 4, 2)
+    full = torch.fft.fft(torch.view_as_complex(x).to(torch.complex128), dim=2)
+    y = torch.ops.amd_dft.c2c_axis(x, 2, 10, 10, 0, 3, 2, False, 1.0)
+    ref = torch.cat([full[:, :, :3], full[:, :, -2:]], 2)
+    assert rel_l2(torch.view_as_complex(y.contiguous()), ref) < 1e-6
+    z = torch.ops.amd_dft.c2c_axis(y, 2, 10, 3, 2, 10, 0, True, 0.1)
+    pad = torch.zeros(2, 3, 10, 4, dtype=torch.complex128)
+    pad[:, :, :3] = ref[:, :, :3]
+    pad[:, :, -2:] = ref[:, :, 3:]
+    assert rel_l2(torch.view_as_complex(z.contiguous()), torch.fft.ifft(pad, dim=2)) < 1e-6
+
+
+def test_dftw_r2c_cpu():
+    x = torch.randn(3, 64)
+    y = torch.ops.amd_dft.dftw_r2c(x, 9, 0.5)
+    ref = 0.5 * torch.fft.rfft(x.double())[:, :9]
+    assert rel_l2(torch.view_as_complex(y.contiguous()), ref) < 1e-6
+
+
+def test_fno_c2r_pw_cpu():
+    torch.manual_seed(12)
+    B, Ci, Co, H, W, m = 2, 5, 3, 4, 16, 6
+    yw = torch.randn(B, Co, H, m, 2)
+    x = torch.randn(B, Ci, H, W)
+    wc = torch.randn(Co, Ci)
+    b = torch.randn(Co)
+    y = torch.ops.amd_dft.fno_c2r_pw(yw, x, wc, b, True)
+    full = torch.zeros(B, Co, H, W // 2 + 1, dtype=torch.complex128)
+    full[..., :m] = torch.view_as_complex(yw.double())
+    spec = torch.fft.irfft(full, n=W, dim=3, norm="forward")
+    ref = F.gelu(spec + F.conv2d(x.double(), wc.double()[:, :, None, None], b.double()))
+    assert rel_l2(y, ref) < 1e-6
+
+
+@pytest.mark.gpu
+def test_dftw_r2c_gemm_gpu(device):
+    """Pruned R2C along the innermost axis takes the MFMA DFT-GEMM path; vs torch.fft (fp64)."""
+    from tensorrt_dft_plugins_amd.ops import dft as D
+
+    torch.manual_seed(13)
+    for (R, W, m) in [(14400, 1440, 32), (37, 720, 16), (5, 64, 8), (100, 1440, 64), (16, 200, 20)]:
+        x = torch.randn(R, W)
+        ref = torch.fft.rfft(x.double(), dim=1)[:, :m]
+        for dt, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-6)):
+            xd = x.to(dt)
+            refd = torch.fft.rfft(xd.double(), dim=1)[:, :m]
+            if dt == torch.bfloat16:  # automatic for bf16 inputs
+                out = D.rfftn_pruned(xd.to(device), [1], [(m, 0)])
+            else:  # explicit op for fp32 (bf16x3 split operands)
+                out = torch.ops.amd_dft.dftw_r2c(xd.to(device), m, 1.0)
+            assert out.shape == (R, m, 2)
+            assert rel_l2(torch.view_as_complex(out.cpu().contiguous()), refd) < tol, (R, W, m, dt)
+
+
+@pytest.mark.gpu
+def test_fno_c2r_pw_kernel_gpu(device):
+    torch.manual_seed(14)
+    for (B, Ci, Co, H, W, m, gelu) in [(1, 20, 20, 8, 1440, 32, True), (2, 7, 13, 3, 200, 20, False),
+                                       (1, 32, 32, 2, 720, 64, True), (3, 4, 16, 5, 64, 5, True)]:
+        yw = torch.randn(B, Co, H, m, 2) / W
+        wc = torch.randn(Co, Ci) / Ci ** 0.5
+        b = torch.randn(Co)
+        for dt, tol in ((torch.float32, 2e-5), (torch.bfloat16, 1e-2)):
+            x = torch.randn(B, Ci, H, W).to(dt)
+            ref = torch.ops.amd_dft.fno_c2r_pw(yw, x.float(), wc, b, gelu)
+            out = torch.ops.amd_dft.fno_c2r_pw(yw.to(device), x.to(device), wc.to(device), b.to(device), gelu)
+            assert out.dtype == dt
+            assert rel_l2(out.float(), ref) < tol, (B, Ci, Co, H, W, m, dt)
