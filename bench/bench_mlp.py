@@ -50,3 +50,19 @@ for k, f in variants.items():
 y = torch._addmm_activation(b1, x, w1.t(), use_gelu=True)
 print("addmm_act vs erf gelu max abs diff", (y.float() - ref.float()).abs().max().item(),
       "vs tanh", (y.float() - F.gelu(F.linear(x, w1, b1), approximate="tanh").float()).abs().max().item())
+
+# operand-layout variants (hipBLASLt picks different kernels per transpose case)
+w1t = w1.t().contiguous()  # [C, Hd]
+w2t = w2.t().contiguous()  # [Hd, C]
+hid = ref
+layout = {
+    "fc1 x@W^T (TN)": lambda: torch.mm(x, w1.t()),
+    "fc1 x@Wt (NN)": lambda: torch.mm(x, w1t),
+    "fc1 (W x^T)^T": lambda: torch.mm(w1, x.t()),
+    "fc2 h@W^T (TN)": lambda: torch.mm(hid, w2.t()),
+    "fc2 h@Wt (NN)": lambda: torch.mm(hid, w2t),
+    "fc2 (W h^T)^T": lambda: torch.mm(w2, hid.t()),
+}
+for k, f in layout.items():
+    ms = t(f)
+    print(f"{k:18s} {ms:8.3f} ms  {2 * M * C * Hd / ms / 1e9:7.1f} TFLOP/s")

@@ -31,6 +31,7 @@
 
 #include "../fft/fft_plan.h"
 #include "../spectral/dft_gemm.h"
+#include "checks.h"
 #include "plan_cache.h"
 
 namespace amd_dft {
@@ -231,7 +232,7 @@ at::Tensor dftw_r2c_cuda(const at::Tensor& x_, int64_t m, double scale) {
   if (x.numel() == 0) return out;
   DimSpec s{static_cast<int>(x.dim() - 1), W, m, 0};
   run_dftw(x, out, s, static_cast<float>(scale));
-  return out;
+  return checked(out, "dftw_r2c");
 }
 
 at::Tensor dftw_r2c_cpu(const at::Tensor& x, int64_t m, double scale) {
@@ -280,7 +281,7 @@ at::Tensor r2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, double scale, at:
     cur = nxt;
     cur_t = out;
   }
-  return cur_t;
+  return checked(cur_t, "r2c");
 }
 
 at::Tensor c2r_cuda_impl(const at::Tensor& x_, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
@@ -330,7 +331,7 @@ at::Tensor c2r_cuda_impl(const at::Tensor& x_, at::IntArrayRef dim, at::IntArray
     }
     cur = nxt;
   }
-  return cur_t;
+  return checked(cur_t, "c2r");
 }
 
 at::Tensor c2r_cuda(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
@@ -366,7 +367,7 @@ at::Tensor c2c_cuda(const at::Tensor& x_, at::IntArrayRef dim, bool inverse, dou
              final_pass ? static_cast<float>(scale) : 1.0f, inverse);
     cur_t = out;
   }
-  return cur_t;
+  return checked(cur_t, "c2c");
 }
 
 // Pruned C2C along one axis: input stores modes [0, in_lo) u [n - in_hi, n) of a length-n
@@ -397,7 +398,7 @@ at::Tensor c2c_axis_cuda(const at::Tensor& x_, int64_t dim, int64_t n, int64_t i
   if (out.numel() == 0) return out;
   run_pass(Kind::C2C, x, out, cur, nxt, static_cast<int>(dim), n, static_cast<int>(in_lo), static_cast<int>(in_hi),
            static_cast<int>(out_lo), static_cast<int>(out_hi), static_cast<float>(scale), inverse);
-  return out;
+  return checked(out, "c2c_axis");
 }
 
 at::Tensor c2c_axis_cpu(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,

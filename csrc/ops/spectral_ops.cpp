@@ -9,6 +9,7 @@
 
 #include "../spectral/dft_gemm.h"
 #include "../spectral/spectral.h"
+#include "checks.h"
 #include "plan_cache.h"
 
 namespace amd_dft {
@@ -76,7 +77,7 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   p.NB = static_cast<int>(NB);
   p.lambda = static_cast<float>(lam);
   launch_afno_spectral(p, c10::hip::getCurrentHIPStream(xw.device().index()).stream());
-  return y;
+  return checked(y, "afno_spectral");
 }
 
 bool afno_spectral_ok(int64_t H, int64_t block_size) {
@@ -117,7 +118,7 @@ at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
   p.Cout = static_cast<int>(Cout);
   p.M = static_cast<int>(M);
   launch_fno_mix(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
-  return y;
+  return checked(y, "fno_mix");
 }
 
 at::Tensor fno_mix_meta(const at::Tensor& x, const at::Tensor& w) {
@@ -180,7 +181,7 @@ at::Tensor fno_pointwise_cuda(const c10::optional<at::Tensor>& spec_, const at::
   p.bf16 = x.scalar_type() == at::kBFloat16;
   p.gelu = gelu;
   launch_fno_pointwise(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
-  return y;
+  return checked(y, "fno_pointwise");
 }
 
 at::Tensor fno_pointwise_meta(const c10::optional<at::Tensor>& spec, const at::Tensor& x, const at::Tensor& w,
@@ -256,7 +257,7 @@ at::Tensor fno_c2r_pw_cuda(const at::Tensor& yw_, const at::Tensor& x_, const at
   p.bf16 = x.scalar_type() == at::kBFloat16;
   p.gelu = gelu;
   launch_fno_c2r_pw(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
-  return y;
+  return checked(y, "fno_c2r_pw");
 }
 
 at::Tensor fno_c2r_pw_meta(const at::Tensor& yw, const at::Tensor& x, const at::Tensor& wc,

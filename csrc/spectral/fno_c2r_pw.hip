@@ -174,7 +174,8 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
   const int st_ch = lane / LPR, st_px = (lane % LPR) * 8;  // staging role of this lane
   float2 Yv[CO][KS][4];
   int64_t cur_row = -1;
-  char* yrow = nullptr;  // &y[b][0][h][4 lq]
+  char* yrow[CO];        // &y[b][16 ot + l15][h][4 lq]  (clamped to a valid channel)
+  char* yrowp = nullptr;  // same for the packed channel tile: channel 16 + (l15 & 3)
 
   // x staging: this lane's 8-pixel pieces of channel rows st_ch + RPI*q of unit u, kept in
   // registers one unit ahead so the loads are in flight while the previous chunk computes.
@@ -216,7 +217,10 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
             const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
             Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
           }
-      yrow = static_cast<char*>(y) + ((b * Cout * H + h) * W + 4 * lq) * ES;
+      char* y0 = static_cast<char*>(y) + ((b * Cout * H + h) * W + 4 * lq) * ES;
+#pragma unroll
+      for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
+      yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
     }
     const int w0 = c * CH;
     // ---- x chunk (channels x pixels) into this wave's LDS tile, then prefetch the next one
@@ -254,7 +258,6 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
     }
     wave_lds_fence();
     // ---- MFMA, 4 pixel tiles at a time: conv + spectral into bias-initialised accumulators
-    char* ychunk = yrow + static_cast<int64_t>(w0) * ES;
 #pragma unroll
     for (int pg = 0; pg < PT / 4; ++pg) {
       f32x4 acc[4][CO];
@@ -284,8 +287,10 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
 #pragma unroll
         for (int ot = 0; ot < CO; ++ot) {
           acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wh[ot], acc[p4][ot], 0, 0, 0);
-          acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wl[ot], acc[p4][ot], 0, 0, 0);
-          if constexpr (!BF) acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(axl, Wh[ot], acc[p4][ot], 0, 0, 0);
+          if constexpr (!BF) {  // bf16 output: bf16 conv weights, as a bf16 nn.Conv2d has
+            acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wl[ot], acc[p4][ot], 0, 0, 0);
+            acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(axl, Wh[ot], acc[p4][ot], 0, 0, 0);
+          }
         }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -314,7 +319,7 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
-          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(ychunk + o * plane + (64 * pg + 16 * p4) * ES, v);
+          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
         }
       }
       if (CO == 2 && pack) {
@@ -328,7 +333,7 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
           v[i] = act<ACT>(s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3);
         }
         const int o = 16 + cc;
-        if (o < Cout && pxg + 16 * s < W) store4<BF>(ychunk + o * plane + (64 * pg + 16 * s) * ES, v);
+        if (o < Cout && pxg + 16 * s < W) store4<BF>(yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
       }
     }
   }

@@ -153,3 +153,12 @@ def test_planner_factorisation():
     # FourCastNet sizes need the mixed radices: three passes each
     assert "radices=[8,9,10]" in torch.ops.amd_dft.plan_info(720)
     assert len(re.search(r"radices=\[([0-9,]*)\]", torch.ops.amd_dft.plan_info(1440)).group(1).split(",")) == 3
+
+
+def test_utils_runtime_helpers():
+    from tensorrt_dft_plugins_amd.utils import check_finite, env_report
+
+    assert "torch" in env_report()
+    check_finite(torch.ones(3))
+    with pytest.raises(FloatingPointError):
+        check_finite(torch.tensor([1.0, float("nan")]))

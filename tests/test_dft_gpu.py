@@ -190,3 +190,21 @@ def test_fixed_vs_generic_paths(device, env, monkeypatch):
         assert rel_l2(z, x) < 5e-6
         c = torch.randn(*shape, dtype=torch.complex64, device=device)
         assert rel_l2(tdp.fftn(c, dim=dims), torch.fft.fftn(c.cpu().to(torch.complex128), dim=dims)) < 5e-6
+
+
+def test_finite_check_mode_gpu(device):
+    """MI_DFT_CHECK_FINITE=1 turns a NaN output into a Python error (opt-in)."""
+    import subprocess
+    import sys
+
+    code = ("import torch, tensorrt_dft_plugins_amd as t; t.load_plugins();"
+            "x = torch.randn(4, 64, device='cuda'); x[1, 3] = float('nan');"
+            "ok = torch.ops.amd_dft.r2c(torch.randn(4, 64, device='cuda'), [1]); torch.cuda.synchronize();\n"
+            "try:\n    torch.ops.amd_dft.r2c(x, [1]); print('NOERR')\n"
+            "except RuntimeError as e:\n    print('RAISED', 'NaN/Inf' in str(e))\n")
+    import os
+
+    env = dict(os.environ, MI_DFT_CHECK_FINITE="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert "RAISED True" in r.stdout, r.stdout + r.stderr[-2000:]

@@ -92,3 +92,18 @@ def test_bench_harness_torchrun_gloo():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["parallelism"] == "dp2"
     assert d["value"] > 0 and d["higher_is_better"] is True
+
+
+def test_rccl_sweep_harness_gloo():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench", "bench_rccl.py"), "--mb", "0.01",
+           "--iters", "2", "--dtype", "fp32"]
+    env = dict(os.environ)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and lines[0]["world"] == 2 and lines[0]["backend"] == "gloo"
