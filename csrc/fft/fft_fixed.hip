@@ -62,7 +62,11 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     const int64_t waves = wgs * ((c.TP * c.T + 63) / 64);
     // enough waves to put >= 2 on every SIMD (1024 SIMDs), then the widest tile
     // (coalescing, fewer twiddle re-reads); otherwise the most waves.
-    const double score = waves >= 2048 ? 1e12 + c.T * 1e6 + c.TP : static_cast<double>(waves);
+    // Measured on the AFNO W-transforms ([32,90,180,768] bf16, bench/bench_afno_w.py): the
+    // C2R with fused addends prefers 32-channel tiles, the R2C 16 (wider R2C tiles lose).
+    const int t_pref = (cols && d.kind == Kind::R2C) ? 16 : 1 << 30;
+    const double tw = c.T <= t_pref ? c.T : -c.T;
+    const double score = waves >= 2048 ? 1e12 + tw * 1e6 + c.TP : static_cast<double>(waves);
     if (score > best_score) {
       best_score = score;
       best = i;
