@@ -63,13 +63,27 @@ def _obj_path(src: str) -> str:
     return os.path.join(BUILD, rel + ".o")
 
 
+def _file_flags(src: str) -> list:
+    """Per-file hipcc flags from a ``// amd_dft-build-flags: ...`` line in the first lines of the
+    source (e.g. -fno-slp-vectorize where SLP-packed f32 ops sit between MFMAs)."""
+    with open(src) as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// amd_dft-build-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
     obj = _obj_path(src)
     cmd = [_hipcc(), "-c", "-fPIC", "-std=c++17", "-O3", "-Wall", "-Wno-unused-function",
            "-Wno-unused-variable", "-Wno-sign-compare", "-I" + CSRC,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-o", obj]
     if src.endswith(".hip"):
-        cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        # -fno-slp-vectorize: SLP packs f32 pairs into v_pk_* ops plus the v_mov shuffles to feed
+        # them; measured faster without on every kernel family here (scripts/ab_slp.sh:
+        # afno 561->537 us, rfft2 18.8->17.9 us, AFNO R2C-W 387->320 us).
+        cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
+        cmd += _file_flags(src) + os.environ.get("MI_DFT_HIPCC_EXTRA", "").split()
     else:
         # host-only C++ that includes HIP runtime headers (torch's c10/hip)
         rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
