@@ -21,6 +21,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <list>
 #include <memory>
@@ -77,9 +78,23 @@ at::Tensor alloc_complex(const std::vector<int64_t>& logical, const at::TensorOp
   return at::empty(s, o.dtype(dt));
 }
 
+void run_pass_large(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
+                    const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
+                    int out_hi, float scale, bool inverse, const void* add1, const void* add2);
+
+int64_t lds_limit() {
+  static const int64_t lim = max_lds_length();
+  return lim;
+}
+
 void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
               const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
               int out_hi, float scale, bool inverse, const void* add1 = nullptr, const void* add2 = nullptr) {
+  if (L > lds_limit()) {
+    run_pass_large(kind, in, out, in_shape, out_shape, axis, L, in_lo, in_hi, out_lo, out_hi, scale, inverse, add1,
+                   add2);
+    return;
+  }
   auto dp = get_plan(L, in.device());
   PassDesc d;
   d.kind = kind;
@@ -108,6 +123,141 @@ void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
     if (a == "notw" || a == "io") d.tw_count = 0;
   }
   launch_fft_pass(d, c10::hip::getCurrentHIPStream(in.device().index()).stream());
+}
+
+// ------------------------------------------------------------------ lengths beyond one LDS-resident pass
+// cuFFT (the reference's backend) takes any length; the Stockham kernels keep a whole signal in
+// LDS (<= lds_limit() points).  Longer transforms are composed from LDS-resident ones:
+//  * four-step (Bailey): N = N1*N2 -> N1-point FFTs along the strided axis, twiddle
+//    e^{-+2 pi i k1 n2 / N}, N2-point FFTs, transpose (N1, N2 recurse if still too long);
+//  * Bluestein (chirp-z) when N has no usable factor (a large prime): a length-M >= 2N-1
+//    smooth convolution done with the same kernels.
+// The glue (twiddle multiply, transposes, padding) is ATen elementwise work on the device.
+at::Tensor c2c_full(const at::Tensor& z, bool inverse);
+
+at::Tensor c2c_lastdim_kernels(const at::Tensor& z, int axis, bool inverse) {
+  // z: complex64 contiguous; transform along `axis` with the native pass (recurses if long)
+  at::Tensor zr = at::view_as_real(z);
+  std::vector<int64_t> shape(z.sizes().begin(), z.sizes().end());
+  at::Tensor out = at::empty_like(zr);
+  const int64_t n = shape[axis];
+  run_pass(Kind::C2C, zr, out, shape, shape, axis, n, static_cast<int>(n), 0, static_cast<int>(n), 0, 1.f, inverse);
+  return at::view_as_complex(out);
+}
+
+int64_t split_length(int64_t N) {
+  // divisor closest to sqrt(N) with N1 <= limit (N2 may recurse); 0 if N is prime
+  int64_t best = 0;
+  const double r = std::sqrt(static_cast<double>(N));
+  for (int64_t d = 2; d * d <= N; ++d) {
+    if (N % d) continue;
+    for (int64_t c : {d, N / d}) {
+      if (c > lds_limit() || c == N) continue;
+      if (!best || std::fabs(static_cast<double>(c) - r) < std::fabs(static_cast<double>(best) - r)) best = c;
+    }
+  }
+  return best;
+}
+
+int64_t smooth_at_least(int64_t n) {
+  for (int64_t m = n;; ++m) {
+    int64_t k = m;
+    for (int64_t p : {2, 3, 5}) while (k % p == 0) k /= p;
+    if (k == 1) return m;
+  }
+}
+
+at::Tensor phase_table(int64_t rows, int64_t cols, int64_t N, double sign, const at::Device& dev) {
+  // exp(sign * 2 pi i * ((r * c) mod N) / N), exact integer angle reduction, fp64 trig
+  auto o = at::TensorOptions().dtype(at::kLong).device(dev);
+  at::Tensor idx = at::remainder(at::arange(rows, o).unsqueeze(1) * at::arange(cols, o).unsqueeze(0), N);
+  at::Tensor ang = idx.to(at::kDouble) * (sign * 2.0 * M_PI / static_cast<double>(N));
+  return at::polar(at::ones_like(ang), ang).to(at::kComplexFloat);
+}
+
+at::Tensor four_step(const at::Tensor& z, int64_t N1, bool inverse) {
+  const int64_t N = z.size(-1), N2 = N / N1;
+  std::vector<int64_t> s3(z.sizes().begin(), z.sizes().end() - 1);
+  s3.push_back(N1);
+  s3.push_back(N2);
+  at::Tensor a = c2c_lastdim_kernels(z.reshape(s3).contiguous(), static_cast<int>(s3.size()) - 2, inverse);
+  a = a * phase_table(N1, N2, N, inverse ? 1.0 : -1.0, z.device());
+  a = c2c_lastdim_kernels(a.contiguous(), static_cast<int>(s3.size()) - 1, inverse);
+  return a.transpose(-1, -2).reshape(z.sizes()).contiguous();
+}
+
+at::Tensor bluestein(const at::Tensor& z, bool inverse) {
+  if (inverse) return at::conj_physical(bluestein(at::conj_physical(z), false));
+  const int64_t N = z.size(-1), M = smooth_at_least(2 * N - 1);
+  auto lo = at::TensorOptions().dtype(at::kLong).device(z.device());
+  at::Tensor n = at::arange(N, lo);
+  at::Tensor ang = at::remainder(n * n, 2 * N).to(at::kDouble) * (-M_PI / static_cast<double>(N));
+  at::Tensor w = at::polar(at::ones_like(ang), ang).to(at::kComplexFloat);  // e^{-i pi n^2 / N}
+  std::vector<int64_t> sa(z.sizes().begin(), z.sizes().end());
+  sa.back() = M;
+  at::Tensor a = at::zeros(sa, z.options());
+  a.narrow(-1, 0, N).copy_(z * w);
+  at::Tensor b = at::zeros({M}, z.options());
+  at::Tensor cw = at::conj_physical(w);
+  b.narrow(0, 0, N).copy_(cw);
+  if (N > 1) b.narrow(0, M - N + 1, N - 1).copy_(cw.narrow(0, 1, N - 1).flip(0));
+  at::Tensor fa = c2c_full(a, false), fb = c2c_full(b.unsqueeze(0), false).squeeze(0);
+  at::Tensor c = c2c_full((fa * fb).contiguous(), true) * (1.0 / static_cast<double>(M));
+  return (c.narrow(-1, 0, N) * w).contiguous();
+}
+
+at::Tensor c2c_full(const at::Tensor& z, bool inverse) {
+  // z: complex64 contiguous [..., N]; unnormalised transform along the last dim
+  const int64_t N = z.size(-1);
+  if (N <= lds_limit()) return c2c_lastdim_kernels(z, static_cast<int>(z.dim()) - 1, inverse);
+  const int64_t N1 = split_length(N);
+  return N1 ? four_step(z, N1, inverse) : bluestein(z, inverse);
+}
+
+void run_pass_large(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
+                    const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
+                    int out_hi, float scale, bool inverse, const void* add1, const void* add2) {
+  const auto cf = in.options().dtype(at::kComplexFloat);
+  std::vector<int64_t> full_shape = in_shape;
+  full_shape[axis] = L;
+  at::Tensor z;
+  if (kind == Kind::R2C) {
+    at::Tensor xr = in.to(at::kFloat).reshape(in_shape);
+    z = at::complex(xr, at::zeros_like(xr));
+  } else {
+    std::vector<int64_t> s2 = in_shape;
+    s2.push_back(2);
+    at::Tensor st = at::view_as_complex(in.to(at::kFloat).reshape(s2).contiguous());
+    z = at::zeros(full_shape, cf);
+    if (kind == Kind::C2C) {
+      if (in_lo) z.narrow(axis, 0, in_lo).copy_(st.narrow(axis, 0, in_lo));
+      if (in_hi) z.narrow(axis, L - in_hi, in_hi).copy_(st.narrow(axis, in_lo, in_hi));
+    } else {  // C2R: Hermitian extension of the stored half spectrum
+      const int64_t kmax = std::min<int64_t>(in_lo, L / 2 + 1);
+      z.narrow(axis, 0, kmax).copy_(st.narrow(axis, 0, kmax));
+      const int64_t m = std::min<int64_t>(kmax, (L + 1) / 2) - 1;
+      if (m > 0) z.narrow(axis, L - m, m).copy_(at::conj_physical(st.narrow(axis, 1, m).flip({axis})));
+    }
+  }
+  at::Tensor r = c2c_full(z.movedim(axis, -1).contiguous(), inverse).movedim(-1, axis);
+  if (scale != 1.f) r = r * static_cast<double>(scale);
+  if (kind == Kind::C2R) {
+    at::Tensor y = at::real(r);
+    for (const void* ad : {add1, add2})
+      if (ad) y = y + at::from_blob(const_cast<void*>(ad), out_shape, out.options()).to(at::kFloat);
+    out.copy_(y.reshape(out.sizes()));
+    return;
+  }
+  at::Tensor o;
+  if (kind == Kind::R2C) {
+    o = r.narrow(axis, 0, out_lo);
+  } else {
+    std::vector<at::Tensor> parts;
+    if (out_lo) parts.push_back(r.narrow(axis, 0, out_lo));
+    if (out_hi) parts.push_back(r.narrow(axis, L - out_hi, out_hi));
+    o = parts.size() == 1 ? parts[0] : at::cat(parts, axis);
+  }
+  out.copy_(at::view_as_real(o.contiguous()).reshape(out.sizes()));
 }
 
 // ------------------------------------------------------------------ shape logic (shared)

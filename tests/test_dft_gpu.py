@@ -208,3 +208,34 @@ def test_finite_check_mode_gpu(device):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=root)
     assert "RAISED True" in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("n", [6553, 8192, 8198, 10007, 20000, 65536, 100003])
+def test_long_lengths_four_step_bluestein(device, n):
+    """Lengths beyond one LDS-resident pass (limit 6552): four-step composition, and Bluestein
+    for primes (10007, 100003) -- cuFFT, the reference's backend, accepts any length."""
+    torch.manual_seed(n % 97)
+    x = torch.randn(2, n, device=device)
+    y = tdp.rfft(x)
+    ref = torch.fft.rfft(x.double().cpu())
+    tol = 2e-5 if n in (10007, 100003, 6553) else 5e-6
+    assert rel_l2(y, ref) < tol, n
+    xr = tdp.irfft(y, n=n)
+    assert rel_l2(xr, x) < tol, n
+    z = torch.randn(2, n, dtype=torch.complex64, device=device)
+    assert rel_l2(tdp.fft(z), torch.fft.fft(z.cpu().to(torch.complex128))) < tol, n
+    assert rel_l2(tdp.ifft(z), torch.fft.ifft(z.cpu().to(torch.complex128))) < tol, n
+
+
+def test_long_length_2d_and_pruned(device):
+    torch.manual_seed(3)
+    x = torch.randn(2, 12, 9000, device=device)
+    y = tdp.rfft2(x)
+    assert rel_l2(y, torch.fft.rfft2(x.double().cpu())) < 1e-5
+    assert rel_l2(tdp.irfft2(y, s=(12, 9000)), x) < 1e-5
+    from tensorrt_dft_plugins_amd.ops import dft as D
+
+    yp = D.rfftn_pruned(x, [1, 2], [(3, 2), (40, 0)])
+    full = torch.fft.rfft2(x.double().cpu())
+    ref = torch.cat([full[:, :3, :40], full[:, -2:, :40]], 1)
+    assert rel_l2(yp, ref) < 1e-5
