@@ -1,0 +1,61 @@
+"""Hand-written fused-epilogue GEMM vs hipBLASLt (torch) on the FourCastNet MLP shapes,
+interleaved rounds in one process.
+
+Usage: python bench/bench_gemm.py [--rows 518400]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import tensorrt_dft_plugins_amd as tdp  # noqa: E402
+from bench.bench_fft import time_graph  # noqa: E402
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=32 * 16200)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args(argv)
+    tdp.load_plugins()
+    M, C, Hd = a.rows, 768, 3072
+    dev = "cuda"
+    x = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    h = torch.randn(M, Hd, device=dev).to(torch.bfloat16)
+    w1 = (torch.randn(Hd, C, device=dev) * 0.02).to(torch.bfloat16)
+    w2 = (torch.randn(C, Hd, device=dev) * 0.02).to(torch.bfloat16)
+    b1 = (torch.randn(Hd, device=dev) * 0.02)
+    b2 = (torch.randn(C, device=dev) * 0.02)
+    b1h, b2h = b1.to(torch.bfloat16), b2.to(torch.bfloat16)
+    ops = torch.ops.amd_dft
+    v = {
+        "fc1_gelu amd": lambda: ops.linear(x, w1, b1, 1, None),
+        "fc1_gelu hipblaslt": lambda: torch._addmm_activation(b1h, x, w1.t(), use_gelu=True),
+        "fc1 amd": lambda: ops.linear(x, w1, b1, 0, None),
+        "fc1 hipblaslt": lambda: F.linear(x, w1, b1h),
+        "fc2 amd": lambda: ops.linear(h, w2, b2, 0, None),
+        "fc2 hipblaslt": lambda: F.linear(h, w2, b2h),
+    }
+    res = {k: [] for k in v}
+    for _ in range(a.rounds):
+        for k, f in v.items():
+            res[k].append(time_graph(f, 3))
+    flop = 2.0 * M * C * Hd
+    out = {}
+    for k, t in res.items():
+        med = statistics.median(t)
+        out[k] = {"us": round(med, 1), "TFLOPs": round(flop / med / 1e6, 1)}
+        print(f"{k:22s} {med:9.1f} us  {flop / med / 1e6:7.1f} TFLOP/s", flush=True)
+    y = ops.linear(x[:4096], w1, b1, 1, None).float()
+    ref = F.gelu(F.linear(x[:4096].float(), w1.float(), b1))
+    print("rel err", ((y - ref).norm() / ref.norm()).item())
+    return out
+
+
+if __name__ == "__main__":
+    main()

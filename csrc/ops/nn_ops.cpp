@@ -1,8 +1,13 @@
-// Torch op layer for the non-spectral FourCastNet helpers: patchify / un-patchify.
+// Torch op layer for the non-spectral FourCastNet pieces: patchify / un-patchify and the
+// fused-epilogue linear layer.
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
+
+#include <algorithm>
+
+#include "../nn/gemm.h"
 
 namespace amd_dft {
 void launch_patch_remap(const void* src, void* dst, int64_t B, int C, int h, int w, bool to_tokens, void* stream);
@@ -58,22 +63,86 @@ at::Tensor unpatchify_meta(const at::Tensor& t, int64_t C, int64_t h, int64_t w,
   return at::empty({t.numel() / (h * w * C * p * p), C, h * p, w * p}, t.options());
 }
 
+
+// ------------------------------------------------------------------ fused-epilogue linear
+// y = act(x @ w^T + bias) (+ residual); x [..., K] bf16, w [N, K] bf16, y [..., N] bf16.
+// act: 0 none, 1 GELU (erf).  CUDA: the hand-written MFMA GEMM (csrc/nn/gemm.hip) when
+// N % 256 == 0 and K % 64 == 0, otherwise hipBLASLt through at::linear.
+at::Tensor linear_ref(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
+                      const c10::optional<at::Tensor>& residual) {
+  at::Tensor y = at::linear(x.to(at::kFloat), w.to(at::kFloat),
+                            bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
+                                                                : c10::nullopt);
+  if (act == 1) y = at::gelu(y);
+  if (residual.has_value() && residual->defined()) y = y + residual->to(at::kFloat);
+  return y.to(x.scalar_type());
+}
+
+at::Tensor linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
+                      const c10::optional<at::Tensor>& residual) {
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear: act must be 0 (none) or 1 (gelu)");
+  return linear_ref(x, w, bias, act, residual);
+}
+
+at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
+                       int64_t act, const c10::optional<at::Tensor>& residual) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear: act must be 0 (none) or 1 (gelu)");
+  TORCH_CHECK(w_.dim() == 2 && x_.size(-1) == w_.size(1), "amd_dft.linear: x [..., K], w [N, K]");
+  const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
+  if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K))
+    return linear_ref(x_, w_, bias, act, residual);
+  at::Tensor x = x_.contiguous(), w = w_.contiguous();
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = N;
+  at::Tensor y = at::empty(os, x.options());
+  at::Tensor b, r;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->numel() == M * N, "amd_dft.linear: residual must have the output's shape");
+    r = residual->to(at::kBFloat16).contiguous();
+  }
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  p.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  p.residual = r.defined() ? reinterpret_cast<const uint16_t*>(r.data_ptr()) : nullptr;
+  p.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.act = static_cast<int>(act);
+  launch_gemm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>&, int64_t,
+                       const c10::optional<at::Tensor>&) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = w.size(0);
+  return at::empty(os, x.options());
+}
+
 }  // namespace
 }  // namespace amd_dft
 
 TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("patchify(Tensor x, int p) -> Tensor");
   m.def("unpatchify(Tensor t, int C, int h, int w, int p) -> Tensor");
+  m.def("linear(Tensor x, Tensor w, Tensor? bias=None, int act=0, Tensor? residual=None) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("patchify", &amd_dft::patchify_cuda);
   m.impl("unpatchify", &amd_dft::unpatchify_cuda);
+  m.impl("linear", &amd_dft::linear_cuda);
 }
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("patchify", &amd_dft::patchify_cpu);
   m.impl("unpatchify", &amd_dft::unpatchify_cpu);
+  m.impl("linear", &amd_dft::linear_cpu);
 }
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("patchify", &amd_dft::patchify_meta);
   m.impl("unpatchify", &amd_dft::unpatchify_meta);
+  m.impl("linear", &amd_dft::linear_meta);
 }

@@ -15,7 +15,7 @@ for d in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
             agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg.items()):
-    if not any(s in k for s in ("fft_", "afno", "ln_", "patch", "Cijk", "fno", "dftw")):
+    if not any(s in k for s in ("fft_", "afno", "ln_", "patch", "Cijk", "fno", "dftw", "gemm")):
         continue
     a = {c: sum(x) / len(x) for c, x in v.items()}
     w = a.get("SQ_WAVES", 0) or 1
