@@ -117,12 +117,118 @@ def register_symbolic(qualname: str, fn) -> None:
     _EXTRA_SYMBOLICS[qualname] = fn
 
 
+_TENSOR_TYPES = ("Tensor", "Optional[Tensor]")
+
+
+def amd_op_names() -> list:
+    """The ``torch.ops.amd_dft`` operators that export as ``com.amd.dft`` nodes (all tensor ops
+    except the contrib Rfft/Irfft, which keep the ``com.microsoft`` form)."""
+    load_plugins()
+    out = []
+    names = sorted({n.split("::", 1)[1].split(".")[0] for n in torch._C._dispatch_get_all_op_names()
+                    if n.startswith("amd_dft::")})
+    for name in names:
+        if name in ("Rfft", "Irfft") or name.startswith("_"):
+            continue
+        op = getattr(torch.ops.amd_dft, name, None)
+        try:
+            sc = op.default._schema
+        except Exception:  # noqa: BLE001 -- not an operator overload packet
+            continue
+        if sc.returns and all(str(r.type) == "Tensor" for r in sc.returns) and any(
+                str(a.type) in _TENSOR_TYPES for a in sc.arguments):
+            out.append(name)
+    return sorted(out)
+
+
+def _make_amd_symbolic(opname: str):
+    """Generic symbolic: tensor arguments become node inputs (absent optionals recorded in
+    ``tensor_mask``), scalars/lists become attributes named after the schema arguments."""
+    sc = getattr(torch.ops.amd_dft, opname).default._schema
+    args = list(sc.arguments)
+    nret = len(sc.returns)
+
+    def sym(g, *vals):
+        from torch.onnx import symbolic_helper as sh
+
+        tensors, mask, attrs = [], [], {}
+        for a, v in zip(args, vals):
+            t = str(a.type)
+            if t in _TENSOR_TYPES:
+                if sh._is_none(v):
+                    mask.append(0)
+                else:
+                    mask.append(1)
+                    tensors.append(v)
+            elif t == "List[int]":
+                ints = [int(i) for i in sh._get_const(v, "is", a.name)]
+                if ints:
+                    attrs[a.name + "_i"] = ints
+            elif t in ("int", "bool", "SymInt"):
+                attrs[a.name + "_i"] = int(sh._get_const(v, "i", a.name))
+            elif t == "float":
+                attrs[a.name + "_f"] = float(sh._get_const(v, "f", a.name))
+            elif t == "Optional[int]":
+                attrs[a.name + "_i"] = -1 if sh._is_none(v) else int(sh._get_const(v, "i", a.name))
+            else:
+                raise NotImplementedError(f"amd_dft::{opname}: cannot export argument {a.name}: {t}")
+        attrs["tensor_mask_i"] = mask
+        outs = g.op(f"{AMD_DOMAIN}::{opname}", *tensors, outputs=nret, **attrs)
+        _set_output_types(opname, args, vals, outs)
+        return outs
+
+    return sym
+
+
+_SCALAR = {"Float": torch.float32, "BFloat16": torch.bfloat16, "Half": torch.float16, "Double": torch.float64,
+           "Long": torch.int64, "Int": torch.int32, "Bool": torch.bool}
+
+
+def _set_output_types(opname, args, vals, outs) -> None:
+    """Static shape inference for com.amd.dft nodes: run the op's Meta kernel on meta tensors of
+    the traced input shapes and stamp the result types on the node outputs."""
+    from torch.onnx import symbolic_helper as sh
+
+    try:
+        call = []
+        for a, v in zip(args, vals):
+            t = str(a.type)
+            if t in _TENSOR_TYPES:
+                if sh._is_none(v):
+                    call.append(None)
+                    continue
+                sizes = sh._get_tensor_sizes(v)
+                st = v.type().scalarType()
+                if sizes is None or any(d is None for d in sizes) or st not in _SCALAR:
+                    return
+                call.append(torch.empty(sizes, dtype=_SCALAR[st], device="meta"))
+            elif t == "List[int]":
+                call.append([int(i) for i in sh._get_const(v, "is", a.name)])
+            elif t in ("int", "SymInt"):
+                call.append(int(sh._get_const(v, "i", a.name)))
+            elif t == "bool":
+                call.append(bool(sh._get_const(v, "i", a.name)))
+            elif t == "float":
+                call.append(float(sh._get_const(v, "f", a.name)))
+            elif t == "Optional[int]":
+                call.append(None if sh._is_none(v) else int(sh._get_const(v, "i", a.name)))
+        res = getattr(torch.ops.amd_dft, opname)(*call)
+        res = res if isinstance(res, (tuple, list)) else (res,)
+        outs_l = outs if isinstance(outs, (tuple, list)) else (outs,)
+        for o, r in zip(outs_l, res):
+            o.setType(o.type().with_sizes(list(r.shape)).with_dtype(r.dtype))
+    except Exception:  # noqa: BLE001 -- inference is best effort; the runner infers at run time
+        return
+
+
 def register_symbolics(opset_version: int = DEFAULT_OPSET) -> None:
     load_plugins()
     if opset_version in _registered:
         return
     torch.onnx.register_custom_op_symbolic("amd_dft::Rfft", _sym_rfft, opset_version)
     torch.onnx.register_custom_op_symbolic("amd_dft::Irfft", _sym_irfft, opset_version)
+    for name in amd_op_names():
+        torch.onnx.register_custom_op_symbolic(f"amd_dft::{name}", _make_amd_symbolic(name), opset_version)
     for name, fn in _EXTRA_SYMBOLICS.items():
         torch.onnx.register_custom_op_symbolic(name, fn, opset_version)
     _registered.add(opset_version)

@@ -163,7 +163,9 @@ def _clip(attrs, x, lo=None, hi=None):
 def _where(attrs, c, a, b):
     dev = next((t.device for t in (c, a, b) if isinstance(t, torch.Tensor) and not _is_host(t)), None)
     if dev is not None:
-        c, a, b = (_to_dev(t, dev) if isinstance(t, torch.Tensor) and _is_host(t) else t for t in (c, a, b))
+        # 0-dim host values stay scalars (no host->device copy, which a hipGraph capture forbids)
+        c, a, b = (t.item() if isinstance(t, torch.Tensor) and _is_host(t) and t.dim() == 0 and t is not c
+                   else _to_dev(t, dev) if isinstance(t, torch.Tensor) and _is_host(t) else t for t in (c, a, b))
     return torch.where(c, a, b)
 
 
@@ -456,6 +458,47 @@ def register_op(name: str, domain: str, fn: OpFn) -> None:
     _OPS[(domain, name)] = fn
 
 
+# ----------------------------------------------------------------- com.amd.dft nodes
+AMD_DOMAIN = "com.amd.dft"
+
+
+def _amd_node(opname: str):
+    """Executor for a ``com.amd.dft::<op>`` node written by the exporter's generic symbolic:
+    rebuilds the ``torch.ops.amd_dft.<op>`` call from the schema, the node inputs and attributes."""
+    from .._loader import load_plugins
+
+    load_plugins()
+    if not hasattr(torch.ops.amd_dft, opname):
+        raise NotImplementedError(f"com.amd.dft::{opname}: no such operator in the loaded library")
+    op = getattr(torch.ops.amd_dft, opname)
+    sc = op.default._schema
+
+    def run(attrs, *inputs):
+        mask = list(attrs.get("tensor_mask", []))
+        it = iter(inputs)
+        args, mi = [], 0
+        for a in sc.arguments:
+            t = str(a.type)
+            if t in ("Tensor", "Optional[Tensor]"):
+                present = mask[mi] if mi < len(mask) else 1
+                mi += 1
+                args.append(next(it) if present else None)
+            elif a.name in attrs:
+                v = attrs[a.name]
+                if t == "bool":
+                    v = bool(v)
+                elif t == "Optional[int]":
+                    v = None if v == -1 else int(v)
+                elif t == "List[int]":
+                    v = [int(i) for i in v]
+                args.append(v)
+            else:
+                args.append(a.default_value if a.has_default_value() else ([] if t == "List[int]" else None))
+        return op(*args)
+
+    return run
+
+
 # ----------------------------------------------------------------- graph
 class OnnxGraph:
     """A parsed ONNX model bound to a device; ``run(*inputs)`` executes it."""
@@ -485,6 +528,8 @@ class OnnxGraph:
         self.nodes = []
         for n in g.node:
             key = (n.domain, n.op_type)
+            if key not in _OPS and n.domain == AMD_DOMAIN:
+                _OPS[key] = _amd_node(n.op_type)
             if key not in _OPS:
                 raise NotImplementedError(f"ONNX op {n.domain or 'ai.onnx'}::{n.op_type} is not supported "
                                           f"(node {n.name!r}); supported: {', '.join(supported_ops())}")

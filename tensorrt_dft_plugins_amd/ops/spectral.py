@@ -113,10 +113,6 @@ def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None)
 
 def fno_spectral_mix(xm: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """FNO mode mixing out[b,o,m] = sum_i x[b,i,m] w[i,o,m] on complex-as-pair tensors
-    xm [B, Cin, M, 2], w [Cin, Cout, M, 2] -> [B, Cout, M, 2] (fp32)."""
-    ops = _ops()
-    if xm.is_cuda and hasattr(ops, "fno_mix"):
-        return ops.fno_mix(xm.contiguous(), w.contiguous())
-    xc = torch.view_as_complex(xm.float().contiguous())
-    wc = torch.view_as_complex(w.float().contiguous())
-    return torch.view_as_real(torch.einsum("bim,iom->bom", xc, wc)).contiguous()
+    xm [B, Cin, M, 2], w [Cin, Cout, M, 2] -> [B, Cout, M, 2] (fp32).  Native op on every device
+    (CPU: ATen einsum; GPU: csrc/spectral/fno_mix.hip), so it also exports as one ONNX node."""
+    return _ops().fno_mix(xm.contiguous(), w.contiguous())

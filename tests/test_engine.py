@@ -97,3 +97,30 @@ def test_engine_hipgraph_gpu(device, tmp_path):
     assert torch.allclose(y.cpu(), 0.25 * x, atol=1e-5)
     st = eng2.benchmark(iterations=20, warmup=2)
     assert st["latency_median_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_engine_from_fast_models_gpu(device, tmp_path):
+    """Engines built from the MI355X model paths (com.amd.dft nodes) replay under hipGraph and
+    match the eager model."""
+    from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet, FNO2d, FNOConfig
+
+    torch.manual_seed(0)
+    fno = FNO2d(FNOConfig(img_size=(90, 180), modes1=12, modes2=12, n_layers=2), backend="amd").eval()
+    x = torch.randn(2, 20, 90, 180)
+    with torch.no_grad():
+        ref = fno.to(device)(x.to(device))
+    eng = Engine.build(fno.cpu(), (x,), device=device)
+    assert eng.use_graph
+    (y,) = eng.infer(x.to(device))
+    assert torch.allclose(y, ref, atol=1e-4)
+
+    cfg = AFNOConfig(img_size=(64, 128), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=8)
+    afno = AFNONet(cfg, backend="amd").eval()
+    xa = torch.randn(1, 4, 64, 128)
+    with torch.no_grad():
+        refa = afno.to(device)(xa.to(device))
+    p = str(tmp_path / "afno.engine")
+    Engine.build(afno.cpu(), (xa,), device=device).save(p)
+    (ya,) = Engine.load(p, device=device).infer(xa.to(device))
+    assert torch.allclose(ya, refa, atol=1e-3)

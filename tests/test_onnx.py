@@ -168,3 +168,39 @@ def test_generic_model_ops_roundtrip():
 def test_supported_ops_listing():
     ops = supported_ops()
     assert "com.microsoft::Rfft" in ops and "com.microsoft::Irfft" in ops and "DFT" in ops
+
+
+def test_export_fast_fno_model_amd_nodes():
+    """The MI355X FNO path (native spectral ops) exports as com.amd.dft nodes and re-imports."""
+    from tensorrt_dft_plugins_amd.models import FNO2d, FNOConfig
+    from tensorrt_dft_plugins_amd.onnx import proto as P
+
+    torch.manual_seed(0)
+    cfg = FNOConfig(img_size=(16, 24), in_chans=3, out_chans=2, width=8, modes1=3, modes2=4, n_layers=2,
+                    proj_hidden=16)
+    m = FNO2d(cfg, backend="amd").eval()
+    x = torch.randn(2, 3, 16, 24)
+    with torch.no_grad():
+        ref = m(x)
+    data = ex.export(m, x)
+    model = P.load_model(data)
+    doms = {n.domain for n in model.graph.node}
+    assert "com.amd.dft" in doms
+    ops = {n.op_type for n in model.graph.node if n.domain == "com.amd.dft"}
+    assert {"dftw_r2c", "c2c_axis", "fno_mix", "fno_c2r_pw", "fno_pointwise"} <= ops
+    (y,) = OnnxGraph(data, device="cpu").run(x)
+    assert torch.allclose(y, ref, atol=1e-5)
+
+
+def test_export_fast_afno_model_amd_nodes():
+    from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+
+    torch.manual_seed(1)
+    cfg = AFNOConfig(img_size=(32, 64), in_chans=3, out_chans=3, embed_dim=64, depth=2, num_blocks=4, patch_size=8)
+    m = AFNONet(cfg, backend="amd").eval()
+    x = torch.randn(1, 3, 32, 64)
+    with torch.no_grad():
+        ref = m(x)
+    data = ex.export(m, x)
+    (y,) = OnnxGraph(data, device="cpu").run(x)
+    assert torch.allclose(y, ref, atol=1e-4)
