@@ -82,6 +82,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 latency probe")
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--streams", type=int, default=1, help="micro-batches on concurrent HIP streams per GPU")
     a = ap.parse_args(argv)
 
     rank, world, local = init_distributed()
@@ -109,6 +110,7 @@ def main(argv=None) -> int:
         log(f"fft probe: {fft}")
 
     t_build = time.perf_counter()
+    model.micro_batches = max(1, a.streams)
     runner = DataParallelInference(model, x, gather=not a.no_gather, use_graph=not a.no_graph)
     log(f"captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t_build:.1f}s; "
         f"world={world} batch/GPU={B}")
@@ -165,6 +167,7 @@ def main(argv=None) -> int:
                 "per_gpu_batch": B,
                 "hipgraph": runner.cap.use_graph,
                 "output_allgather": runner.gather,
+                "streams": a.streams,
             },
             "model_tflops_per_s": round(tflops, 2),
         }

@@ -197,6 +197,7 @@ class AFNONet(nn.Module):
         self.pos_embed = nn.Parameter(0.02 * torch.randn(1, cfg.h * cfg.w, cfg.embed_dim))
         self.blocks = nn.ModuleList([Block(cfg, backend) for _ in range(cfg.depth)])
         self.head = nn.Linear(cfg.embed_dim, cfg.out_chans * p * p, bias=False)
+        self.micro_batches = 1  # >1: batch slices on concurrent HIP streams (amd backend, GPU)
 
     def set_backend(self, backend: str) -> "AFNONet":
         self.backend = backend
@@ -224,11 +225,14 @@ class AFNONet(nn.Module):
         if self.backend == "amd":
             from ..ops import spectral as S
 
-            pending = None
-            for blk in self.blocks:
-                t, pending = S.afno_block_amd(blk, t, pending)
-            if pending is not None:
-                t = t + pending
+            if self.micro_batches > 1 and t.is_cuda and B >= self.micro_batches and not torch.jit.is_tracing():
+                t = self._blocks_microbatched(t)
+            else:
+                pending = None
+                for blk in self.blocks:
+                    t, pending = S.afno_block_amd(blk, t, pending)
+                if pending is not None:
+                    t = t + pending
         else:
             for blk in self.blocks:
                 t = blk(t)
@@ -240,6 +244,47 @@ class AFNONet(nn.Module):
         t = self.head(t)  # [B, h, w, out*p*p], feature order (p1, p2, c_out) as FourCastNet
         t = t.reshape(B, cfg.h, cfg.w, p, p, cfg.out_chans).permute(0, 5, 1, 3, 2, 4)
         return t.reshape(B, cfg.out_chans, cfg.h * p, cfg.w * p)
+
+    def _blocks_microbatched(self, t: torch.Tensor) -> torch.Tensor:
+        """Blocks over ``micro_batches`` batch slices on their own HIP streams.  The MLP GEMMs of
+        the slices are chained (never two GEMMs at once -- hipBLASLt's stream-K
+        kernels spin on tiles of their own grid and must not share the chip with another
+        spinning GEMM), so one slice's bandwidth-bound spectral kernels run beside the other
+        slice's MFMA-bound GEMMs.  Fork/join via stream waits: captures into one hipGraph.
+        Measured at batch 32 (bench.py --streams 2): 86.4 vs 85.6 ms -- hipBLASLt's GEMM blocks
+        hold every CU's registers/LDS, so the other slice's kernels only fill GEMM tails; off
+        by default."""
+        from ..ops import spectral as S
+
+        n = self.micro_batches
+        cur = torch.cuda.current_stream(t.device)
+        if getattr(self, "_mb_streams", None) is None or len(self._mb_streams) != n:
+            self._mb_streams = [torch.cuda.Stream(t.device) for _ in range(n)]
+        streams = self._mb_streams
+        ts = list(t.chunk(n))
+        pend = [None] * n
+        for s in streams:
+            s.wait_stream(cur)
+        prev = None
+        for blk in self.blocks:
+            for i, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    x, yn = S.afno_block_spectral(blk, ts[i], pend[i])
+                    if prev is not None and prev is not s:
+                        # chain through the origin stream: a direct wait between two side
+                        # streams crashes ROCm graph capture (scripts/mb_capture_probe.py)
+                        cur.wait_stream(prev)
+                        s.wait_stream(cur)
+                    pend[i] = S.afno_block_mlp(blk, yn)
+                    prev = s
+                    ts[i] = x
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                ts[i] = ts[i] + pend[i]
+        for s, x in zip(streams, ts):
+            cur.wait_stream(s)
+            x.record_stream(cur)
+        return torch.cat(ts, 0)
 
     def _head_weight_cpp(self) -> torch.Tensor:
         """Head weight with rows reordered from (p1, p2, c_out) to (c_out, p1, p2); cached."""

@@ -17,7 +17,7 @@ from .._loader import load_plugins
 from . import dft as D
 
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
-           "afno_block_amd", "fno_spectral_mix"]
+           "afno_block_amd", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
 
 
 def _ops():
@@ -95,6 +95,13 @@ def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None)
     LN1 (which also writes the summed residual stream), so fc2 needs no residual GEMM input
     (hipBLASLt would copy it into the output first) and no separate bias/residual kernels.
     """
+    x, yn = afno_block_spectral(blk, x, pending)
+    return x, afno_block_mlp(blk, yn)
+
+
+def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
+    """Bandwidth/VALU-bound half of a block: LN1(+pending residual) -> AFNO filter (+ both skips,
+    fused into the C2R store) -> LN2.  Returns (residual stream x, LN2 output)."""
     from ..models.afno import afno2d_amd
 
     f = blk.filter
@@ -104,11 +111,16 @@ def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None)
     x = afno2d_amd(h, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, c.hard_thresholding_fraction,
                    residual=x)
     yn, _ = layer_norm(x, blk.norm2)
+    return x, yn
+
+
+def afno_block_mlp(blk, yn: torch.Tensor) -> torch.Tensor:
+    """MFMA-bound half of a block: fc1 (+bias, GELU epilogue) and fc2 (+bias) on hipBLASLt."""
     m = blk.mlp
     B, H, W, C = yn.shape
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
     y = F.linear(hid, m.fc2.weight, m.fc2.bias)
-    return x, y.reshape(B, H, W, C)
+    return y.reshape(B, H, W, C)
 
 
 def fno_spectral_mix(xm: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
