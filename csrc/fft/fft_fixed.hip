@@ -66,7 +66,12 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     // C2R with fused addends prefers 32-channel tiles, the R2C 16 (wider R2C tiles lose).
     const int t_pref = (cols && d.kind == Kind::R2C) ? 16 : 1 << 30;
     const double tw = c.T <= t_pref ? c.T : -c.T;
-    const double score = waves >= 2048 ? 1e12 + tw * 1e6 + c.TP : static_cast<double>(waves);
+    // Small problems (rfft2 720x1440 column pass: 721 columns): wide column tiles win over
+    // occupancy as long as ~one wave per SIMD remains (bench/bench_fft_cfg.py: T=8 15.8 us,
+    // T=2 19.8 us, T=16 17.7 us with only 552 waves).
+    const double score = waves >= 2048 ? 1e12 + tw * 1e6 + c.TP
+                         : waves >= 1000 ? 1e9 + tw * 1e3 + c.TP
+                                         : static_cast<double>(waves);
     if (score > best_score) {
       best_score = score;
       best = i;

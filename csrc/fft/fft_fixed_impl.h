@@ -415,6 +415,8 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(720, true, 90, 2, 8, 9, 10)           \
   X(720, true, 45, 8, 8, 9, 10)           \
   X(720, true, 45, 4, 8, 9, 10)           \
+  X(720, true, 90, 8, 8, 9, 10)           \
+  X(720, true, 45, 16, 8, 9, 10)          \
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)            \
   X(180, true, 15, 32, 12, 15)
