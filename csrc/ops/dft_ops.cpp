@@ -339,7 +339,7 @@ bool use_dftw(const at::Tensor& in, const DimSpec& s, at::ScalarType out_t) {
   // fp32 inputs stay on the Stockham kernels (~1e-7): the GEMM's bf16x3 split of fp32 data is
   // good to ~4e-6 relative; bf16 inputs are exact operands and get fp32-grade results.
   if (in.scalar_type() != at::kBFloat16) return false;
-  if (s.lo < 1 || s.lo > 64 || s.n % 8 != 0 || s.n < 64 || 8 * s.lo > s.n) return false;
+  if (s.n < 64 || 8 * s.lo > s.n || !dftw_r2c_supported(static_cast<int>(s.n), static_cast<int>(s.lo))) return false;
   return in.numel() < (int64_t(1) << 31);
 }
 
@@ -369,7 +369,7 @@ at::Tensor dftw_r2c_cuda(const at::Tensor& x_, int64_t m, double scale) {
               "amd_dft.dftw_r2c: x must be float32 or bfloat16");
   const int64_t W = x.size(-1);
   TORCH_CHECK(m >= 1 && m <= W / 2 + 1, "amd_dft.dftw_r2c: needs 1 <= m <= W/2+1");
-  if (m > 64 || W % 8 != 0)  // outside the GEMM kernel: pruned Stockham R2C
+  if (!dftw_r2c_supported(static_cast<int>(W), static_cast<int>(m)))  // outside the GEMM kernel: pruned Stockham R2C
   {
     const std::vector<int64_t> d{x.dim() - 1}, k{m, 0};
     return r2c_cuda(x, d, scale, k, at::kFloat);

@@ -220,7 +220,7 @@ at::Tensor fno_c2r_pw_cuda(const at::Tensor& yw_, const at::Tensor& x_, const at
   const int64_t B = x_.size(0), Cin = x_.size(1), H = x_.size(2), W = x_.size(3), Cout = yw_.size(1),
                 m = yw_.size(3);
   if (!fno_c2r_pw_supported(static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(m),
-                            static_cast<int>(W))) {
+                            static_cast<int>(W), x_.scalar_type() == at::kBFloat16)) {
     // shapes outside the fused kernel: C2R on the FFT kernels + the pointwise kernel
     static auto c2r = c10::Dispatcher::singleton()
                           .findSchemaOrThrow("amd_dft::c2r", "")

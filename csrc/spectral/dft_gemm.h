@@ -11,6 +11,9 @@ constexpr int kDftGemmKB = 64;     // samples per phase block of the forward ker
 // output pixels per phase block of the inverse kernel (bf16 / fp32 I/O)
 constexpr int kFnoChunkBF = 128;
 constexpr int kFnoChunkF32 = 64;
+// per-block phase / per-chunk rotation tables are LDS-resident (float2 entries)
+constexpr int kDftwPhMax = 2048;
+constexpr int kFnoRotMax = 2048;
 
 // ---- forward: out[r, n] = scale * sum_k x[r, k] e^{-2 pi i n k / W},  n < m <= 64
 struct DftwR2CLaunch {
@@ -24,6 +27,8 @@ struct DftwR2CLaunch {
 };
 // b0: uint16 bf16 bits, [kk][g][re/im][hi/lo][64 lanes][8];  phase: float (re, im) pairs
 void dftw_r2c_tables(int W, int m, std::vector<uint16_t>& b0, std::vector<float>& phase);
+// 1 <= m <= 64, W % 8 == 0 and the phase table (ceil(W/KB) x 16 ceil(m/16)) fits in LDS
+bool dftw_r2c_supported(int W, int m);
 void launch_dftw_r2c(const DftwR2CLaunch& p, void* stream);
 
 // ---- FNO layer tail: inverse real DFT along W of the kept modes, fused with the pointwise path
@@ -42,7 +47,8 @@ struct FnoC2RPwLaunch {
 };
 // g0: uint16 bf16 bits, [ks][pt][hi/lo][64 lanes][8] (pt < chunk/16);  rot: [ceil(W/chunk)][16KS] (cos, sin)
 void fno_c2r_tables(int W, int m, int chunk, std::vector<uint16_t>& g0, std::vector<float>& rot);
-bool fno_c2r_pw_supported(int cin, int cout, int m, int W);
+// Cin, Cout <= 32, m <= 64, W % 8 == 0 and the rotation table fits in LDS (W <= 4096 bf16 / 2048 fp32 at m = 64)
+bool fno_c2r_pw_supported(int cin, int cout, int m, int W, bool bf16);
 void launch_fno_c2r_pw(const FnoC2RPwLaunch& p, void* stream);
 
 }  // namespace amd_dft

@@ -14,8 +14,11 @@
 //   x:   [R, W] bf16 or fp32 rows (contiguous)     out: [R, m] complex fp32 (re, im)
 //   A fragment (16x32 bf16): lane l holds x[row0 + (l&15)][k0 + 8(l>>4) + j], j < 8 -- one
 //   16-byte load per lane straight from HBM (no LDS); fp32 input is split hi + lo on the fly.
-// A workgroup (4 waves) owns 16 rows; the waves take interleaved KB-blocks (split-K) and are
-// summed through LDS, so a 20x720-row FNO input still launches 900 workgroups.
+// A workgroup (NW = 2..4 waves) owns 16 rows; the waves take interleaved KB-blocks (split-K) and
+// are summed through LDS, so a 20x720-row FNO input still launches 900 workgroups.  NW is picked
+// per launch so the whole grid is resident at once when possible: 900 4-wave workgroups at 3
+// waves/SIMD are 1.17 rounds of 768 (the second round costs a full workgroup latency), 900
+// 3-wave workgroups fit in one round of 1024 at 4/3 of the per-wave work.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -30,6 +33,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNKS = kDftGemmKB / 32;  // 32-deep MFMA k-steps per block
 
@@ -42,21 +46,21 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& 
   }
 }
 
-template <bool BF, int G>
-__global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
+template <bool BF, int G, int NW>
+// waves_per_eu pins the register budget (3 waves up to 32 modes): without it the scheduler
+// trades the batched prefetch for occupancy it cannot reach anyway (LDS, grid size).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(G <= 2 ? 3 : 5 - G, G <= 2 ? 3 : 5 - G)))
+dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
                                                        const bf16x8* __restrict__ b0, const float2* __restrict__ ph,
                                                        int R, int W, int m, float scale, int nblk) {
-  __shared__ f32x4 red[3][G][2][64];
+  __shared__ f32x4 red[NW - 1][G][2][64];
   // block phases in LDS: read once per block and mode right before use, so an L2 round trip
   // there would sit on every block's critical path
-  constexpr int kPhMax = 2048;
-  __shared__ float2 phs[kPhMax];
+  // (launch_dftw_r2c guarantees nblk * 16 G <= kDftwPhMax)
+  __shared__ float2 phs[kDftwPhMax];
   const int nph = nblk * 16 * G;
-  const bool ph_lds = nph <= kPhMax;
-  if (ph_lds)
-    for (int t = threadIdx.x; t < nph; t += 256) phs[t] = ph[t];
+  for (int t = threadIdx.x; t < nph; t += 64 * NW) phs[t] = ph[t];
   __syncthreads();
-  const float2* pht = ph_lds ? static_cast<const float2*>(phs) : ph;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row0 = blockIdx.x * 16;
   const int rowA = min(row0 + (lane & 15), R - 1);
@@ -76,9 +80,12 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
   for (int g = 0; g < G; ++g) are[g] = aim[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // A operand: one 16-byte (bf16) / two 16-byte (fp32) loads per lane and k-step.
-  using Raw = typename std::conditional<BF, uint4, float4>::type;
+  using Raw = u32x4;  // 8 bf16 / 4 fp32 (native vector: HIP's uint4/float4 structs copy badly)
   constexpr int NR = BF ? 1 : 2;
   const char* xrow = static_cast<const char*>(x) + static_cast<int64_t>(rowA) * W * (BF ? 2 : 4);
+  // Loads are unconditional (clamped address); samples past W are zeroed where they are
+  // consumed -- a select right after the load would make the compiler wait for it there and
+  // serialise the prefetch batch.
   auto load = [&](int s, Raw (&r)[kNKS][NR]) {
 #pragma unroll
     for (int kk = 0; kk < kNKS; ++kk) {
@@ -86,29 +93,32 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
       const bool ok = k0 < W;  // W % 8 == 0: a lane's 8 samples are all in or all out
       const Raw* p = reinterpret_cast<const Raw*>(xrow + static_cast<int64_t>(ok ? k0 : 0) * (BF ? 2 : 4));
 #pragma unroll
-      for (int t = 0; t < NR; ++t) {
-        r[kk][t] = p[t];
-        if (!ok) r[kk][t] = Raw{};
-      }
+      for (int t = 0; t < NR; ++t) r[kk][t] = p[t];
     }
   };
-  // Batches of PF blocks per wave are loaded before any is consumed: 6 x 1 KB per wave in
-  // flight (one batch covers W <= 1536), enough to cover HBM latency at ~3 waves per SIMD.
-  constexpr int PF = 6;
-  for (int s0 = wv; s0 < nblk; s0 += 4 * PF) {
+  // Batches of PF blocks per wave are loaded before any is consumed (4-6 KB per wave in
+  // flight at 3 waves per SIMD).  Every block of a batch is consumed unconditionally (blocks
+  // past nblk are clamped loads with zeroed data): a conditional consumer lets the compiler
+  // sink each load down to its use, which serialises the batch into one round trip per block.
+  // PF divides the per-wave block count of the 1440-wide FNO rows (8 at NW = 3, 6 at NW = 4).
+  constexpr int PF = G >= 4 ? 2 : BF ? (NW == 3 ? 4 : 6) : 3;
+  for (int s0 = wv; s0 < nblk; s0 += NW * PF) {
     Raw buf[PF][kNKS][NR];
 #pragma unroll
-    for (int j = 0; j < PF; ++j)
-      if (s0 + 4 * j < nblk) load(s0 + 4 * j, buf[j]);
+    for (int j = 0; j < PF; ++j) load(min(s0 + NW * j, nblk - 1), buf[j]);
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
-      const int s = s0 + 4 * j;
-      if (s >= nblk) break;
+      const bool live = s0 + NW * j < nblk;
+      const int s = live ? s0 + NW * j : nblk - 1;
       f32x4 tr[G], ti[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) tr[g] = ti[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < kNKS; ++kk) {
+        const bool ok = live && s * kDftGemmKB + 32 * kk + kq < W;
+        if (!ok)
+#pragma unroll
+          for (int t = 0; t < NR; ++t) buf[j][kk][t] = Raw{};
         if constexpr (BF) {
           const bf16x8 a = __builtin_bit_cast(bf16x8, buf[j][kk][0]);
 #pragma unroll
@@ -119,8 +129,8 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
             ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][1], ti[g], 0, 0, 0);
           }
         } else {
-          const float4 f0 = buf[j][kk][0], f1 = buf[j][kk][NR - 1];
-          const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+          const f32x4 f0 = __builtin_bit_cast(f32x4, buf[j][kk][0]), f1 = __builtin_bit_cast(f32x4, buf[j][kk][NR - 1]);
+          const float v[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
           bf16x8 ah, al;
           split8(v, ah, al);
 #pragma unroll
@@ -137,7 +147,7 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
       // block phase e^{-2 pi i n KB s / W}: one complex scale per accumulator column (mode n)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float2 p = pht[s * 16 * G + 16 * g + (lane & 15)];
+        const float2 p = phs[s * 16 * G + 16 * g + (lane & 15)];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           are[g][i] = fmaf(p.x, tr[g][i], fmaf(-p.y, ti[g][i], are[g][i]));
@@ -146,7 +156,7 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
       }
     }
   }
-  // split-K reduction of the 4 waves
+  // split-K reduction of the NW waves
   if (wv > 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -157,7 +167,7 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
   __syncthreads();
   if (wv != 0) return;
 #pragma unroll
-  for (int w = 0; w < 3; ++w)
+  for (int w = 0; w < NW - 1; ++w)
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       are[g] += red[w][g][0][lane];
@@ -175,33 +185,65 @@ __global__ void __launch_bounds__(256) dftw_r2c_kernel(const void* __restrict__ 
   }
 }
 
-template <bool BF>
-void launch_g(const DftwR2CLaunch& p, hipStream_t st) {
-  const int G = (p.m + 15) / 16;
-  const dim3 grid((p.R + 15) / 16);
+// resident workgroups of one instance on the current device (occupancy x CUs), cached per device
+template <bool BF, int G, int NW>
+int64_t resident_wgs() {
+  static int64_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const auto kern = reinterpret_cast<const void*>(&dftw_r2c_kernel<BF, G, NW>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * NW, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    cache[dev] = static_cast<int64_t>(cus) * per_cu;
+  }
+  return cache[dev];
+}
+
+template <bool BF, int G>
+void launch_nw(const DftwR2CLaunch& p, hipStream_t st) {
+  const int64_t groups = (p.R + 15) / 16;
   const int nblk = (p.W + kDftGemmKB - 1) / kDftGemmKB;
+  // cost ~ rounds of workgroups x blocks per wave; ties go to more waves (more loads in flight)
+  const int64_t r4 = resident_wgs<BF, G, 4>(), r3 = resident_wgs<BF, G, 3>();
+  const int64_t c4 = (groups + r4 - 1) / r4 * ((nblk + 3) / 4), c3 = (groups + r3 - 1) / r3 * ((nblk + 2) / 3);
+  const int nw = c3 < c4 ? 3 : 4;
+  const dim3 grid(static_cast<uint32_t>(groups));
   const bf16x8* b0 = static_cast<const bf16x8*>(p.b0);
   float2* out = static_cast<float2*>(p.out);
   const float2* ph = static_cast<const float2*>(p.phase);
-#define L_(GG)                                                                                                    \
-  hipLaunchKernelGGL((dftw_r2c_kernel<BF, GG>), grid, dim3(256), 0, st, p.x, out, b0, ph, p.R, p.W, p.m, p.scale, \
-                     nblk)
-  switch (G) {
-    case 1: L_(1); break;
-    case 2: L_(2); break;
-    case 3: L_(3); break;
-    case 4: L_(4); break;
+#define L_(NW_)                                                                                                  \
+  hipLaunchKernelGGL((dftw_r2c_kernel<BF, G, NW_>), grid, dim3(64 * NW_), 0, st, p.x, out, b0, ph, p.R, p.W, p.m, \
+                     p.scale, nblk)
+  if (nw == 3) L_(3);
+  else L_(4);
+#undef L_
+}
+
+template <bool BF>
+void launch_g(const DftwR2CLaunch& p, hipStream_t st) {
+  switch ((p.m + 15) / 16) {
+    case 1: launch_nw<BF, 1>(p, st); break;
+    case 2: launch_nw<BF, 2>(p, st); break;
+    case 3: launch_nw<BF, 3>(p, st); break;
+    case 4: launch_nw<BF, 4>(p, st); break;
     default: throw std::runtime_error("amd_dft: dftw_r2c: m must be in [1, 64]");
   }
-#undef L_
 }
 
 }  // namespace
 
+bool dftw_r2c_supported(int W, int m) {
+  if (m < 1 || m > 64 || W % 8 != 0 || W < 8) return false;
+  return static_cast<int64_t>((W + kDftGemmKB - 1) / kDftGemmKB) * 16 * ((m + 15) / 16) <= kDftwPhMax;
+}
+
 void launch_dftw_r2c(const DftwR2CLaunch& p, void* stream) {
   if (p.R == 0) return;
-  if (p.m < 1 || p.m > 64 || p.W % 8 != 0 || p.W < 8)
-    throw std::runtime_error("amd_dft: dftw_r2c needs 1 <= m <= 64 and W % 8 == 0");
+  if (!dftw_r2c_supported(p.W, p.m))
+    throw std::runtime_error("amd_dft: dftw_r2c needs 1 <= m <= 64, W % 8 == 0 and W <= 8192 (m = 64)");
   if (static_cast<int64_t>(p.R) * p.W >= (int64_t(1) << 31))
     throw std::runtime_error("amd_dft: dftw_r2c: tensor too large for 32-bit row offsets");
   hipStream_t st = static_cast<hipStream_t>(stream);

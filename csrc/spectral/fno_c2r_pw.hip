@@ -34,6 +34,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 __device__ __forceinline__ void split1(float v, __bf16& hi, __bf16& lo) {
@@ -108,7 +109,7 @@ __device__ __forceinline__ void store4(char* dst, const float (&v)[4]) {
 }
 
 template <bool BF, int KS, int CO, int ACT>
-__global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restrict__ yw, const void* __restrict__ x,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) fno_c2r_pw_kernel(const float2* __restrict__ yw, const void* __restrict__ x,
                                                          const float* __restrict__ wc, const float* __restrict__ bias,
                                                          void* __restrict__ y, const bf16x8* __restrict__ g0,
                                                          const float2* __restrict__ rot, int Cin, int Cout, int H,
@@ -121,13 +122,10 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
   __shared__ __attribute__((aligned(16))) char xs_raw[4][32 * XP * ES];
   // chunk rotations in LDS (needed right before each chunk's MFMAs; an L2 round trip there
   // stalled every chunk)
-  constexpr int kRotMax = 2048;
-  __shared__ float2 rots[kRotMax];
+  // (launch_fno_c2r_pw guarantees nch * 16 KS <= kFnoRotMax)
+  __shared__ float2 rots[kFnoRotMax];
   const int nrot = nch * 16 * KS;
-  const bool rot_lds = nrot <= kRotMax;
-  if (rot_lds)
-    for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
-  const float2* rtab = rot_lds ? static_cast<const float2*>(rots) : rot;
+  for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l15 = lane & 15, lq = lane >> 4;
 
@@ -174,13 +172,16 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
   const int st_ch = lane / LPR, st_px = (lane % LPR) * 8;  // staging role of this lane
   float2 Yv[CO][KS][4];
   int64_t cur_row = -1;
-  char* yrow[CO];        // &y[b][16 ot + l15][h][4 lq]  (clamped to a valid channel)
-  char* yrowp = nullptr;  // same for the packed channel tile: channel 16 + (l15 & 3)
+  // byte offsets (not pointers: a pointer carried around the loop loses its global address
+  // space and the stores become flat stores, which every later LDS wait would also drain)
+  int64_t yrow[CO];  // &y[b][16 ot + l15][h][4 lq] - y  (clamped to a valid channel)
+  int64_t yrowp = 0;  // same for the packed channel tile: channel 16 + (l15 & 3)
+  char* const yb = static_cast<char*>(y);
 
   // x staging: this lane's 8-pixel pieces of channel rows st_ch + RPI*q of unit u, kept in
   // registers one unit ahead so the loads are in flight while the previous chunk computes.
   constexpr int NQ = 32 / RPI;
-  using Raw = typename std::conditional<BF, uint4, float4>::type;
+  using Raw = u32x4;  // 16 bytes = 8 bf16 or 4 fp32 (a native vector: HIP's uint4 struct copies went to scratch)
   constexpr int NR = BF ? 1 : 2;
   Raw xr[NQ][NR];
   auto load_x = [&](int64_t uu) {
@@ -188,16 +189,16 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
     const int cw = static_cast<int>(uu - rr * nch) * CH + st_px;
     const int64_t bb = rr / H, hh = rr - bb * H;
     const char* src = static_cast<const char*>(x) + (((bb * Cin + st_ch) * H + hh) * W + cw) * ES;
+    // Unconditional loads (clamped address when out of range): pixels >= W only reach outputs
+    // that are never stored and channels >= Cin are never staged, so no zeroing is needed --
+    // a select on the loaded value here would make the compiler wait for the load right away
+    // and serialise the prefetch with the chunk it is meant to overlap.
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      if (RPI * q >= Cin) break;  // wave-uniform
       const bool ok = cw < W && st_ch + RPI * q < Cin;
       const Raw* sp = reinterpret_cast<const Raw*>(ok ? src + RPI * q * plane : static_cast<const char*>(x));
 #pragma unroll
-      for (int t = 0; t < NR; ++t) {
-        xr[q][t] = sp[t];
-        if (!ok) xr[q][t] = Raw{};
-      }
+      for (int t = 0; t < NR; ++t) xr[q][t] = sp[t];
     }
   };
   load_x(u0);
@@ -217,17 +218,16 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
             const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
             Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
           }
-      char* y0 = static_cast<char*>(y) + ((b * Cout * H + h) * W + 4 * lq) * ES;
+      const int64_t y0 = ((b * Cout * H + h) * W + 4 * lq) * ES;
 #pragma unroll
       for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
       yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
     }
     const int w0 = c * CH;
-    // ---- x chunk (channels x pixels) into this wave's LDS tile, then prefetch the next one
+    // ---- x chunk (channels x pixels) into this wave's LDS tile
     wave_lds_fence();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      if (RPI * q >= Cin) break;
       const int ch = st_ch + RPI * q;
       if (ch < Cin) {
         Raw* dst = reinterpret_cast<Raw*>(xs + (ch * XP + st_px) * ES);
@@ -235,7 +235,6 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
         for (int t = 0; t < NR; ++t) dst[t] = xr[q][t];
       }
     }
-    if (u + 1 < u1) load_x(u + 1);
     // ---- rotate + split the spectral operand for this chunk
     bf16x8 Bh[CO][KS], Bl[CO][KS];
 #pragma unroll
@@ -243,7 +242,7 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
       uint32_t hi[CO][4], lo[CO][4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float2 r = rtab[c * 16 * KS + 16 * ks + 4 * lq + q];
+        const float2 r = rots[c * 16 * KS + 16 * ks + 4 * lq + q];
 #pragma unroll
         for (int ot = 0; ot < CO; ++ot) {
           const float2 v = Yv[ot][ks][q];
@@ -256,6 +255,9 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
         Bl[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(lo[ot][0], lo[ot][1], lo[ot][2], lo[ot][3]));
       }
     }
+    // prefetch the next unit's x (unconditionally -- the last unit re-loads itself: behind a
+    // branch, the waits after the join would be merged conservatively to vmcnt(0) and drain it)
+    load_x(u + 1 < u1 ? u + 1 : u);
     wave_lds_fence();
     // ---- MFMA, 4 pixel tiles at a time: conv + spectral into bias-initialised accumulators
 #pragma unroll
@@ -319,7 +321,7 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
           float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
-          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
+          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yb + yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
         }
       }
       if (CO == 2 && pack) {
@@ -333,10 +335,26 @@ __global__ void __launch_bounds__(256) fno_c2r_pw_kernel(const float2* __restric
           v[i] = act<ACT>(s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3);
         }
         const int o = 16 + cc;
-        if (o < Cout && pxg + 16 * s < W) store4<BF>(yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
+        if (o < Cout && pxg + 16 * s < W) store4<BF>(yb + yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
       }
     }
   }
+}
+
+// workgroups of one kernel instance resident on the current device (occupancy x CUs), cached
+template <bool BF, int KS, int CO>
+int64_t resident_wgs() {
+  static int64_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const auto kern = reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, BF ? 2 : 1>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+    cache[dev] = static_cast<int64_t>(cus) * per_cu;
+  }
+  return cache[dev];
 }
 
 template <bool BF, int KS, int CO>
@@ -344,8 +362,9 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
   constexpr int CH = Geo<BF>::CH;
   const int nch = (p.W + CH - 1) / CH;
   const int64_t units = static_cast<int64_t>(p.B) * p.H * nch;
-  // ~4 chunks per wave; every wave of the grid is resident at once for the FNO shapes
-  const int64_t nwg = std::min<int64_t>(std::max<int64_t>((units + 15) / 16, 1), 1 << 20);
+  // Persistent grid: at most as many workgroups as are resident at once (a second partial round
+  // of workgroups would double the kernel time), and >= 4 chunks per wave.
+  const int64_t nwg = std::max<int64_t>(std::min<int64_t>((units + 15) / 16, resident_wgs<BF, KS, CO>()), 1);
   const dim3 grid(static_cast<uint32_t>(nwg));
   const float2* yw = static_cast<const float2*>(p.yw);
   const bf16x8* g0 = static_cast<const bf16x8*>(p.g0);
@@ -377,14 +396,17 @@ void launch_ks(const FnoC2RPwLaunch& p, hipStream_t st) {
 
 }  // namespace
 
-bool fno_c2r_pw_supported(int cin, int cout, int m, int W) {
-  return cin >= 1 && cin <= 32 && cout >= 1 && cout <= 32 && m >= 1 && m <= 64 && 2 * (m - 1) <= W && W % 8 == 0;
+bool fno_c2r_pw_supported(int cin, int cout, int m, int W, bool bf16) {
+  if (!(cin >= 1 && cin <= 32 && cout >= 1 && cout <= 32 && m >= 1 && m <= 64 && 2 * (m - 1) <= W && W % 8 == 0))
+    return false;
+  const int ch = bf16 ? kFnoChunkBF : kFnoChunkF32;
+  return static_cast<int64_t>((W + ch - 1) / ch) * 16 * ((m + 15) / 16) <= kFnoRotMax;
 }
 
 void launch_fno_c2r_pw(const FnoC2RPwLaunch& p, void* stream) {
   if (p.B == 0 || p.H == 0) return;
-  if (!fno_c2r_pw_supported(p.Cin, p.Cout, p.m, p.W))
-    throw std::runtime_error("amd_dft: fno_c2r_pw: needs Cin, Cout <= 32, m <= 64, W % 8 == 0");
+  if (!fno_c2r_pw_supported(p.Cin, p.Cout, p.m, p.W, p.bf16 != 0))
+    throw std::runtime_error("amd_dft: fno_c2r_pw: needs Cin, Cout <= 32, m <= 64, W % 8 == 0, W <= 4096 (bf16)");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (p.bf16) launch_ks<true>(p, st);
   else launch_ks<false>(p, st);

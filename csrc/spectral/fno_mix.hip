@@ -96,33 +96,55 @@ __global__ void __launch_bounds__(kNT) fno_mix_kernel(const float* __restrict__ 
 }
 
 // Small batch (B <= 8): the MFMA M dimension (batch) would be >= 50% padding and the op is
-// a pure stream over the per-mode weights (Cin*Cout*M complex, 6.5 MB for 20x20x2048), so one
-// thread per (o, m) reads its Cin weights exactly once (coalesced along m) and keeps the B
-// accumulators in registers.
+// a pure stream over the per-mode weights (Cin*Cout*M complex, 6.5 MB for 20x20x2048).  A
+// workgroup owns 64 consecutive (o, m) outputs (coalesced along m); its 4 waves split the Cin
+// sum (split-K, reduced through LDS) so a 20x2048-mode layer runs 2560 waves instead of 640 --
+// with one wave per SIMD the per-thread chain of Cin dependent loads was the whole kernel time.
 template <int NB>
 __global__ void __launch_bounds__(256) fno_mix_small_kernel(const float2* __restrict__ x, const float2* __restrict__ w,
                                                             float2* __restrict__ y, int B, int Cin, int Cout, int M) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (t >= static_cast<int64_t>(Cout) * M) return;
-  const int o = static_cast<int>(t / M), mm = static_cast<int>(t - static_cast<int64_t>(o) * M);
+  __shared__ float2 red[3][NB][64];
+  const int lane = threadIdx.x & 63, s = threadIdx.x >> 6;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const bool live = t < static_cast<int64_t>(Cout) * M;
+  const int o = live ? static_cast<int>(t / M) : 0;
+  const int mm = live ? static_cast<int>(t - static_cast<int64_t>(o) * M) : 0;
   float2 acc[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) acc[b] = make_float2(0.f, 0.f);
+  const int i0 = s * Cin / 4, i1 = (s + 1) * Cin / 4;
+  if (live) {
 #pragma unroll 8
-  for (int i = 0; i < Cin; ++i) {
-    const float2 wv = w[(static_cast<int64_t>(i) * Cout + o) * M + mm];
+    for (int i = i0; i < i1; ++i) {
+      const float2 wv = w[(static_cast<int64_t>(i) * Cout + o) * M + mm];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      if (b < B) {
-        const float2 xv = x[(static_cast<int64_t>(b) * Cin + i) * M + mm];
-        acc[b].x = fmaf(xv.x, wv.x, fmaf(-xv.y, wv.y, acc[b].x));
-        acc[b].y = fmaf(xv.x, wv.y, fmaf(xv.y, wv.x, acc[b].y));
+      for (int b = 0; b < NB; ++b) {
+        if (b < B) {
+          const float2 xv = x[(static_cast<int64_t>(b) * Cin + i) * M + mm];
+          acc[b].x = fmaf(xv.x, wv.x, fmaf(-xv.y, wv.y, acc[b].x));
+          acc[b].y = fmaf(xv.x, wv.y, fmaf(xv.y, wv.x, acc[b].y));
+        }
       }
     }
   }
+  if (s > 0) {
 #pragma unroll
-  for (int b = 0; b < NB; ++b)
-    if (b < B) y[(static_cast<int64_t>(b) * Cout + o) * M + mm] = acc[b];
+    for (int b = 0; b < NB; ++b) red[s - 1][b][lane] = acc[b];
+  }
+  __syncthreads();
+  if (s != 0 || !live) return;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < B) {
+      float2 v = acc[b];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        v.x += red[r][b][lane].x;
+        v.y += red[r][b][lane].y;
+      }
+      y[(static_cast<int64_t>(b) * Cout + o) * M + mm] = v;
+    }
+  }
 }
 
 }  // namespace
@@ -131,7 +153,7 @@ void launch_fno_mix(const FnoMixLaunch& p, void* stream) {
   if (p.B <= 0 || p.M <= 0) return;
   if (p.B <= 8) {
     const int64_t n = static_cast<int64_t>(p.Cout) * p.M;
-    const dim3 grid(static_cast<uint32_t>((n + 255) / 256));
+    const dim3 grid(static_cast<uint32_t>((n + 63) / 64));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const float2* xx = reinterpret_cast<const float2*>(p.x);
     const float2* ww = reinterpret_cast<const float2*>(p.w);
