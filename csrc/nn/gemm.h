@@ -6,12 +6,14 @@
 namespace amd_dft {
 
 struct GemmLaunch {
-  const uint16_t* x;         // [M, K] bf16 (activations)
-  const uint16_t* w;         // [N, K] bf16 (weight, F.linear layout)
-  const float* bias;         // [N] fp32 or nullptr
-  const uint16_t* residual;  // [M, N] bf16 or nullptr (added after the activation)
-  uint16_t* y;               // [M, N] bf16
-  int M, N, K;
+  const uint16_t* x = nullptr;       // [M, K] bf16 (activations)
+  const uint16_t* w = nullptr;       // [N, K] bf16 (weight, F.linear layout)
+  const float* bias = nullptr;       // [N] fp32 or nullptr
+  const uint16_t* residual = nullptr;  // [M, N] bf16 or nullptr (added after the activation)
+  uint16_t* y = nullptr;             // [M, N] bf16
+  const float* ln_stats = nullptr;     // [M, 2] (mean, rstd) fp32 or nullptr: LayerNorm fold (see gemm.hip)
+  const float* ln_c1 = nullptr;        // [N] fp32: sum_k W'[n, k] (required with ln_stats)
+  int M = 0, N = 0, K = 0;
   int act = 0;               // 0 none, 1 GELU (erf)
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);

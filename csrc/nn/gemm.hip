@@ -1,23 +1,28 @@
 // bf16 GEMM with fused epilogue for the FourCastNet MLP / embed / head layers:
 //   Y[m, n] = act( sum_k X[m, k] * W[n, k] + bias[n] ) (+ R[m, n])        (F.linear layout)
 // X [M, K] and W [N, K] are both K-contiguous; Y [M, N] bf16; fp32 accumulation.
+// Optional LayerNorm fold (p.ln_stats): the GEMM consumes the raw residual stream x and the
+// caller passes W' = W * gamma (per k), c1[n] = sum_k W'[n,k], c2[n] = sum_k beta_k W[n,k] + bias;
+// then LN(x) W^T + bias = rstd_m * (x W'^T - mean_m * c1) + c2 is applied in the epilogue.
 //
-// MI355X design:
+// MI355X design (256 x 256 x 64 block tile, 512 threads, one workgroup per CU):
 //  * computed as Y^T = W . X^T so that an MFMA accumulator holds 4 CONSECUTIVE output features of
-//    one token (C/D row = feature): the epilogue adds a 4-wide bias vector, applies the
-//    activation and writes 8 contiguous bytes per lane (16 lanes = one 32-byte row run);
-//  * 256 (features) x 256 (tokens) x 64 (k) block tile, 8 waves as 2 x 4, 128 x 64 per wave on
+//    one token: the epilogue adds a 4-wide bias vector and writes 8 contiguous bytes per lane;
+//  * 8 waves as 2 (features, "wr") x 4 (tokens, "wc"), 128 x 64 outputs per wave on
 //    v_mfma_f32_16x16x32_bf16 (8 x 4 accumulator tiles = 128 fp32 per lane);
-//  * both operand tiles staged HBM -> LDS by global_load_lds_dwordx4 (no VGPR round trip),
-//    double-buffered (2 x 64 KB); LDS rows are 128 B with the 16-byte chunk index XOR-swizzled
-//    by (row & 7): the DMA writes lane-linear, so the swizzle is applied to the SOURCE address
-//    and undone on the ds_read_b128 fragment reads (conflict-free 8-row groups);
+//  * ping-pong schedule: the two wave groups (wr = 0 / 1, one wave of each per SIMD) run one
+//    barrier apart, so on every SIMD one wave issues its LDS fragment reads and DMA while the
+//    other one runs its 16-MFMA cluster;
+//  * each 64-deep K-tile is 4 phases (one 64x32 quadrant of the wave's output per phase, snake
+//    order so fragments are reused) and 4 LDS regions of 16 KB; every phase DMAs one region of
+//    the K-tile 1..2 ahead with global_load_lds_dwordx4 (no VGPR round trip), so 3 regions
+//    (6 DMA instructions per wave) stay in flight across the barriers: counted vmcnt, never 0
+//    in the main loop, raw s_barrier (no __syncthreads, which would drain the DMA);
+//  * region = 128 rows x 128 B with the 16-byte chunk XOR-swizzled by (row & 7): the DMA writes
+//    lane-linear, so the swizzle is applied to the SOURCE address; fragment reads are
+//    bank-conflict free for the ds_read_b128 lane groups;
 //  * blockIdx -> tile remap keeps consecutive tiles (same token panel, different feature
 //    panels) on one XCD so the token panel is served from that XCD's L2.
-// Status (profiles/gemm_vs_hipblaslt_r1k.txt, pmc_gemm_r1k.txt): correct, bank-conflict free,
-// 0.73-0.82x of hipBLASLt on the FourCastNet MLP shapes (MFMA busy ~34 %, ~40 % of wave time
-// waiting on the one-K-tile-deep DMA prefetch).  The models keep hipBLASLt for their plain
-// GEMMs until this kernel gets the ping-pong (staggered wave-group) schedule.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -37,6 +42,9 @@ constexpr int kBF = 256;  // features per block (MFMA M)
 constexpr int kBT = 256;  // tokens per block (MFMA N)
 constexpr int kBK = 64;
 constexpr int kThreads = 512;
+constexpr int kRegion = 128 * 128;     // 128 rows x 128 B (64 bf16 of K)
+constexpr int kStage = 4 * kRegion;    // one K-tile: 64 KB
+constexpr int kLds = 2 * kStage;       // two K-tiles: 128 KB
 
 __device__ __forceinline__ float gelu_erf(float v) {
   const float z = fabsf(v) * 0.70710678118654752f;
@@ -58,66 +66,105 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// Pipeline: K-tiles of 64 in two LDS buffers (2 x 64 KB), one K-tile of global_load_lds in
-// flight while the current one is computed; fragment reads run one MFMA k-step ahead in a
-// second register set, so the barrier that publishes the next K-tile sits between the two
-// k-steps' MFMA bursts instead of in front of an idle LDS read.
-constexpr int kTileBytes = kBF * kBK * 2;  // one operand, one K-tile: 32 KB
-
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
 
-// one operand tile: rows [r0, r0 + 256) clamped to rmax, k-block kb (64 wide)
-__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, int64_t ld, int r0, int rmax, int kb,
-                                           char* lds_tile, int wave, int lane) {
+// Regions of one K-tile stage (phase q of K-tile t reads region kReadRegion[q]):
+//   R0: feature rows {0-63, 128-191}   -> A fragments, row group mi = 0 of each wave group
+//   R1: token rows {64c + 0..31}       -> B fragments, ni = 0 of each token wave c
+//   R2: token rows {64c + 32..63}      -> B fragments, ni = 1
+//   R3: feature rows {64-127, 192-255} -> A fragments, mi = 1
+template <int REG>
+__device__ __forceinline__ int region_row(int r) {
+  if constexpr (REG == 0) return (r >> 6) * 128 + (r & 63);
+  else if constexpr (REG == 3) return (r >> 6) * 128 + 64 + (r & 63);
+  else if constexpr (REG == 1) return (r >> 5) * 64 + (r & 31);
+  else return (r >> 5) * 64 + 32 + (r & 31);
+}
+
+// DMA one region (2 x 1 KB per wave: 8 rows x 128 B per instruction, lane-linear in LDS)
+template <int REG>
+__device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
+                                             int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
+                                             int lane) {
+  char* dst = stage + REG * kRegion;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rb = (wave * 4 + i) * 8;  // 8 rows x 128 B per wave-instruction (1 KB, lane-linear)
+  for (int i = 0; i < 2; ++i) {
+    const int rb = (wave * 2 + i) * 8;
     const int row = rb + (lane >> 3), pos = lane & 7;
     const int chunk = pos ^ (row & 7);  // source swizzle = inverse of the read swizzle
-    const int grow = min(r0 + row, rmax);
-    const uint16_t* g = src + static_cast<int64_t>(grow) * ld + kb * kBK + chunk * 8;
-    __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(lds_tile + rb * 128), 16, 0, 0);
+    const int tr = region_row<REG>(row);
+    const uint16_t* g;
+    if constexpr (REG == 0 || REG == 3) {
+      g = W + static_cast<int64_t>(f0 + tr) * K;
+    } else {
+      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * K;
+    }
+    g += kt * kBK + chunk * 8;
+    __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
   }
 }
 
-// Fragments of one phase: A = 4 of the wave's 8 feature tiles (half `ah`) at k-step `ks`,
-// B = the wave's 4 token tiles at k-step `ks` (loaded on ah == 0, reused on ah == 1).
-__device__ __forceinline__ void read_a(bf16x8 (&a)[4], const char* buf, int ks, int ah, int wf, int r16, int kq) {
+// 4 A fragments (16 rows each) x 2 k-steps from region REG (rows wr*64 + i*16 + r16)
+template <int REG>
+__device__ __forceinline__ void read_a(bf16x8 (&a)[8], const char* stage, int wr, int r16, int kq) {
+  const char* base = stage + REG * kRegion;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    a[i] = *reinterpret_cast<const bf16x8*>(buf + swz(wf * 128 + (ah * 4 + i) * 16 + r16, ks * 4 + kq));
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[s * 4 + i] = *reinterpret_cast<const bf16x8*>(base + swz(wr * 64 + i * 16 + r16, s * 4 + kq));
 }
-__device__ __forceinline__ void read_b(bf16x8 (&bq)[4], const char* buf, int ks, int wt, int r16, int kq) {
+// 2 B fragments x 2 k-steps from region REG (rows wc*32 + j*16 + r16)
+template <int REG>
+__device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc, int r16, int kq) {
+  const char* base = stage + REG * kRegion;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    bq[j] = *reinterpret_cast<const bf16x8*>(buf + kTileBytes + swz(wt * 64 + j * 16 + r16, ks * 4 + kq));
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      b[s * 2 + j] = *reinterpret_cast<const bf16x8*>(base + swz(wc * 32 + j * 16 + r16, s * 4 + kq));
 }
 
-template <int AH>
-__device__ __forceinline__ void mfma_phase(f32x4 (&acc)[8][4], const bf16x8 (&a)[4], const bf16x8 (&bq)[4]) {
+template <int MI, int NI>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc[AH * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bq[j], acc[AH * 4 + i][j], 0, 0, 0);
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[MI * 4 + i][NI * 2 + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s * 4 + i], b[s * 2 + j], acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int ACT, bool BIAS, bool RES>
-__global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(const uint16_t* __restrict__ X,
-                                                             const uint16_t* __restrict__ Wt,
-                                                             const float* __restrict__ bias,
-                                                             const uint16_t* __restrict__ R,
-                                                             uint16_t* __restrict__ Y, int M, int N, int K) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][W tile | X tile]
+// vmcnt(2n): the region issued 3 phases ago has landed, n younger regions may still fly
+__device__ __forceinline__ void wait_regions(int n) {
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int ACT, bool BIAS, bool RES, bool LN>
+__global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
+  const uint16_t* __restrict__ W = p.w;
+  const uint16_t* __restrict__ X = p.x;
+  const int M = p.M, N = p.N, K = p.K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wf = wave >> 2, wt = wave & 3;  // 2 (features) x 4 (tokens)
+  const int wr = wave >> 2, wc = wave & 3;  // 2 (features) x 4 (tokens)
   // ---- XCD-aware tile order (bijective for any grid size)
   const int tiles_f = N / kBF;
   const int nwg = gridDim.x, b = blockIdx.x;
-  const int q = nwg / 8, r = nwg % 8, xcd = b % 8;
-  const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
   const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
   const int f0 = ft * kBF, t0 = tt * kBT;
   const int KT = K / kBK;
@@ -129,98 +176,140 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(const uint16_t* __r
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto stage = [&](int kt) {
-    char* buf = smem + (kt & 1) * 2 * kTileBytes;
-    stage_tile(Wt, K, f0, N - 1, kt, buf, wave, lane);
-    stage_tile(X, K, t0, M - 1, kt, buf + kTileBytes, wave, lane);
-  };
-  stage(0);
-  if (KT > 1) {
-    stage(1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed, tile 1 may fly
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  // phases per K-tile: (ks, ah) = (0,0) (0,1) (1,0) (1,1); fragments are read one phase ahead
-  bf16x8 a0[4], a1[4], b0[4], b1[4];
-  read_a(a0, smem, 0, 0, wf, r16, kq);
-  read_b(b0, smem, 0, wt, r16, kq);
+  // Linear phase index P = 4 t + q.  Phase P DMAs region (q+1) & 3 of K-tile tgt(P) into
+  // stage tgt(P) & 1 and reads the region that phase P - 4 DMA'd.
+  //   q = 0: R1(t+1)   q = 1: R2(t+1)   q = 2: R3(t+1)   q = 3: R0(t+2)
+  auto tgt = [](int P) { return (P >> 2) + 1 + ((P & 3) == 3 ? 1 : 0); };
+  auto issued = [&](int P) { return tgt(P) < KT ? 1 : 0; };
 
-  for (int kt = 0; kt < KT; ++kt) {
-    const char* cur = smem + (kt & 1) * 2 * kTileBytes;
-    read_a(a1, cur, 0, 1, wf, r16, kq);
-    mfma_phase<0>(acc, a0, b0);
-    read_a(a0, cur, 1, 0, wf, r16, kq);
-    read_b(b1, cur, 1, wt, r16, kq);
-    mfma_phase<1>(acc, a1, b0);
-    read_a(a1, cur, 1, 1, wf, r16, kq);
-    mfma_phase<0>(acc, a0, b1);
-    // publish tile kt+1 (this wave's only outstanding DMA) after every read of tile kt retired
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < KT) stage(kt + 2);  // into the buffer every wave just finished reading
-    if (kt + 1 < KT) {
-      const char* nxt = smem + ((kt + 1) & 1) * 2 * kTileBytes;
-      read_a(a0, nxt, 0, 0, wf, r16, kq);
-      read_b(b0, nxt, 0, wt, r16, kq);
-    }
-    mfma_phase<1>(acc, a1, b1);
+  // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
+  stage_region<0>(W, X, K, f0, t0, M, 0, smem, wave, lane);
+  stage_region<1>(W, X, K, f0, t0, M, 0, smem, wave, lane);
+  stage_region<2>(W, X, K, f0, t0, M, 0, smem, wave, lane);
+  stage_region<3>(W, X, K, f0, t0, M, 0, smem, wave, lane);
+  if (KT > 1) {
+    stage_region<0>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
+  barrier();
+  bf16x8 a0[8], a1[8], b0[4], b1[4];
+  read_a<0>(a0, smem, wr, r16, kq);
+  if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
+
+  for (int t = 0; t < KT; ++t) {
+    char* cur = smem + (t & 1) * kStage;
+    char* nxt = smem + ((t + 1) & 1) * kStage;
+    const int P = 4 * t;
+    // ---- phase 0: quadrant (mi 0, ni 0)
+    wait_regions(issued(P - 2) + issued(P - 1));
+    if (issued(P)) stage_region<1>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    read_b<1>(b0, cur, wc, r16, kq);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<0, 0>(acc, a0, b0);
+    barrier();
+    // ---- phase 1: (0, 1)
+    wait_regions(issued(P - 1) + issued(P));
+    if (issued(P + 1)) stage_region<2>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    read_b<2>(b1, cur, wc, r16, kq);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<0, 1>(acc, a0, b1);
+    barrier();
+    // ---- phase 2: (1, 1)
+    wait_regions(issued(P) + issued(P + 1));
+    if (issued(P + 2)) stage_region<3>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    read_a<3>(a1, cur, wr, r16, kq);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<1, 1>(acc, a1, b1);
+    barrier();
+    // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
+    wait_regions(issued(P + 1) + issued(P + 2));
+    if (issued(P + 3)) stage_region<0>(W, X, K, f0, t0, M, t + 2, cur, wave, lane);
+    if (t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<1, 0>(acc, a1, b0);
+    barrier();
+  }
+  if (wr == 0) barrier();  // re-align the two wave groups
 
   // ---- epilogue: lane holds features f..f+3 of token t for each (i, j) tile
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int f = f0 + wf * 128 + i * 16 + 4 * kq;
+    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float cv[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (BIAS) {
-      const float4 b4 = *reinterpret_cast<const float4*>(bias + f);
+      const float4 b4 = *reinterpret_cast<const float4*>(p.bias + f);
       bv[0] = b4.x;
       bv[1] = b4.y;
       bv[2] = b4.z;
       bv[3] = b4.w;
     }
+    if constexpr (LN) {
+      const float4 c4 = *reinterpret_cast<const float4*>(p.ln_c1 + f);
+      cv[0] = c4.x;
+      cv[1] = c4.y;
+      cv[2] = c4.z;
+      cv[3] = c4.w;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int t = t0 + wt * 64 + j * 16 + r16;
+      const int t = t0 + wc * 64 + j * 16 + r16;
       if (t >= M) continue;
       float v[4];
+      float mean = 0.f, rstd = 1.f;
+      if constexpr (LN) {
+        const float2 st = *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(t));
+        mean = st.x;
+        rstd = st.y;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] + bv[e];
+        float a = acc[i][j][e];
+        if constexpr (LN) a = rstd * fmaf(-mean, cv[e], a);
+        v[e] = a + bv[e];
         if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
       }
       const int64_t off = static_cast<int64_t>(t) * N + f;
       if constexpr (RES) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(R + off);
+        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
         v[0] += __uint_as_float(rr.x << 16);
         v[1] += __uint_as_float(rr.x & 0xffff0000u);
         v[2] += __uint_as_float(rr.y << 16);
         v[3] += __uint_as_float(rr.y & 0xffff0000u);
       }
-      *reinterpret_cast<uint2*>(Y + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+      *reinterpret_cast<uint2*>(p.y + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
     }
   }
 }
 
-template <int ACT, bool BIAS>
-void launch_res(const GemmLaunch& p, hipStream_t st, dim3 grid, size_t lds) {
-  if (p.residual)
-    hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, true>), grid, dim3(kThreads), lds, st, p.x, p.w, p.bias,
-                       p.residual, p.y, p.M, p.N, p.K);
-  else
-    hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, false>), grid, dim3(kThreads), lds, st, p.x, p.w, p.bias,
-                       p.residual, p.y, p.M, p.N, p.K);
+template <int ACT, bool BIAS, bool RES, bool LN>
+void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, RES, LN>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm attr: ") + hipGetErrorString(e));
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, RES, LN>), grid, dim3(kThreads), kLds, st, p);
+}
+
+template <int ACT, bool BIAS, bool RES>
+void launch_ln(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if (p.ln_stats) launch_one<ACT, BIAS, RES, true>(p, st, grid);
+  else launch_one<ACT, BIAS, RES, false>(p, st, grid);
 }
 
 template <int ACT, bool BIAS>
-void set_attr() {
-  for (bool res : {false, true}) {
-    const void* f = res ? reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, true>)
-                        : reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, false>);
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTileBytes);
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm attr: ") + hipGetErrorString(e));
-  }
+void launch_res(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if (p.residual) launch_ln<ACT, BIAS, true>(p, st, grid);
+  else launch_ln<ACT, BIAS, false>(p, st, grid);
 }
 
 }  // namespace
@@ -232,25 +321,17 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
 
 void launch_gemm(const GemmLaunch& p, void* stream) {
   if (!gemm_supported(p.M, p.N, p.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
-  static bool attr_done = false;
-  if (!attr_done) {
-    set_attr<0, false>();
-    set_attr<0, true>();
-    set_attr<1, false>();
-    set_attr<1, true>();
-    attr_done = true;
-  }
+  if (p.ln_stats && !p.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t lds = 4 * kTileBytes;
   const bool bias = p.bias != nullptr;
   if (p.act == 1) {
-    if (bias) launch_res<1, true>(p, st, grid, lds);
-    else launch_res<1, false>(p, st, grid, lds);
+    if (bias) launch_res<1, true>(p, st, grid);
+    else launch_res<1, false>(p, st, grid);
   } else {
-    if (bias) launch_res<0, true>(p, st, grid, lds);
-    else launch_res<0, false>(p, st, grid, lds);
+    if (bias) launch_res<0, true>(p, st, grid);
+    else launch_res<0, false>(p, st, grid);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm launch: ") + hipGetErrorString(e));
