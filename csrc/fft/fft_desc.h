@@ -44,6 +44,14 @@ struct PassDesc {
   const void* tw = nullptr;  // device float2 table: per-pass twiddles + generic radix roots
   const void* add1 = nullptr;  // C2R epilogue addends (same layout and dtype as out), or null
   const void* add2 = nullptr;
+  // LayerNorm fused into the IO of a channel-last transform (AFNO W-direction passes over
+  // [B, H, W, C]: outer o = (b, h), inner = channel, token = o * L + n).  R2C: the input is
+  // normalised on load, LN(x + pre).  C2R: add1 = x (stored residual stream) and the epilogue
+  // adds x' + LN(x'), x' = x + pre.  Fixed (specialised) kernels only.
+  const float* ln_stats = nullptr;  // [O * L] x (mean, rstd) of x' per token
+  const float* ln_gamma = nullptr;  // [I] fp32
+  const float* ln_beta = nullptr;   // [I] fp32
+  const float* ln_pre = nullptr;    // [I] fp32 or null
 
   int32_t L = 1;       // transform length
   int32_t npass = 0;   // number of Stockham passes (0 when L == 1)

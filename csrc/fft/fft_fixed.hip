@@ -98,6 +98,10 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
   a.bf16_in = d.tin == DType::BF16; a.bf16_out = d.tout == DType::BF16;
   a.add1 = d.add1;
   a.add2 = d.add2;
+  a.ln_stats = d.ln_stats;
+  a.ln_gamma = d.ln_gamma;
+  a.ln_beta = d.ln_beta;
+  a.ln_pre = d.ln_pre;
   {
     // paired-vector IO: the two real signals of a complex FFT are adjacent (and 2 scalars
     // apart on the complex side), I even, and every pair offset suitably aligned
@@ -110,6 +114,11 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     for (const void* ad : {d.add1, d.add2})
       pv = pv && (ad == nullptr || reinterpret_cast<uintptr_t>(ad) % (2 * rout * eso) == 0);
     a.pairvec = pv ? 1 : 0;
+  }
+  if (d.ln_stats) {  // LayerNorm IO: channel-last bf16 pairs, R2C input / C2R addend only
+    const bool ok = cfg.cols && d.kind != Kind::C2C && a.pairvec && a.bf16_in && a.bf16_out && d.ln_gamma &&
+                    d.ln_beta && (d.kind == Kind::R2C || (d.add1 && !d.add2)) && d.I % 2 == 0;
+    if (!ok) return false;
   }
   const int64_t nblocks = d.O * a.tiles_per_outer;
   if (nblocks <= 0) return true;

@@ -33,6 +33,11 @@ struct FixedArgs {
   const void* add1;  // C2R epilogue: out = scale * irfft + add1 (+ add2); same layout/dtype as out
   const void* add2;
   int32_t pairvec;   // paired real signals adjacent in memory (channel-last) and I even
+  // LayerNorm IO fusion (NADD == 3 instantiations, see PassDesc::ln_stats)
+  const float* ln_stats;
+  const float* ln_gamma;
+  const float* ln_beta;
+  const float* ln_pre;
 };
 
 template <int... Rs>
@@ -117,7 +122,17 @@ struct Ctx {
   bool ok0, ok1;    // c < I (C2C) / 2c < I, 2c+1 < I (paired)
   int t, tp;
   float2* lds;
+  // NADD == 3 (LayerNorm IO): stats of this outer row, per-channel params of the signal pair
+  const float2* st;
+  float2 g, be, pre;
 };
+
+// LayerNorm of one stored channel pair at position n: x' = v + pre, LN(x') (x' returned in xp)
+__device__ __forceinline__ float2 ln_pair(const Ctx& x, int n, float2 v, float2& xp) {
+  const float2 s = x.st[n];  // (mean, rstd) of token (o, n)
+  xp = make_float2(v.x + x.pre.x, v.y + x.pre.y);
+  return make_float2((xp.x - s.x) * s.y * x.g.x + x.be.x, (xp.y - s.x) * s.y * x.g.y + x.be.y);
+}
 
 template <bool COLS, int T, int L>
 __device__ __forceinline__ int lidx(const Ctx& x, int n) {
@@ -129,7 +144,7 @@ __device__ __forceinline__ int lidx(const Ctx& x, int n) {
 // First-pass element fetch (includes the C2R Hermitian assembly and input pruning).
 // Every load is unconditional from a clamped (valid) address and masked afterwards with a
 // select: a branch around a load makes hipcc wait vmcnt(0) per element.
-template <Kind K, int L, bool BF, bool PR, bool PV>
+template <Kind K, int L, bool BF, bool PR, bool PV, int NADD = 0>
 __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
   const FixedArgs& a = x.a;
   float2 z;
@@ -143,7 +158,10 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
     }
     if (a.inverse) z.y = -z.y;
   } else if constexpr (K == Kind::R2C) {
-    if constexpr (PV) {  // the two packed real signals are adjacent: one vector load
+    if constexpr (PV && NADD == 3) {  // LayerNorm on load
+      float2 xp;
+      z = sel(x.ok0, ln_pair(x, n, ld_c<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in), xp));
+    } else if constexpr (PV) {  // the two packed real signals are adjacent: one vector load
       z = sel(x.ok0, ld_c<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in));
     } else {
       const float va = ld_r<BF>(x.in, x.i0c * a.Si_in + n * a.Sn_in);
@@ -207,16 +225,20 @@ __device__ __forceinline__ float2 load_addend(const Ctx& x, int n) {
     const FixedArgs& a = x.a;
     const int32_t off = x.i0c * a.Si_out + n * a.Sn_out;
     const int32_t offb = x.i1c * a.Si_out + n * a.Sn_out;
-    if constexpr (PV) {
+    if constexpr (PV && NADD == 3) {  // x' + LN(x') of the stored residual stream x
+      float2 xp;
+      const float2 h = ln_pair(x, n, ld_c<BF>(x.add1, off), xp);
+      r = make_float2(xp.x + h.x, xp.y + h.y);
+    } else if constexpr (PV) {
       r = ld_c<BF>(x.add1, off);
-      if constexpr (NADD >= 2) {
+      if constexpr (NADD == 2) {
         const float2 t = ld_c<BF>(x.add2, off);
         r.x += t.x;
         r.y += t.y;
       }
     } else {
       r = make_float2(ld_r<BF>(x.add1, off), ld_r<BF>(x.add1, offb));
-      if constexpr (NADD >= 2) {
+      if constexpr (NADD == 2) {
         r.x += ld_r<BF>(x.add2, off);
         r.y += ld_r<BF>(x.add2, offb);
       }
@@ -295,7 +317,7 @@ struct Step {
       if (G::EXACT || j < LR) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if constexpr (P == 0) v[q][r] = gather<K, L, BFI, PR, PV>(x, j + r * LR);
+          if constexpr (P == 0) v[q][r] = gather<K, L, BFI, PR, PV, NADD>(x, j + r * LR);
           else v[q][r] = x.lds[lidx<COLS, T, L>(x, j + r * LR)];
         }
       }
@@ -372,7 +394,14 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
   x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
   if constexpr (NADD >= 1) x.add1 = static_cast<const char*>(a.add1) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
-  if constexpr (NADD >= 2) x.add2 = static_cast<const char*>(a.add2) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  if constexpr (NADD == 2) x.add2 = static_cast<const char*>(a.add2) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  if constexpr (NADD == 3) {
+    x.st = reinterpret_cast<const float2*>(a.ln_stats) + static_cast<int64_t>(o) * L;
+    const int ch = x.i0c;  // pairvec: channels ch, ch + 1
+    x.g = *reinterpret_cast<const float2*>(a.ln_gamma + ch);
+    x.be = *reinterpret_cast<const float2*>(a.ln_beta + ch);
+    x.pre = a.ln_pre ? *reinterpret_cast<const float2*>(a.ln_pre + ch) : make_float2(0.f, 0.f);
+  }
   x.lds = lds;
   using G0 = PassGeom<F, TP, 0>;
   float2 tw0[G0::Q][G0::TWR];
@@ -443,6 +472,11 @@ void launch_one(const FixedArgs& a, dim3 grid, hipStream_t st) {
     if (pr) return launch_dt<K, COLS, TP, T, F, true, 0, false>(a, grid, st);
   }
   if constexpr (COLS && K != Kind::C2C) {
+    if (a.ln_stats) {  // LayerNorm IO: bf16 channel-last pairs only (host-checked)
+      if (a.bf16_in && a.bf16_out && a.pairvec)
+        hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, true, true, false, 3, true>), grid, dim3(TP * T), 0, st, a);
+      return;
+    }
     if (a.pairvec) {
       if constexpr (K == Kind::C2R) {
         if (a.add2) return launch_dt<K, COLS, TP, T, F, false, 2, true>(a, grid, st);

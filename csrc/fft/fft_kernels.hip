@@ -395,6 +395,7 @@ int64_t pass_lds_bytes(const PassDesc& d) {
 
 void launch_fft_pass(const PassDesc& d, void* stream) {
   if (launch_fft_fixed(d, stream)) return;
+  if (d.ln_stats) throw std::runtime_error("amd_dft: LayerNorm-fused pass needs a specialised (fixed) kernel");
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (d.kind) {
     case Kind::C2C: return launch_k<Kind::C2C>(d, st);

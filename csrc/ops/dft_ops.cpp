@@ -30,8 +30,10 @@
 #include <string>
 #include <unordered_map>
 
+#include "../fft/fft_fixed.h"
 #include "../fft/fft_plan.h"
 #include "../spectral/dft_gemm.h"
+#include "../spectral/spectral.h"
 #include "checks.h"
 #include "plan_cache.h"
 
@@ -87,13 +89,24 @@ int64_t lds_limit() {
   return lim;
 }
 
-void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
+// LayerNorm fused into the IO of an AFNO W-direction pass (see PassDesc::ln_stats)
+struct LnIO {
+  const float* stats = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  const float* pre = nullptr;
+};
+
+// Returns false only for an LnIO pass that no specialised kernel covers (nothing launched).
+bool run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
               const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
-              int out_hi, float scale, bool inverse, const void* add1 = nullptr, const void* add2 = nullptr) {
+              int out_hi, float scale, bool inverse, const void* add1 = nullptr, const void* add2 = nullptr,
+              const LnIO* ln = nullptr) {
+  if (ln && L > lds_limit()) return false;
   if (L > lds_limit()) {
     run_pass_large(kind, in, out, in_shape, out_shape, axis, L, in_lo, in_hi, out_lo, out_hi, scale, inverse, add1,
                    add2);
-    return;
+    return true;
   }
   auto dp = get_plan(L, in.device());
   PassDesc d;
@@ -122,7 +135,16 @@ void run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
     if (a == "nopass" || a == "io") d.npass = 0;
     if (a == "notw" || a == "io") d.tw_count = 0;
   }
-  launch_fft_pass(d, c10::hip::getCurrentHIPStream(in.device().index()).stream());
+  void* stream = c10::hip::getCurrentHIPStream(in.device().index()).stream();
+  if (ln) {
+    d.ln_stats = ln->stats;
+    d.ln_gamma = ln->gamma;
+    d.ln_beta = ln->beta;
+    d.ln_pre = ln->pre;
+    return launch_fft_fixed(d, stream);
+  }
+  launch_fft_pass(d, stream);
+  return true;
 }
 
 // ------------------------------------------------------------------ lengths beyond one LDS-resident pass
@@ -579,6 +601,182 @@ at::Tensor c2c_axis_meta(const at::Tensor& x, int64_t dim, int64_t n, int64_t in
   return at::empty(s, x.options().dtype(at::kFloat));
 }
 
+// ------------------------------------------------------------------ LayerNorm-fused AFNO W passes
+// x' = x + pre (per channel), LN(x') = (x' - mean) * rstd * gamma + beta with per-token stats
+// from ln_stats.  Channel-last [..., W, C]: the transform axis is dim -2, channels last.
+at::Tensor ln_apply(const at::Tensor& x, const at::Tensor& stats, const at::Tensor& g, const at::Tensor& b,
+                    const std::optional<at::Tensor>& pre, at::Tensor* xp_out) {
+  at::Tensor xp = x.to(at::kFloat);
+  if (pre.has_value()) xp = xp + pre->to(at::kFloat);
+  std::vector<int64_t> ss(x.sizes().begin(), x.sizes().end());
+  ss.back() = 1;
+  at::Tensor st = stats.to(at::kFloat).reshape({-1, 2});
+  at::Tensor mean = st.select(1, 0).reshape(ss), rstd = st.select(1, 1).reshape(ss);
+  if (xp_out) *xp_out = xp;
+  return (xp - mean) * rstd * g.to(at::kFloat) + b.to(at::kFloat);
+}
+
+void check_ln_args(const at::Tensor& x, int64_t dim, const at::Tensor& stats, const at::Tensor& g,
+                   const at::Tensor& b, const std::optional<at::Tensor>& pre, const char* op) {
+  TORCH_CHECK(x.dim() >= 2, "amd_dft.", op, ": needs a [..., W, C] channel-last tensor");
+  TORCH_CHECK(dim == x.dim() - 2 || dim == -2, "amd_dft.", op, ": the transform axis must be dim -2 (channel-last)");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(g.numel() == C && b.numel() == C && (!pre.has_value() || pre->numel() == C), "amd_dft.", op,
+              ": gamma/beta/pre must have one entry per channel");
+  TORCH_CHECK(stats.numel() == 2 * (x.numel() / std::max<int64_t>(C, 1)), "amd_dft.", op,
+              ": stats must hold (mean, rstd) per token");
+}
+
+at::Tensor r2c_cpu(const at::Tensor& x, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
+                   std::optional<at::ScalarType> out_dtype);
+at::Tensor c2r_cpu(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
+                   at::IntArrayRef keep, std::optional<at::ScalarType> out_dtype);
+
+at::Tensor r2c_ln_cuda(const at::Tensor& x_, int64_t dim, double scale, int64_t keep, const at::Tensor& stats_,
+                       const at::Tensor& g_, const at::Tensor& b_, const std::optional<at::Tensor>& pre_,
+                       std::optional<at::ScalarType> out_dtype) {
+  const c10::DeviceGuard guard(x_.device());
+  check_ln_args(x_, dim, stats_, g_, b_, pre_, "r2c_ln");
+  const int64_t axis = x_.dim() - 2;
+  at::Tensor x = x_.contiguous();
+  const at::ScalarType odt = out_dtype.value_or(x.scalar_type());
+  to_dtype(x.scalar_type());
+  to_dtype(odt);
+  const std::vector<int64_t> dv{axis}, kv{keep, 0};
+  R2CShape sh = r2c_shape(x.sizes(), dv, kv);
+  const DimSpec& s = sh.specs[0];
+  std::vector<int64_t> cur(x.sizes().begin(), x.sizes().end()), nxt = cur;
+  nxt[axis] = s.lo;
+  at::Tensor out = alloc_complex(nxt, x.options(), odt);
+  if (x.numel() == 0) return out.zero_();
+  at::Tensor stats = stats_.to(at::kFloat).contiguous(), g = g_.to(at::kFloat).contiguous(),
+             b = b_.to(at::kFloat).contiguous();
+  at::Tensor pre;
+  if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+  LnIO ln{stats.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(),
+          pre_.has_value() ? pre.data_ptr<float>() : nullptr};
+  const int64_t C = x.size(-1);
+  if (x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16 && !std::getenv("MI_DFT_NO_AFNO_W") &&
+      afno_w_supported(static_cast<int>(s.n), static_cast<int>(C), static_cast<int>(s.lo)) &&
+      x.numel() / (s.n * C) < (int64_t(1) << 31)) {
+    AfnoWLaunch p;  // 16-byte-lane two-pass kernel (afno_wfft.hip)
+    p.x = x.data_ptr();
+    p.stats = ln.stats;
+    p.gamma = ln.gamma;
+    p.beta = ln.beta;
+    p.pre = ln.pre;
+    p.out = out.data_ptr();
+    p.O = static_cast<int>(x.numel() / (s.n * C));
+    p.L = static_cast<int>(s.n);
+    p.C = static_cast<int>(C);
+    p.KM = static_cast<int>(s.lo);
+    p.scale = static_cast<float>(scale);
+    launch_afno_w_r2c_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return checked(out, "r2c_ln");
+  }
+  if (x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16 &&
+      run_pass(Kind::R2C, x, out, cur, nxt, static_cast<int>(axis), s.n, static_cast<int>(s.n), 0,
+               static_cast<int>(s.lo), 0, static_cast<float>(scale), false, nullptr, nullptr, &ln))
+    return checked(out, "r2c_ln");
+  // no specialised kernel for this shape: normalise with ATen, then the plain R2C
+  TORCH_WARN_ONCE("amd_dft.r2c_ln: no specialised LayerNorm-fused kernel for this shape/dtype; "
+                  "using ATen LayerNorm + the plain R2C");
+  at::Tensor h = ln_apply(x, stats, g, b, pre_, nullptr).to(x.scalar_type());
+  return r2c_cuda(h, dv, scale, kv, odt);
+}
+
+at::Tensor r2c_ln_cpu(const at::Tensor& x, int64_t dim, double scale, int64_t keep, const at::Tensor& stats,
+                      const at::Tensor& g, const at::Tensor& b, const std::optional<at::Tensor>& pre,
+                      std::optional<at::ScalarType> out_dtype) {
+  check_ln_args(x, dim, stats, g, b, pre, "r2c_ln");
+  at::Tensor h = ln_apply(x, stats, g, b, pre, nullptr).to(x.scalar_type());
+  const std::vector<int64_t> dv{x.dim() - 2}, kv{keep, 0};
+  return r2c_cpu(h, dv, scale, kv, out_dtype);
+}
+
+at::Tensor r2c_ln_meta(const at::Tensor& x, int64_t dim, double scale, int64_t keep, const at::Tensor&,
+                       const at::Tensor&, const at::Tensor&, const std::optional<at::Tensor>&,
+                       std::optional<at::ScalarType> out_dtype) {
+  std::vector<int64_t> s(x.sizes().begin(), x.sizes().end());
+  s[x.dim() - 2] = keep;
+  s.push_back(2);
+  return at::empty(s, x.options().dtype(out_dtype.value_or(x.scalar_type())));
+}
+
+// out = scale * irfft_W(X) + x' + LN(x'),  X = [..., km, C, 2], x = stored residual stream [..., W, C]
+at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double scale, const at::Tensor& x_,
+                           const at::Tensor& stats_, const at::Tensor& g_, const at::Tensor& b_,
+                           const std::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(X_.device());
+  check_ln_args(x_, dim, stats_, g_, b_, pre_, "c2r_ln_add");
+  const int64_t axis = x_.dim() - 2;
+  TORCH_CHECK(X_.dim() == x_.dim() + 1 && X_.size(-1) == 2 && x_.size(axis) == n, "amd_dft.c2r_ln_add: shape mismatch");
+  at::Tensor X = X_.contiguous(), x = x_.contiguous();
+  const int64_t km = X.size(axis);
+  const std::vector<int64_t> dv{axis}, nv{n}, kv{km, 0};
+  at::Tensor stats = stats_.to(at::kFloat).contiguous(), g = g_.to(at::kFloat).contiguous(),
+             b = b_.to(at::kFloat).contiguous();
+  at::Tensor pre;
+  if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+  if (X.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && X.numel() > 0) {
+    C2RShape sh = c2r_shape(X.sizes(), dv, nv, kv);
+    const DimSpec& s = sh.specs[0];
+    std::vector<int64_t> cur = sh.in_logical, nxt = cur;
+    nxt[axis] = s.n;
+    at::Tensor out = at::empty(nxt, x.options());
+    const int64_t half = s.n / 2 + 1;
+    const int in_lo = static_cast<int>(std::min<int64_t>(s.lo, half));
+    LnIO ln{stats.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(),
+            pre_.has_value() ? pre.data_ptr<float>() : nullptr};
+    const int64_t C = x.size(-1);
+    if (!std::getenv("MI_DFT_NO_AFNO_W") &&
+        afno_w_supported(static_cast<int>(s.n), static_cast<int>(C), static_cast<int>(km)) &&
+        x.numel() / (s.n * C) < (int64_t(1) << 31)) {
+      AfnoWLaunch p;  // 16-byte-lane two-pass kernel (afno_wfft.hip)
+      p.x = x.data_ptr();
+      p.stats = ln.stats;
+      p.gamma = ln.gamma;
+      p.beta = ln.beta;
+      p.pre = ln.pre;
+      p.spec = X.data_ptr();
+      p.out = out.data_ptr();
+      p.O = static_cast<int>(x.numel() / (s.n * C));
+      p.L = static_cast<int>(s.n);
+      p.C = static_cast<int>(C);
+      p.KM = static_cast<int>(km);
+      p.scale = static_cast<float>(scale);
+      launch_afno_w_c2r_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+      return checked(out, "c2r_ln_add");
+    }
+    if (run_pass(Kind::C2R, X, out, cur, nxt, static_cast<int>(axis), s.n, in_lo, 0, static_cast<int>(s.n), 0,
+                 static_cast<float>(scale), true, x.data_ptr(), nullptr, &ln))
+      return checked(out, "c2r_ln_add");
+  }
+  TORCH_WARN_ONCE("amd_dft.c2r_ln_add: no specialised LayerNorm-fused kernel for this shape/dtype; "
+                  "using ATen LayerNorm + the plain C2R");
+  at::Tensor xp;
+  at::Tensor h = ln_apply(x, stats, g, b, pre_, &xp);
+  return c2r_add_cuda(X, dv, nv, scale, kv, xp.to(x.scalar_type()).contiguous(), h.to(x.scalar_type()).contiguous(),
+                      x.scalar_type());
+}
+
+at::Tensor c2r_ln_add_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale, const at::Tensor& x,
+                          const at::Tensor& stats, const at::Tensor& g, const at::Tensor& b,
+                          const std::optional<at::Tensor>& pre) {
+  check_ln_args(x, dim, stats, g, b, pre, "c2r_ln_add");
+  const int64_t axis = x.dim() - 2;
+  at::Tensor xp;
+  at::Tensor h = ln_apply(x, stats, g, b, pre, &xp);
+  const std::vector<int64_t> dv{axis}, nv{n}, kv{X.size(axis), 0};
+  at::Tensor y = c2r_cpu(X, dv, nv, scale, kv, at::kFloat);
+  return (y + xp + h).to(x.scalar_type()).contiguous();
+}
+
+at::Tensor c2r_ln_add_meta(const at::Tensor&, int64_t, int64_t, double, const at::Tensor& x, const at::Tensor&,
+                           const at::Tensor&, const at::Tensor&, const std::optional<at::Tensor>&) {
+  return at::empty_like(x);
+}
+
 // ------------------------------------------------------------------ CPU impls (torch.fft)
 at::Tensor select_modes(at::Tensor y, int axis, int64_t lo, int64_t hi) {
   const int64_t n = y.size(axis);
@@ -750,6 +948,10 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("c2c_axis(Tensor x, int dim, int n, int in_lo, int in_hi, int out_lo, int out_hi, bool inverse=False, "
         "float scale=1.0) -> Tensor");
   m.def("dftw_r2c(Tensor x, int m, float scale=1.0) -> Tensor");
+  m.def("r2c_ln(Tensor x, int dim, float scale, int keep, Tensor stats, Tensor gamma, Tensor beta, Tensor? pre=None, "
+        "ScalarType? out_dtype=None) -> Tensor");
+  m.def("c2r_ln_add(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
+        "Tensor? pre=None) -> Tensor");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("plan_info(int n) -> str", &amd_dft::plan_info);
@@ -765,6 +967,8 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("c2r_add", &amd_dft::c2r_add_cuda);
   m.impl("c2c_axis", &amd_dft::c2c_axis_cuda);
   m.impl("dftw_r2c", &amd_dft::dftw_r2c_cuda);
+  m.impl("r2c_ln", &amd_dft::r2c_ln_cuda);
+  m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_cuda);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -774,6 +978,8 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("c2r_add", &amd_dft::c2r_add_cpu);
   m.impl("c2c_axis", &amd_dft::c2c_axis_cpu);
   m.impl("dftw_r2c", &amd_dft::dftw_r2c_cpu);
+  m.impl("r2c_ln", &amd_dft::r2c_ln_cpu);
+  m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_cpu);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -783,6 +989,8 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("c2r_add", &amd_dft::c2r_add_meta);
   m.impl("c2c_axis", &amd_dft::c2c_axis_meta);
   m.impl("dftw_r2c", &amd_dft::dftw_r2c_meta);
+  m.impl("r2c_ln", &amd_dft::r2c_ln_meta);
+  m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_meta);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {

@@ -311,6 +311,43 @@ std::tuple<at::Tensor, at::Tensor> layer_norm_meta(const at::Tensor& x, const at
   return {at::empty_like(x), at::empty_like(x)};
 }
 
+// ------------------------------------------------------------------ LayerNorm statistics only
+// (mean, rstd) per row of x' = x + pre: the AFNO W-transforms apply LN(x') on load.
+at::Tensor ln_stats_cpu(const at::Tensor& x, const std::optional<at::Tensor>& pre, double eps) {
+  at::Tensor xp = x.to(at::kFloat);
+  if (pre.has_value()) xp = xp + pre->to(at::kFloat);
+  xp = xp.reshape({-1, x.size(-1)});
+  auto vm = at::var_mean(xp, {1}, /*correction=*/0, /*keepdim=*/false);
+  return at::stack({std::get<1>(vm), at::rsqrt(std::get<0>(vm) + eps)}, 1).contiguous();
+}
+
+at::Tensor ln_stats_cuda(const at::Tensor& x_, const std::optional<at::Tensor>& pre_, double eps) {
+  const c10::DeviceGuard guard(x_.device());
+  const int64_t C = x_.size(-1);
+  if (x_.scalar_type() != at::kBFloat16 || C % 8 != 0 || C > 2048) return ln_stats_cpu(x_, pre_, eps);
+  at::Tensor x = x_.contiguous();
+  at::Tensor pre;
+  if (pre_.has_value()) {
+    pre = pre_->to(at::kFloat).contiguous();
+    TORCH_CHECK(pre.numel() == C, "amd_dft.ln_stats: pre must have one entry per channel");
+  }
+  const int64_t rows = x.numel() / C;
+  at::Tensor st = at::empty({rows, 2}, x.options().dtype(at::kFloat));
+  LnStatsLaunch p;
+  p.x = x.data_ptr();
+  p.pre = pre_.has_value() ? pre.data_ptr<float>() : nullptr;
+  p.stats = st.data_ptr<float>();
+  p.rows = rows;
+  p.cols = static_cast<int>(C);
+  p.eps = static_cast<float>(eps);
+  if (rows > 0) launch_ln_stats(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return checked(st, "ln_stats");
+}
+
+at::Tensor ln_stats_meta(const at::Tensor& x, const std::optional<at::Tensor>&, double) {
+  return at::empty({x.numel() / std::max<int64_t>(x.size(-1), 1), 2}, x.options().dtype(at::kFloat));
+}
+
 at::Tensor afno_spectral_meta(const at::Tensor& xw, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                               const at::Tensor&, double) {
   return at::empty_like(xw);
@@ -323,6 +360,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral(Tensor x, Tensor w1t, Tensor w2t, Tensor b1, Tensor b2, float lam) -> Tensor");
   m.def("afno_spectral_supported(int H, int block_size) -> bool", &amd_dft::afno_spectral_ok);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
+  m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
   m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
   m.def("fno_c2r_pw(Tensor yw, Tensor x, Tensor wc, Tensor? bias=None, bool gelu=True) -> Tensor");
@@ -331,6 +369,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_cuda);
   m.impl("layer_norm", &amd_dft::layer_norm_cuda);
+  m.impl("ln_stats", &amd_dft::ln_stats_cuda);
   m.impl("fno_mix", &amd_dft::fno_mix_cuda);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_cuda);
   m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cuda);
@@ -339,6 +378,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_cpu);
   m.impl("layer_norm", &amd_dft::layer_norm_cpu);
+  m.impl("ln_stats", &amd_dft::ln_stats_cpu);
   m.impl("fno_mix", &amd_dft::fno_mix_cpu);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_cpu);
   m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cpu);
@@ -347,6 +387,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_meta);
   m.impl("layer_norm", &amd_dft::layer_norm_meta);
+  m.impl("ln_stats", &amd_dft::ln_stats_meta);
   m.impl("fno_mix", &amd_dft::fno_mix_meta);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);
   m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_meta);

@@ -1,0 +1,335 @@
+// AFNO W-direction transforms with LayerNorm fused into their IO (FourCastNet 90 x 180 token
+// grid, channel-last [B, H, W=180, C] bf16).  Two kernels per block:
+//
+//   afno_w_r2c_ln : X[o, k, c] = scale * sum_w LN1(x'[o, w, :])[c] e^{-2 pi i k w / 180},  k < KM
+//   afno_w_c2r_ln : y[o, w, c] = scale * irfft_w(Y[o, :, c]) + x'[o, w, c] + LN1(x')[o, w, c]
+//
+// with x' = x + pre (pre = the previous block's fc2 bias, carried per channel), o = (b, h) and
+// per-token LayerNorm statistics from ln_stats.  Same math as the generic fixed-kernel path
+// (fft_fixed_impl.h, NADD = 3) but laid out for the memory system:
+//  * a lane owns 4 consecutive channels = 2 packed real pairs (z = x_c + i x_{c+1}): every
+//    global access is an 8- or 16-byte vector (the generic column kernel moves 4 bytes per
+//    lane); 16 lanes cover 64 channels = one full 128-byte line per row;
+//  * 180 = 12 x 15 Cooley-Tukey in two register passes: pass 0 (12-point DFTs over
+//    n = n2 + 15 n1, one thread per n2, straight from global) and pass 1 (15-point DFTs, one
+//    thread per k1) with one LDS transpose between them; the C2R output and its addends
+//    stream straight from registers to global;
+//  * the C2R input is the pruned half spectrum: which of the 12 pass-0 inputs can be non-zero
+//    is resolved at compile time from KM (6 of 12 loads at KM = 46), the rest are constants.
+// Reference: the AFNO filter runs rfft2/irfft2 on the whole [B, C, H, W] tensor after a
+// separate LayerNorm kernel (FourCastNet AFNO2D; this repo's SURVEY.md §2.5 K5/K1e).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../fft/radix.h"
+#include "spectral.h"
+#include "w180_table.h"
+
+namespace amd_dft {
+namespace {
+
+constexpr int kL = 180, kA = 12, kB = 15;  // n = kB * n1 + n2, k = k1 + kA * k2
+constexpr int kPPL = 2;                     // packed pairs per lane (4 channels)
+constexpr int kCh = 2 * kPPL;               // channels per lane
+constexpr int kG = 16;                      // lanes per row: 64 channels / workgroup
+constexpr int kSlab = kCh * kG;             // 64
+constexpr int kPairs = kPPL * kG;           // packed pairs per workgroup
+constexpr int kPitch = kPairs + 2;          // float2 per LDS position (+16 B: spreads the k1 stride)
+constexpr int kThreads = kB * kG;           // 240
+
+__device__ __forceinline__ void unpack4(uint2 u, float (&f)[4]) {
+  f[0] = __uint_as_float(u.x << 16);
+  f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16);
+  f[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t bfpack(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 v;
+  v[0] = static_cast<__bf16>(a);
+  v[1] = static_cast<__bf16>(b);
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+struct WArgs {
+  const uint16_t* x;     // [O, 180, C] bf16 (stored residual stream)
+  const float2* stats;   // [O, 180] (mean, rstd) of x'
+  const float* gamma;    // [C]
+  const float* beta;     // [C]
+  const float* pre;      // [C] or nullptr
+  const uint16_t* spec;  // C2R input [O, KM, C, 2] bf16
+  uint16_t* out;         // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
+  int C, nslab;
+  float scale;
+};
+
+struct ChanParams {
+  float g[kCh], b[kCh], p[kCh];
+};
+
+__device__ __forceinline__ void load_params(const WArgs& a, int c0, ChanParams& cp) {
+  const float4 g4 = *reinterpret_cast<const float4*>(a.gamma + c0);
+  const float4 b4 = *reinterpret_cast<const float4*>(a.beta + c0);
+  const float4 p4 = a.pre ? *reinterpret_cast<const float4*>(a.pre + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  cp.g[0] = g4.x; cp.g[1] = g4.y; cp.g[2] = g4.z; cp.g[3] = g4.w;
+  cp.b[0] = b4.x; cp.b[1] = b4.y; cp.b[2] = b4.z; cp.b[3] = b4.w;
+  cp.p[0] = p4.x; cp.p[1] = p4.y; cp.p[2] = p4.z; cp.p[3] = p4.w;
+}
+
+// x' (4 channels) and LN(x') of one token
+__device__ __forceinline__ void ln4(const uint2 raw, const float2 st, const ChanParams& cp, float (&xp)[kCh],
+                                    float (&h)[kCh]) {
+  unpack4(raw, xp);
+#pragma unroll
+  for (int i = 0; i < kCh; ++i) {
+    xp[i] += cp.p[i];
+    h[i] = (xp[i] - st.x) * st.y * cp.g[i] + cp.b[i];
+  }
+}
+
+// pass 0 epilogue: 12-point DFTs, twiddle W_180^{n2 k1}, store s[k1] at LDS position k1 * 15 + n2
+__device__ __forceinline__ void pass0_store(float2 (&v)[kPPL][kA], int n2, int g, float2* lds) {
+#pragma unroll
+  for (int p = 0; p < kPPL; ++p) Dft<kA>::run(v[p]);
+#pragma unroll
+  for (int k1 = 0; k1 < kA; ++k1) {
+    const float2 w = kW180[n2 * k1];  // n2 * k1 <= 154
+    const float2 t0 = k1 == 0 ? v[0][0] : c_mul(v[0][k1], w);
+    const float2 t1 = k1 == 0 ? v[1][0] : c_mul(v[1][k1], w);
+    *reinterpret_cast<float4*>(lds + (k1 * kB + n2) * kPitch + kPPL * g) = make_float4(t0.x, t0.y, t1.x, t1.y);
+  }
+}
+
+// pass 1: 15-point DFTs of row k1; result u[p][k2] = X[k1 + 12 k2]
+__device__ __forceinline__ void pass1(int k1, int g, const float2* lds, float2 (&u)[kPPL][kB]) {
+#pragma unroll
+  for (int n2 = 0; n2 < kB; ++n2) {
+    const float4 q = *reinterpret_cast<const float4*>(lds + (k1 * kB + n2) * kPitch + kPPL * g);
+    u[0][n2] = make_float2(q.x, q.y);
+    u[1][n2] = make_float2(q.z, q.w);
+  }
+#pragma unroll
+  for (int p = 0; p < kPPL; ++p) Dft<kB>::run(u[p]);
+}
+
+template <int KM>
+__global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
+  const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
+  const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
+  const int c0 = slab * kSlab + kCh * g;
+  const int C = a.C;
+  const uint16_t* xr = a.x + static_cast<int64_t>(o) * kL * C + c0;
+  const float2* st = a.stats + static_cast<int64_t>(o) * kL;
+  // ---- pass 0: n = n2 + 15 n1 straight from global, LayerNorm on load
+  uint2 raw[kA];
+  float2 sv[kA];
+#pragma unroll
+  for (int n1 = 0; n1 < kA; ++n1) {
+    const int n = n2 + kB * n1;
+    raw[n1] = *reinterpret_cast<const uint2*>(xr + static_cast<int64_t>(n) * C);
+    sv[n1] = st[n];
+  }
+  ChanParams cp;
+  load_params(a, c0, cp);
+  float2 v[kPPL][kA];
+#pragma unroll
+  for (int n1 = 0; n1 < kA; ++n1) {
+    float xp[kCh], h[kCh];
+    ln4(raw[n1], sv[n1], cp, xp, h);
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) v[p][n1] = make_float2(h[2 * p], h[2 * p + 1]);
+  }
+  pass0_store(v, n2, g, lds);
+  __syncthreads();
+  // ---- pass 1 (threads k1 < 12), result back to LDS in natural order k = k1 + 12 k2
+  float2 u[kPPL][kB];
+  const int k1 = n2;
+  if (k1 < kA) pass1(k1, g, lds, u);
+  __syncthreads();
+  if (k1 < kA) {
+#pragma unroll
+    for (int k2 = 0; k2 < kB; ++k2)
+      *reinterpret_cast<float4*>(lds + (k1 + kA * k2) * kPitch + kPPL * g) =
+          make_float4(u[0][k2].x, u[0][k2].y, u[1][k2].x, u[1][k2].y);
+  }
+  __syncthreads();
+  // ---- separate the packed pairs: X_a[k] = (Z[k] + conj Z[L-k]) / 2, X_b[k] = (Z[k] - conj Z[L-k]) / 2i
+  const float hs = 0.5f * a.scale;
+  uint16_t* orow = a.out + static_cast<int64_t>(o) * KM * C * 2;
+  constexpr int kItems = KM * kG;
+#pragma unroll
+  for (int it = 0; it < (kItems + kThreads - 1) / kThreads; ++it) {
+    const int item = it * kThreads + threadIdx.x;
+    if (item >= kItems) break;
+    const int k = item / kG, gg = item % kG;
+    const int km = k == 0 ? 0 : kL - k;
+    const float4 zk = *reinterpret_cast<const float4*>(lds + k * kPitch + kPPL * gg);
+    const float4 zm = *reinterpret_cast<const float4*>(lds + km * kPitch + kPPL * gg);
+    const float2 Zk[2] = {{zk.x, zk.y}, {zk.z, zk.w}};
+    const float2 Zm[2] = {{zm.x, zm.y}, {zm.z, zm.w}};
+    uint32_t w[4];
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+      const float2 xa = make_float2((Zk[p].x + Zm[p].x) * hs, (Zk[p].y - Zm[p].y) * hs);
+      const float2 xb = make_float2((Zk[p].y + Zm[p].y) * hs, (Zm[p].x - Zk[p].x) * hs);
+      w[2 * p] = bfpack(xa.x, xa.y);
+      w[2 * p + 1] = bfpack(xb.x, xb.y);
+    }
+    *reinterpret_cast<uint4*>(orow + (static_cast<int64_t>(k) * C + slab * kSlab + kCh * gg) * 2) =
+        make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// compile-time support of the pruned C2R input: 0 = never stored, 1 = always, 2 = depends on n2
+template <int KM>
+constexpr int c2r_load_kind(int n1) {
+  bool all = true, any = false;
+  for (int n = kB * n1; n < kB * n1 + kB; ++n) {
+    const bool ok = n < KM || kL - n < KM;
+    all = all && ok;
+    any = any || ok;
+  }
+  return all ? 1 : (any ? 2 : 0);
+}
+
+template <int KM>
+__global__ void __launch_bounds__(kThreads) afno_w_c2r_ln_kernel(const WArgs a) {
+  static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
+  __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
+  const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
+  const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
+  const int c0 = slab * kSlab + kCh * g;
+  const int C = a.C;
+  const uint16_t* srow = a.spec + static_cast<int64_t>(o) * KM * C * 2 + c0 * 2;
+  // ---- pass 0: Hermitian assembly of the packed pair spectrum Z = X_a + i X_b, conjugated
+  // (inverse transform as conj(FFT(conj Z))); only the stored modes are loaded
+  uint4 raw[kA];
+#pragma unroll
+  for (int n1 = 0; n1 < kA; ++n1) {
+    if (c2r_load_kind<KM>(n1) != 0) {
+      const int n = n2 + kB * n1;
+      const int kk = 2 * n > kL ? kL - n : n;
+      const int kc = kk < KM ? kk : 0;  // clamped: unconditional load, masked below
+      raw[n1] = *reinterpret_cast<const uint4*>(srow + static_cast<int64_t>(kc) * C * 2);
+    }
+  }
+  float2 v[kPPL][kA];
+#pragma unroll
+  for (int n1 = 0; n1 < kA; ++n1) {
+    const int kind = c2r_load_kind<KM>(n1);
+    if (kind == 0) {
+#pragma unroll
+      for (int p = 0; p < kPPL; ++p) v[p][n1] = make_float2(0.f, 0.f);
+      continue;
+    }
+    const int n = n2 + kB * n1;
+    const bool upper = 2 * n > kL;
+    const int kk = upper ? kL - n : n;
+    const bool ok = kind == 1 || kk < KM;
+    float f[8];
+    unpack4(make_uint2(raw[n1].x, raw[n1].y), *reinterpret_cast<float(*)[4]>(f));
+    unpack4(make_uint2(raw[n1].z, raw[n1].w), *reinterpret_cast<float(*)[4]>(f + 4));
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+      // channel pair (c0 + 2p, c0 + 2p + 1): A = X_a[kk], B = X_b[kk] (complex)
+      float2 A = make_float2(f[4 * p], f[4 * p + 1]);
+      float2 B = make_float2(f[4 * p + 2], f[4 * p + 3]);
+      if (kk == 0 || 2 * kk == kL) {
+        A.y = 0.f;
+        B.y = 0.f;
+      }
+      if (upper) {
+        A.y = -A.y;
+        B.y = -B.y;
+      }
+      const float2 z = make_float2(A.x - B.y, -(A.y + B.x));  // conj(A + iB)
+      v[p][n1] = ok ? z : make_float2(0.f, 0.f);
+    }
+  }
+  pass0_store(v, n2, g, lds);
+  __syncthreads();
+  const int k1 = n2;
+  if (k1 >= kA) return;
+  // residual-stream addends of this thread's outputs (latency under the pass-1 LDS reads)
+  const uint16_t* xr = a.x + static_cast<int64_t>(o) * kL * C + c0;
+  const float2* st = a.stats + static_cast<int64_t>(o) * kL;
+  uint2 xraw[kB];
+  float2 sv[kB];
+#pragma unroll
+  for (int k2 = 0; k2 < kB; ++k2) {
+    const int n = k1 + kA * k2;
+    xraw[k2] = *reinterpret_cast<const uint2*>(xr + static_cast<int64_t>(n) * C);
+    sv[k2] = st[n];
+  }
+  ChanParams cp;
+  load_params(a, c0, cp);
+  float2 u[kPPL][kB];
+  pass1(k1, g, lds, u);
+  // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
+  uint16_t* orow = a.out + static_cast<int64_t>(o) * kL * C + c0;
+  const float sc = a.scale;
+#pragma unroll
+  for (int k2 = 0; k2 < kB; ++k2) {
+    const int n = k1 + kA * k2;
+    float xp[kCh], h[kCh];
+    ln4(xraw[k2], sv[k2], cp, xp, h);
+    uint32_t w[kPPL];
+#pragma unroll
+    for (int p = 0; p < kPPL; ++p) {
+      const float ya = u[p][k2].x * sc + xp[2 * p] + h[2 * p];
+      const float yb = -u[p][k2].y * sc + xp[2 * p + 1] + h[2 * p + 1];
+      w[p] = bfpack(ya, yb);
+    }
+    *reinterpret_cast<uint2*>(orow + static_cast<int64_t>(n) * C) = make_uint2(w[0], w[1]);
+  }
+}
+
+WArgs make_args(const AfnoWLaunch& p) {
+  WArgs a;
+  a.x = static_cast<const uint16_t*>(p.x);
+  a.stats = reinterpret_cast<const float2*>(p.stats);
+  a.gamma = p.gamma;
+  a.beta = p.beta;
+  a.pre = p.pre;
+  a.spec = static_cast<const uint16_t*>(p.spec);
+  a.out = static_cast<uint16_t*>(p.out);
+  a.C = p.C;
+  a.nslab = p.C / kSlab;
+  a.scale = p.scale;
+  return a;
+}
+
+void check_launch(const AfnoWLaunch& p, const char* what) {
+  if (!afno_w_supported(p.L, p.C, p.KM)) throw std::runtime_error(std::string("amd_dft: ") + what + ": unsupported shape");
+  const int64_t nwg = static_cast<int64_t>(p.O) * (p.C / kSlab);
+  if (nwg <= 0 || nwg > 0x7fffffffLL) throw std::runtime_error(std::string("amd_dft: ") + what + ": bad grid");
+  if (static_cast<int64_t>(p.O) * kL * p.C >= (int64_t(1) << 40)) throw std::runtime_error("amd_dft: afno_w: too large");
+}
+
+}  // namespace
+
+bool afno_w_supported(int L, int C, int KM) { return L == kL && C % kSlab == 0 && KM == 46; }
+
+void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream) {
+  check_launch(p, "afno_w_r2c_ln");
+  const WArgs a = make_args(p);
+  const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
+  hipLaunchKernelGGL(afno_w_r2c_ln_kernel<46>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_w_r2c_ln launch: ") + hipGetErrorString(e));
+}
+
+void launch_afno_w_c2r_ln(const AfnoWLaunch& p, void* stream) {
+  check_launch(p, "afno_w_c2r_ln");
+  const WArgs a = make_args(p);
+  const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
+  hipLaunchKernelGGL(afno_w_c2r_ln_kernel<46>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_w_c2r_ln launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft

@@ -115,7 +115,76 @@ void launch_bf16(const LayerNormLaunch& p, hipStream_t st) {
                        p.rows, p.cols, p.eps);
 }
 
+// Statistics only: (mean, rstd) of x' = x + pre per row, fp32 [rows, 2].  The normalised
+// row is never written: the consumers (AFNO W-transforms) apply LN(x') on load.
+template <int NCH, bool PRE>
+__global__ void __launch_bounds__(64 * kWaves) ln_stats_kernel(const uint16_t* __restrict__ x,
+                                                               const float* __restrict__ pre, float2* __restrict__ st,
+                                                               int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nchunk = cols >> 3;
+  const uint16_t* xr = x + row * cols;
+  float v[NCH][8];
+  bool ok[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + 64 * c;
+    ok[c] = ch < nchunk;
+    const int chc = ok[c] ? ch : 0;
+    unpack8(*reinterpret_cast<const uint4*>(xr + chc * 8), v[c]);
+    if constexpr (PRE) {
+      const float4 p0 = *reinterpret_cast<const float4*>(pre + chc * 8);
+      const float4 p1 = *reinterpret_cast<const float4*>(pre + chc * 8 + 4);
+      v[c][0] += p0.x; v[c][1] += p0.y; v[c][2] += p0.z; v[c][3] += p0.w;
+      v[c][4] += p1.x; v[c][5] += p1.y; v[c][6] += p1.z; v[c][7] += p1.w;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += ok[c] ? v[c][i] : 0.f;
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[c][i] - mean;
+      q += ok[c] ? d * d : 0.f;
+    }
+  const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+  if (lane == 0) st[row] = make_float2(mean, rstd);
+}
+
+template <int NCH>
+void launch_stats_n(const LnStatsLaunch& p, hipStream_t st) {
+  const dim3 grid(static_cast<uint32_t>((p.rows + kWaves - 1) / kWaves));
+  const auto* x = static_cast<const uint16_t*>(p.x);
+  auto* o = reinterpret_cast<float2*>(p.stats);
+  if (p.pre)
+    hipLaunchKernelGGL((ln_stats_kernel<NCH, true>), grid, dim3(64 * kWaves), 0, st, x, p.pre, o, p.rows, p.cols, p.eps);
+  else
+    hipLaunchKernelGGL((ln_stats_kernel<NCH, false>), grid, dim3(64 * kWaves), 0, st, x, nullptr, o, p.rows, p.cols,
+                       p.eps);
+}
+
 }  // namespace
+
+void launch_ln_stats(const LnStatsLaunch& p, void* stream) {
+  if (p.cols % 8 != 0 || p.cols > 64 * 8 * 4)
+    throw std::runtime_error("amd_dft: ln_stats kernel supports bf16 rows with cols % 8 == 0 and cols <= 2048");
+  if (p.rows > static_cast<int64_t>(0x7fffffff) * kWaves) throw std::runtime_error("amd_dft: ln_stats: too many rows");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nch = (p.cols / 8 + 63) / 64;
+  if (nch <= 1) launch_stats_n<1>(p, st);
+  else if (nch == 2) launch_stats_n<2>(p, st);
+  else launch_stats_n<4>(p, st);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ln_stats launch: ") + hipGetErrorString(e));
+}
 
 void launch_layernorm(const LayerNormLaunch& p, void* stream) {
   if (!p.bf16 || p.cols % 8 != 0 || p.cols > 64 * 8 * 4)

@@ -59,4 +59,31 @@ struct LayerNormLaunch {
 };
 void launch_layernorm(const LayerNormLaunch& p, void* stream);
 
+// ---- AFNO W-direction transforms with LayerNorm fused into the IO (afno_wfft.hip)
+struct AfnoWLaunch {
+  const void* x = nullptr;        // [O, L, C] bf16 stored residual stream
+  const float* stats = nullptr;   // [O, L, 2] (mean, rstd) of x + pre
+  const float* gamma = nullptr;   // [C] fp32
+  const float* beta = nullptr;    // [C] fp32
+  const float* pre = nullptr;     // [C] fp32 or nullptr
+  const void* spec = nullptr;     // C2R input [O, KM, C, 2] bf16
+  void* out = nullptr;            // R2C: [O, KM, C, 2] bf16; C2R: [O, L, C] bf16
+  int O = 0, L = 0, C = 0, KM = 0;
+  float scale = 1.f;
+};
+bool afno_w_supported(int L, int C, int KM);
+void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream);
+void launch_afno_w_c2r_ln(const AfnoWLaunch& p, void* stream);
+
+// ---- LayerNorm statistics only: stats[r] = (mean, rstd) of x[r, :] + pre (bf16 rows)
+struct LnStatsLaunch {
+  const void* x;       // [rows, cols] bf16
+  const float* pre;    // [cols] fp32 or nullptr
+  float* stats;        // [rows, 2] fp32
+  int64_t rows;
+  int cols;
+  float eps;
+};
+void launch_ln_stats(const LnStatsLaunch& p, void* stream);
+
 }  // namespace amd_dft

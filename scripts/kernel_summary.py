@@ -9,7 +9,7 @@ def short(n: str) -> str:
     m = re.search(r"fft_fixed_kernel<\(amd_dft::Kind\)(\d), (\w+), (\d+), (\d+), amd_dft::fixed_detail::FL<(.*?)>", n)
     if m:
         return f"fft_fixed K{m.group(1)} cols={m.group(2)} TP={m.group(3)} T={m.group(4)} R=<{m.group(5)}>"
-    for k in ("afno_spectral_kernel", "ln_bf16_kernel", "fft_pass_kernel", "fno_mix", "fno_pointwise_kernel", "patch_remap", "fno_c2r_pw_kernel", "dftw_r2c_kernel", "gemm_bf16_kernel"):
+    for k in ("afno_spectral_kernel", "ln_bf16_kernel", "fft_pass_kernel", "fno_mix", "fno_pointwise_kernel", "patch_remap", "fno_c2r_pw_kernel", "dftw_r2c_kernel", "gemm_bf16_kernel", "ln_stats_kernel"):
         if k in n:
             return k + (n[n.index(k) + len(k):][:40])
     return n[:110]

@@ -231,6 +231,12 @@ class AFNONet(nn.Module):
                 pending = None
                 for blk in self.blocks:
                     t, pending = S.afno_block_amd(blk, t, pending)
+                if pending is not None and pending.dim() == 1:
+                    # per-channel residual bias left by the LN-fused blocks: folded into the
+                    # head GEMM's bias, head(t + p) = head(t) + W_head p
+                    return torch.ops.amd_dft.unpatchify(
+                        F.linear(t, self._head_weight_cpp(), self._head_bias_cpp(pending)), cfg.out_chans, cfg.h,
+                        cfg.w, p)
                 if pending is not None:
                     t = t + pending
         else:
@@ -285,6 +291,16 @@ class AFNONet(nn.Module):
             cur.wait_stream(s)
             x.record_stream(cur)
         return torch.cat(ts, 0)
+
+    def _head_bias_cpp(self, pre: torch.Tensor) -> torch.Tensor:
+        """W_head(c_out, p1, p2 order) @ pre, cached per (weight, pre) version."""
+        w = self._head_weight_cpp()
+        key = (w.data_ptr(), w._version, pre.data_ptr(), pre._version, w.dtype)
+        if getattr(self, "_hb_key", None) != key:
+            with torch.no_grad():
+                self._hb = (w.float() @ pre.float()).to(w.dtype)
+            self._hb_key = key
+        return self._hb
 
     def _head_weight_cpp(self) -> torch.Tensor:
         """Head weight with rows reordered from (p1, p2, c_out) to (c_out, p1, p2); cached."""

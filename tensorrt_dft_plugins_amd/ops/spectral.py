@@ -17,7 +17,7 @@ from .._loader import load_plugins
 from . import dft as D
 
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
-           "afno_block_amd", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
+           "afno_block_amd", "afno_block_fused", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
 
 
 def _ops():
@@ -90,13 +90,84 @@ def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
 def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
     """One FourCastNet block on the MI355X path (bf16 activations).
 
-    Residual-stream fusion: the block returns ``(x, y)`` with the true block output being
-    ``x + y`` (``y`` = fc2 output incl. bias).  The addition is fused into the next block's
-    LN1 (which also writes the summed residual stream), so fc2 needs no residual GEMM input
-    (hipBLASLt would copy it into the output first) and no separate bias/residual kernels.
+    Residual-stream fusion: the block returns ``(x, p)`` with the true block output being
+    ``x + p``.  ``p`` is either a per-channel vector (the fc2 bias; LayerNorm-fused path, see
+    :func:`afno_block_fused`) or a full tensor (the fc2 output; generic path, where the addition
+    is fused into the next block's LN1).
     """
+    if pending is not None and pending.dim() == 1 and not _ln_fused_ok(blk, x):
+        x, pending = x + pending, None
+    if (pending is None or pending.dim() == 1) and _ln_fused_ok(blk, x):
+        return afno_block_fused(blk, x, pending)
     x, yn = afno_block_spectral(blk, x, pending)
     return x, afno_block_mlp(blk, yn)
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    """fp32 contiguous copy of a small parameter, cached per tensor version (capture safe)."""
+    key = ("f32", id(t), t.data_ptr(), t._version, str(t.device), t.dtype)
+    hit = _pack_cache.get(key)
+    if hit is None:
+        with torch.no_grad():
+            hit = t.detach().float().contiguous()
+        if len(_pack_cache) > 256:
+            _pack_cache.clear()
+        _pack_cache[key] = hit
+    return hit
+
+
+def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
+    from ..models.afno import kept_window
+
+    f = blk.filter
+    c = f.cfg
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[-1] % 8 == 0):
+        return False
+    B, H, W, C = x.shape
+    r0, r1, _ = kept_window(H, W, c.hard_thresholding_fraction)
+    return r0 == 0 and r1 == H and afno_fused_available(x, c.num_blocks)
+
+
+def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
+    """FourCastNet block with LN1 fused into the AFNO W-transforms and fc2 accumulated in place.
+
+    The residual stream is carried as ``(xs, pre)`` with true x = xs + pre (pre = the previous
+    block's fc2 bias, per channel, or None):
+
+      stats = (mean, rstd) of x                  ln_stats: reads xs once, writes 8 B/token
+      X_w   = R2C_W(LN1(x))                      LN applied on load (no normalised copy in HBM)
+      Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral (MFMA)
+      x1    = C2R_W(Y_w) + LN1(x) + x            both skips from one read of xs
+      yn    = LN2(x1); h = GELU(fc1(yn))         hipBLASLt, GELU epilogue
+      x1   += h @ W2^T                           hipBLASLt beta = 1, in place (no bias pass)
+
+    Returns (x1, fc2.bias): the bias is folded into the next block's statistics and loads
+    (or the head GEMM's bias).  Saves the LN1 kernel's normalised write + residual write and
+    one full-tensor read in the C2R versus :func:`afno_block_spectral`.
+    """
+    from ..models.afno import kept_window
+
+    f = blk.filter
+    c = f.cfg
+    n1 = blk.norm1
+    B, H, W, C = xs.shape
+    _, _, km = kept_window(H, W, c.hard_thresholding_fraction)
+    scale = 1.0 / math.sqrt(H * W)
+    ops = _ops()
+    pre32 = None if pre is None else _f32(pre)
+    g1, be1 = _f32(n1.weight), _f32(n1.bias)
+    stats = ops.ln_stats(xs, pre32, n1.eps)
+    xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.bfloat16)
+    yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold)
+    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    yn, _ = layer_norm(x1, blk.norm2)
+    m = blk.mlp
+    hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
+    if torch.jit.is_tracing():
+        x1 = torch.addmm(x1.reshape(-1, C), hid, m.fc2.weight.t()).reshape(B, H, W, C)
+    else:
+        x1.view(-1, C).addmm_(hid, m.fc2.weight.t())
+    return x1, m.fc2.bias
 
 
 def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
