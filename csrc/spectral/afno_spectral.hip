@@ -8,8 +8,8 @@
 //   IFFT_H (register last pass, stored straight to global)
 // where W' = [[W0, W1], [-W1, W0]] is the real 192x192 form of the complex 96x96 block weight
 // (pre-packed transposed, [n][k], so a lane's B fragment is 16 contiguous bytes).
-// Everything between the global load and the global store stays in 69 KB of LDS and in
-// registers (2 workgroups / CU); the reference FourCastNet path is ~10 separate kernels with
+// Everything between the global load and the global store stays in 38 KB of LDS (fp16 FFT
+// staging aliased with the bf16 GEMM tile) and in registers (3 workgroups / CU); the reference FourCastNet path is ~10 separate kernels with
 // 4 spectrum round trips through HBM.
 #include <hip/hip_runtime.h>
 
@@ -32,6 +32,16 @@ constexpr int kK = 2 * kBS;   // real-block GEMM K = N = 192
 constexpr int kAPitch = kK + 8;  // bf16 elements per A row (+16 B pad: ds_read_b128 spread)
 
 __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+
+// FFT staging in LDS as fp16 complex (half the bytes of fp32: 3 workgroups per CU instead of
+// 2).  fp16 keeps 11 significant bits (the GEMM operands downstream are bf16, 8 bits); the
+// spectra of the AFNO filter stay orders of magnitude inside fp16 range.
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_h(h2_t* p, int i, float2 v) { p[i] = h2_t{static_cast<_Float16>(v.x), static_cast<_Float16>(v.y)}; }
+__device__ __forceinline__ float2 ld_h(const h2_t* p, int i) {
+  const h2_t h = p[i];
+  return make_float2(static_cast<float>(h[0]), static_cast<float>(h[1]));
+}
 
 template <bool BF>
 __device__ __forceinline__ float2 ldc(const void* p, int64_t off) {  // off in scalars
@@ -126,10 +136,10 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
 }
 
 template <int L, int R0, int R1, bool BFI, bool BFO>
-__global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a) {
+__global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a) {
   static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
-  extern __shared__ __attribute__((aligned(16))) float2 lds[];  // [L][96] complex fp32 (69 KB at L=90)
-  uint16_t* A = reinterpret_cast<uint16_t*>(lds);               // aliases lds: [96][kAPitch] bf16
+  extern __shared__ __attribute__((aligned(16))) h2_t lds[];  // [L][96] complex fp16 (34.5 KB at L=90)
+  uint16_t* A = reinterpret_cast<uint16_t*>(lds);             // aliases lds: [96][kAPitch] bf16 (38.4 KB)
   const int tid = threadIdx.x;
   const int blk = blockIdx.x % a.NB;
   const int bk = blockIdx.x / a.NB;  // b * KM + kw
@@ -161,7 +171,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int t = bb % kBS, j = bb / kBS;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) lds[(j * R0 + r) * kBS + t] = v[q][r];
+        for (int r = 0; r < R0; ++r) st_h(lds, (j * R0 + r) * kBS + t, v[q][r]);
       }
     }
   }
@@ -175,7 +185,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int t = bb % kBS, j = bb / kBS;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = lds[(j + r * P1::LR) * kBS + t];
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_h(lds, (j + r * P1::LR) * kBS + t);
       }
     }
     __syncthreads();
@@ -220,7 +230,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
   // ---------------- GEMM2 + bias + softshrink -> X (fp32 complex, conjugated for the inverse)
   gemm_96x192(A, w2t, acc);
   __syncthreads();
-  float* X = reinterpret_cast<float*>(lds);
+  _Float16* X = reinterpret_cast<_Float16*>(lds);
   const float lam = a.lambda;
 #pragma unroll
   for (int nj = 0; nj < 3; ++nj) {
@@ -237,7 +247,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
         if (m < L) {
           const float v = acc[mi][nj][i] + bias;
           const float s = v > lam ? v - lam : (v < -lam ? v + lam : 0.f);
-          X[(m * kBS + c) * 2 + part] = sgn * s;
+          X[(m * kBS + c) * 2 + part] = static_cast<_Float16>(sgn * s);
         }
       }
   }
@@ -251,7 +261,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int t = bb % kBS, j = bb / kBS;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = lds[(j + r * P0::LR) * kBS + t];
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_h(lds, (j + r * P0::LR) * kBS + t);
       }
     }
     __syncthreads();
@@ -262,7 +272,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int t = bb % kBS, j = bb / kBS;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) lds[(j * R0 + r) * kBS + t] = v[q][r];
+        for (int r = 0; r < R0; ++r) st_h(lds, (j * R0 + r) * kBS + t, v[q][r]);
       }
     }
   }
@@ -276,7 +286,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int t = bb % kBS, j = bb / kBS;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = lds[(j + r * P1::LR) * kBS + t];
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_h(lds, (j + r * P1::LR) * kBS + t);
       }
     }
     h_twiddle_dft<R1, L, R0, 0, P1::Q>(v, a.tw);
@@ -299,7 +309,11 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_kernel(const AfnoArgs a)
 
 bool afno_spectral_supported(int H, int block_size) { return H == 90 && block_size == kBS; }
 
-int64_t afno_spectral_lds_bytes(int H) { return static_cast<int64_t>(H) * kBS * sizeof(float2); }
+int64_t afno_spectral_lds_bytes(int H) {
+  const int64_t staging = static_cast<int64_t>(H) * kBS * 4;  // fp16 complex
+  const int64_t a_tile = static_cast<int64_t>(kBS) * kAPitch * 2;  // bf16 GEMM operand (aliased)
+  return staging > a_tile ? staging : a_tile;
+}
 
 void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   if (!afno_spectral_supported(p.H, p.C / p.NB)) throw std::runtime_error("amd_dft: afno_spectral: unsupported shape");
