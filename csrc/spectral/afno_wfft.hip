@@ -90,8 +90,31 @@ __device__ __forceinline__ void ln4(const uint2 raw, const float2 st, const Chan
   }
 }
 
+// LDS image of one position: kPitch slots per position, a lane's 2 pairs in slots 2g, 2g+1.
+// fp32 (float2 slots) or fp16 (h2_t slots: half the bytes -> twice the workgroups per CU).
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_pair(float2* l, int i, float2 a, float2 b) {
+  *reinterpret_cast<float4*>(l + i) = make_float4(a.x, a.y, b.x, b.y);
+}
+__device__ __forceinline__ void st_pair(h2_t* l, int i, float2 a, float2 b) {
+  *reinterpret_cast<h4_t*>(l + i) = h4_t{static_cast<_Float16>(a.x), static_cast<_Float16>(a.y),
+                                         static_cast<_Float16>(b.x), static_cast<_Float16>(b.y)};
+}
+__device__ __forceinline__ void ld_pair(const float2* l, int i, float2& a, float2& b) {
+  const float4 q = *reinterpret_cast<const float4*>(l + i);
+  a = make_float2(q.x, q.y);
+  b = make_float2(q.z, q.w);
+}
+__device__ __forceinline__ void ld_pair(const h2_t* l, int i, float2& a, float2& b) {
+  const h4_t q = *reinterpret_cast<const h4_t*>(l + i);
+  a = make_float2(static_cast<float>(q[0]), static_cast<float>(q[1]));
+  b = make_float2(static_cast<float>(q[2]), static_cast<float>(q[3]));
+}
+
 // pass 0 epilogue: 12-point DFTs, twiddle W_180^{n2 k1}, store s[k1] at LDS position k1 * 15 + n2
-__device__ __forceinline__ void pass0_store(float2 (&v)[kPPL][kA], int n2, int g, float2* lds) {
+template <class T>
+__device__ __forceinline__ void pass0_store(float2 (&v)[kPPL][kA], int n2, int g, T* lds) {
 #pragma unroll
   for (int p = 0; p < kPPL; ++p) Dft<kA>::run(v[p]);
 #pragma unroll
@@ -99,39 +122,38 @@ __device__ __forceinline__ void pass0_store(float2 (&v)[kPPL][kA], int n2, int g
     const float2 w = kW180[n2 * k1];  // n2 * k1 <= 154
     const float2 t0 = k1 == 0 ? v[0][0] : c_mul(v[0][k1], w);
     const float2 t1 = k1 == 0 ? v[1][0] : c_mul(v[1][k1], w);
-    *reinterpret_cast<float4*>(lds + (k1 * kB + n2) * kPitch + kPPL * g) = make_float4(t0.x, t0.y, t1.x, t1.y);
+    st_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, t0, t1);
   }
 }
 
 // pass 1: 15-point DFTs of row k1; result u[p][k2] = X[k1 + 12 k2]
-__device__ __forceinline__ void pass1(int k1, int g, const float2* lds, float2 (&u)[kPPL][kB]) {
+template <class T>
+__device__ __forceinline__ void pass1(int k1, int g, const T* lds, float2 (&u)[kPPL][kB]) {
 #pragma unroll
-  for (int n2 = 0; n2 < kB; ++n2) {
-    const float4 q = *reinterpret_cast<const float4*>(lds + (k1 * kB + n2) * kPitch + kPPL * g);
-    u[0][n2] = make_float2(q.x, q.y);
-    u[1][n2] = make_float2(q.z, q.w);
-  }
+  for (int n2 = 0; n2 < kB; ++n2) ld_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, u[0][n2], u[1][n2]);
 #pragma unroll
   for (int p = 0; p < kPPL; ++p) Dft<kB>::run(u[p]);
 }
 
 template <int KM>
 __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) {
-  __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
+  // fp16 staging (the output is bf16): 24.5 KB -> 6 workgroups per CU
+  __shared__ __attribute__((aligned(16))) h2_t lds[kL * kPitch];
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
-  const uint16_t* xr = a.x + static_cast<int64_t>(o) * kL * C + c0;
+  // workgroup-uniform bases + 32-bit lane offsets (SGPR base + VGPR offset addressing)
+  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
   const float2* st = a.stats + static_cast<int64_t>(o) * kL;
+  const int lo = n2 * C + kCh * g;
   // ---- pass 0: n = n2 + 15 n1 straight from global, LayerNorm on load
   uint2 raw[kA];
   float2 sv[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
-    const int n = n2 + kB * n1;
-    raw[n1] = *reinterpret_cast<const uint2*>(xr + static_cast<int64_t>(n) * C);
-    sv[n1] = st[n];
+    raw[n1] = *reinterpret_cast<const uint2*>(xb + lo + kB * n1 * C);
+    sv[n1] = st[n2 + kB * n1];
   }
   ChanParams cp;
   load_params(a, c0, cp);
@@ -152,14 +174,12 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
   __syncthreads();
   if (k1 < kA) {
 #pragma unroll
-    for (int k2 = 0; k2 < kB; ++k2)
-      *reinterpret_cast<float4*>(lds + (k1 + kA * k2) * kPitch + kPPL * g) =
-          make_float4(u[0][k2].x, u[0][k2].y, u[1][k2].x, u[1][k2].y);
+    for (int k2 = 0; k2 < kB; ++k2) st_pair(lds, (k1 + kA * k2) * kPitch + kPPL * g, u[0][k2], u[1][k2]);
   }
   __syncthreads();
   // ---- separate the packed pairs: X_a[k] = (Z[k] + conj Z[L-k]) / 2, X_b[k] = (Z[k] - conj Z[L-k]) / 2i
   const float hs = 0.5f * a.scale;
-  uint16_t* orow = a.out + static_cast<int64_t>(o) * KM * C * 2;
+  uint16_t* ob = a.out + (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
   constexpr int kItems = KM * kG;
 #pragma unroll
   for (int it = 0; it < (kItems + kThreads - 1) / kThreads; ++it) {
@@ -167,10 +187,9 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
     if (item >= kItems) break;
     const int k = item / kG, gg = item % kG;
     const int km = k == 0 ? 0 : kL - k;
-    const float4 zk = *reinterpret_cast<const float4*>(lds + k * kPitch + kPPL * gg);
-    const float4 zm = *reinterpret_cast<const float4*>(lds + km * kPitch + kPPL * gg);
-    const float2 Zk[2] = {{zk.x, zk.y}, {zk.z, zk.w}};
-    const float2 Zm[2] = {{zm.x, zm.y}, {zm.z, zm.w}};
+    float2 Zk[2], Zm[2];
+    ld_pair(lds, k * kPitch + kPPL * gg, Zk[0], Zk[1]);
+    ld_pair(lds, km * kPitch + kPPL * gg, Zm[0], Zm[1]);
     uint32_t w[4];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
@@ -179,7 +198,7 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
       w[2 * p] = bfpack(xa.x, xa.y);
       w[2 * p + 1] = bfpack(xb.x, xb.y);
     }
-    *reinterpret_cast<uint4*>(orow + (static_cast<int64_t>(k) * C + slab * kSlab + kCh * gg) * 2) =
+    *reinterpret_cast<uint4*>(ob + (k * C + kCh * gg) * 2) =
         make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
@@ -197,14 +216,14 @@ constexpr int c2r_load_kind(int n1) {
 }
 
 template <int KM>
-__global__ void __launch_bounds__(kThreads) afno_w_c2r_ln_kernel(const WArgs a) {
+__global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
   __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
-  const uint16_t* srow = a.spec + static_cast<int64_t>(o) * KM * C * 2 + c0 * 2;
+  const uint16_t* sb = a.spec + (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
   // ---- pass 0: Hermitian assembly of the packed pair spectrum Z = X_a + i X_b, conjugated
   // (inverse transform as conj(FFT(conj Z))); only the stored modes are loaded
   uint4 raw[kA];
@@ -214,7 +233,7 @@ __global__ void __launch_bounds__(kThreads) afno_w_c2r_ln_kernel(const WArgs a) 
       const int n = n2 + kB * n1;
       const int kk = 2 * n > kL ? kL - n : n;
       const int kc = kk < KM ? kk : 0;  // clamped: unconditional load, masked below
-      raw[n1] = *reinterpret_cast<const uint4*>(srow + static_cast<int64_t>(kc) * C * 2);
+      raw[n1] = *reinterpret_cast<const uint4*>(sb + (kc * C + kCh * g) * 2);
     }
   }
   float2 v[kPPL][kA];
@@ -254,27 +273,38 @@ __global__ void __launch_bounds__(kThreads) afno_w_c2r_ln_kernel(const WArgs a) 
   __syncthreads();
   const int k1 = n2;
   if (k1 >= kA) return;
-  // residual-stream addends of this thread's outputs (latency under the pass-1 LDS reads)
-  const uint16_t* xr = a.x + static_cast<int64_t>(o) * kL * C + c0;
+  // pass-1 operands from LDS, then the residual-stream addends (their latency hides under the
+  // 15-point DFTs); sched barriers keep the compiler from hoisting the 30 addend loads above
+  // the LDS reads (register pressure -> occupancy)
+  float2 u[kPPL][kB];
+#pragma unroll
+  for (int n2i = 0; n2i < kB; ++n2i) {
+    ld_pair(lds, (k1 * kB + n2i) * kPitch + kPPL * g, u[0][n2i], u[1][n2i]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // workgroup-uniform bases + 32-bit lane offsets (SGPR base + VGPR offset addressing)
+  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
   const float2* st = a.stats + static_cast<int64_t>(o) * kL;
+  const int lo = k1 * C + kCh * g;
   uint2 xraw[kB];
   float2 sv[kB];
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
-    const int n = k1 + kA * k2;
-    xraw[k2] = *reinterpret_cast<const uint2*>(xr + static_cast<int64_t>(n) * C);
-    sv[k2] = st[n];
+    xraw[k2] = *reinterpret_cast<const uint2*>(xb + lo + kA * k2 * C);
+    sv[k2] = st[k1 + kA * k2];
   }
   ChanParams cp;
   load_params(a, c0, cp);
-  float2 u[kPPL][kB];
-  pass1(k1, g, lds, u);
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<kB>::run(u[0]);
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<kB>::run(u[1]);
+  __builtin_amdgcn_sched_barrier(0);
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
-  uint16_t* orow = a.out + static_cast<int64_t>(o) * kL * C + c0;
+  uint16_t* ob = a.out + static_cast<int64_t>(o) * kL * C + slab * kSlab;
   const float sc = a.scale;
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
-    const int n = k1 + kA * k2;
     float xp[kCh], h[kCh];
     ln4(xraw[k2], sv[k2], cp, xp, h);
     uint32_t w[kPPL];
@@ -284,7 +314,7 @@ __global__ void __launch_bounds__(kThreads) afno_w_c2r_ln_kernel(const WArgs a) 
       const float yb = -u[p][k2].y * sc + xp[2 * p + 1] + h[2 * p + 1];
       w[p] = bfpack(ya, yb);
     }
-    *reinterpret_cast<uint2*>(orow + static_cast<int64_t>(n) * C) = make_uint2(w[0], w[1]);
+    *reinterpret_cast<uint2*>(ob + lo + kA * k2 * C) = make_uint2(w[0], w[1]);
   }
 }
 

@@ -159,6 +159,65 @@ __global__ void __launch_bounds__(64 * kWaves) ln_stats_kernel(const uint16_t* _
   if (lane == 0) st[row] = make_float2(mean, rstd);
 }
 
+// Two rows per wave for rows of 96 chunks (768 channels): 192 chunks = exactly 3 per lane, all
+// loads of both rows in flight at once (the one-row-per-wave kernel leaves half the lanes
+// idle on its second chunk and waits on one row's latency per wave).
+template <bool PRE>
+__global__ void __launch_bounds__(64 * kWaves) ln_stats_768_kernel(const uint16_t* __restrict__ x,
+                                                                   const float* __restrict__ pre,
+                                                                   float2* __restrict__ st, int64_t rows, float eps) {
+  constexpr int kCPR = 96;  // chunks per row
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * 2;
+  if (row0 >= rows) return;
+  const bool two = row0 + 1 < rows;
+  float v[3][8];
+  int rsel[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int c = lane + 64 * i;  // chunk in the two-row span
+    const int r = c >= kCPR ? 1 : 0;
+    rsel[i] = r;
+    const int ch = c - r * kCPR;
+    const int64_t row = (r == 1 && !two) ? row0 : row0 + r;
+    unpack8(*reinterpret_cast<const uint4*>(x + row * (kCPR * 8) + ch * 8), v[i]);
+    if constexpr (PRE) {
+      const float4 p0 = *reinterpret_cast<const float4*>(pre + ch * 8);
+      const float4 p1 = *reinterpret_cast<const float4*>(pre + ch * 8 + 4);
+      v[i][0] += p0.x; v[i][1] += p0.y; v[i][2] += p0.z; v[i][3] += p0.w;
+      v[i][4] += p1.x; v[i][5] += p1.y; v[i][6] += p1.z; v[i][7] += p1.w;
+    }
+  }
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += v[i][k];
+    if (rsel[i]) s1 += t;
+    else s0 += t;
+  }
+  const float m0 = wave_sum(s0) * (1.f / 768.f), m1 = wave_sum(s1) * (1.f / 768.f);
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float m = rsel[i] ? m1 : m0;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = v[i][k] - m;
+      t += d * d;
+    }
+    if (rsel[i]) q1 += t;
+    else q0 += t;
+  }
+  const float r0 = rsqrtf(wave_sum(q0) * (1.f / 768.f) + eps), r1 = rsqrtf(wave_sum(q1) * (1.f / 768.f) + eps);
+  if (lane == 0) {
+    st[row0] = make_float2(m0, r0);
+    if (two) st[row0 + 1] = make_float2(m1, r1);
+  }
+}
+
 template <int NCH>
 void launch_stats_n(const LnStatsLaunch& p, hipStream_t st) {
   const dim3 grid(static_cast<uint32_t>((p.rows + kWaves - 1) / kWaves));
@@ -179,7 +238,15 @@ void launch_ln_stats(const LnStatsLaunch& p, void* stream) {
   if (p.rows > static_cast<int64_t>(0x7fffffff) * kWaves) throw std::runtime_error("amd_dft: ln_stats: too many rows");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int nch = (p.cols / 8 + 63) / 64;
-  if (nch <= 1) launch_stats_n<1>(p, st);
+  if (p.cols == 768) {
+    const dim3 grid(static_cast<uint32_t>((p.rows + 2 * kWaves - 1) / (2 * kWaves)));
+    const auto* x = static_cast<const uint16_t*>(p.x);
+    auto* o = reinterpret_cast<float2*>(p.stats);
+    if (p.pre)
+      hipLaunchKernelGGL((ln_stats_768_kernel<true>), grid, dim3(64 * kWaves), 0, st, x, p.pre, o, p.rows, p.eps);
+    else
+      hipLaunchKernelGGL((ln_stats_768_kernel<false>), grid, dim3(64 * kWaves), 0, st, x, nullptr, o, p.rows, p.eps);
+  } else if (nch <= 1) launch_stats_n<1>(p, st);
   else if (nch == 2) launch_stats_n<2>(p, st);
   else launch_stats_n<4>(p, st);
   hipError_t e = hipGetLastError();

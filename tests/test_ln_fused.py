@@ -148,3 +148,16 @@ def test_ln_fused_kernels_gpu(device, with_pre, impl, recwarn, monkeypatch):
     assert out.dtype == torch.bfloat16
     assert rel_l2(out, ref) < 1e-2
     assert not [w for w in recwarn if "no specialised LayerNorm-fused kernel" in str(w.message)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 15, 1024])
+@pytest.mark.parametrize("with_pre", [False, True])
+def test_ln_stats_768_kernel_gpu(device, rows, with_pre):
+    """Two-rows-per-wave statistics kernel (768 channels), including an odd row count."""
+    g = torch.Generator().manual_seed(rows)
+    x = (3 + 2 * torch.randn(rows, 768, generator=g)).to(torch.bfloat16)
+    pre = torch.randn(768, generator=g) if with_pre else None
+    st = ops.ln_stats(x.to(device), None if pre is None else pre.to(device), 1e-6).cpu()
+    ref = ops.ln_stats(x, pre, 1e-6)
+    torch.testing.assert_close(st, ref, rtol=2e-4, atol=2e-4)
