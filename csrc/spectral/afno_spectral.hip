@@ -43,6 +43,41 @@ __device__ __forceinline__ float2 ld_h(const h2_t* p, int i) {
   return make_float2(static_cast<float>(h[0]), static_cast<float>(h[1]));
 }
 
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+// two adjacent channels' complex values (fp16 LDS staging)
+__device__ __forceinline__ void st_h2(h2_t* p, int i, float2 a, float2 b) {
+  *reinterpret_cast<h4_t*>(p + i) = h4_t{static_cast<_Float16>(a.x), static_cast<_Float16>(a.y),
+                                        static_cast<_Float16>(b.x), static_cast<_Float16>(b.y)};
+}
+__device__ __forceinline__ void ld_h2(const h2_t* p, int i, float2& a, float2& b) {
+  const h4_t h = *reinterpret_cast<const h4_t*>(p + i);
+  a = make_float2(static_cast<float>(h[0]), static_cast<float>(h[1]));
+  b = make_float2(static_cast<float>(h[2]), static_cast<float>(h[3]));
+}
+// two adjacent channels' complex values in global memory (off in scalars)
+template <bool BF>
+__device__ __forceinline__ void ldc2(const void* p, int off, float2& a, float2& b) {
+  if constexpr (BF) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + off);
+    a = make_float2(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u));
+    b = make_float2(__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  } else {
+    const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + off);
+    a = make_float2(f.x, f.y);
+    b = make_float2(f.z, f.w);
+  }
+}
+template <bool BF>
+__device__ __forceinline__ void stc2(void* p, int off, float2 a, float2 b) {
+  if constexpr (BF) {
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p) + off) =
+        make_uint2(static_cast<uint32_t>(f2bf16(a.x)) | (static_cast<uint32_t>(f2bf16(a.y)) << 16),
+                   static_cast<uint32_t>(f2bf16(b.x)) | (static_cast<uint32_t>(f2bf16(b.y)) << 16));
+  } else {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + off) = make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
 template <bool BF>
 __device__ __forceinline__ float2 ldc(const void* p, int64_t off) {  // off in scalars
   if constexpr (BF) {
@@ -63,30 +98,38 @@ __device__ __forceinline__ void stc(void* p, int64_t off, float2 v) {
 }
 
 // Stockham pass over 96 interleaved signals in LDS (layout [n][96]) with register staging:
-// gather -> barrier -> twiddle/DFT -> scatter.  SRC_GLOBAL: pass 0 reads global memory.
-template <int R, int L, int Ns, int GOFF>
+// gather -> barrier -> twiddle/DFT -> scatter.  A work item is one butterfly of a PAIR of
+// adjacent channels (8-byte global / LDS accesses, twiddles shared by the pair).
+constexpr int kNP = kBS / 2;  // channel pairs per row
+template <int R, int L>
 struct HPass {
   static constexpr int LR = L / R;
-  static constexpr int NB = LR * kBS;
+  static constexpr int NB = LR * kNP;
   static constexpr int Q = (NB + kNT - 1) / kNT;
 };
 
-template <int R, int L, int Ns, int GOFF, int Q>
-__device__ __forceinline__ void h_twiddle_dft(float2 (&v)[Q][R], const float2* __restrict__ tw) {
-  using P = HPass<R, L, Ns, GOFF>;
+template <int R, int L, int Ns, int Q>
+__device__ __forceinline__ void h_twiddle_dft(float2 (&v0)[Q][R], float2 (&v1)[Q][R], const float2* __restrict__ tw) {
+  using P = HPass<R, L>;
   static_assert(P::Q == Q, "pass geometry");
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int b = threadIdx.x + q * kNT;
     if (P::NB % kNT == 0 || b < P::NB) {
-      const int j = b / kBS;
+      const int j = b / kNP;
       if constexpr (Ns > 1) {
         const int k = j % Ns;
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[GOFF + (r - 1) * Ns + k]);
+        for (int r = 1; r < R; ++r) {
+          const float2 w = tw[(r - 1) * Ns + k];
+          v0[q][r] = c_mul(v0[q][r], w);
+          v1[q][r] = c_mul(v1[q][r], w);
+        }
       }
-      Dft<R>::run(v[q]);
+      Dft<R>::run(v0[q]);
+      Dft<R>::run(v1[q]);
     }
+    __builtin_amdgcn_sched_barrier(0);  // one item at a time: bounds the live registers
   }
 }
 
@@ -113,16 +156,21 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
   for (int mi = 0; mi < 6; ++mi)
 #pragma unroll
     for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 bfr[6][3];
+  // B fragments stream from L2 two k-steps ahead (a full preload would need 72 VGPRs)
+  bf16x8 bq[3][3];
 #pragma unroll
-  for (int ks = 0; ks < 6; ++ks)
+  for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int nj = 0; nj < 3; ++nj) {
-      const int n = (3 * w + nj) * 16 + r16;
-      bfr[ks][nj] = *reinterpret_cast<const bf16x8*>(Bt + n * kK + ks * 32 + kq * 8);
-    }
+    for (int nj = 0; nj < 3; ++nj)
+      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + s2 * 32 + kq * 8);
 #pragma unroll
   for (int ks = 0; ks < 6; ++ks) {
+    if (ks + 2 < 6) {
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj)
+        bq[(ks + 2) % 3][nj] =
+            *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + (ks + 2) * 32 + kq * 8);
+    }
     bf16x8 afr[6];
 #pragma unroll
     for (int mi = 0; mi < 6; ++mi)
@@ -131,7 +179,7 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
     for (int mi = 0; mi < 6; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj)
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bfr[ks][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % 3][nj], acc[mi][nj], 0, 0, 0);
   }
 }
 
@@ -145,61 +193,62 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
   const int bk = blockIdx.x / a.NB;  // b * KM + kw
   const int kw = bk % a.KM;
   const int b = bk / a.KM;
-  const int64_t row_stride = static_cast<int64_t>(a.KM) * a.C * 2;  // floats between consecutive h
+  const int row_stride = a.KM * a.C * 2;  // scalars between consecutive h (host-checked: 32-bit offsets)
   const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
   const void* xin = static_cast<const char*>(a.x) + base * (BFI ? 2 : 4);
   void* yout = static_cast<char*>(a.y) + base * (BFO ? 2 : 4);
-  using P0 = HPass<R0, L, 1, 0>;
-  using P1 = HPass<R1, L, R0, 0>;
+  using P0 = HPass<R0, L>;
+  using P1 = HPass<R1, L>;
 
   // ---------------- forward FFT_H: pass 0 straight from global
   {
-    float2 v[P0::Q][R0];
+    float2 v0[P0::Q][R0], v1[P0::Q][R0];
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
       const int bc = ok ? bb : 0;
-      const int t = bc % kBS, j = bc / kBS;
+      const int tp = bc % kNP, j = bc / kNP;
 #pragma unroll
-      for (int r = 0; r < R0; ++r) v[q][r] = ldc<BFI>(xin, (j + r * P0::LR) * row_stride + 2 * t);
+      for (int r = 0; r < R0; ++r) ldc2<BFI>(xin, (j + r * P0::LR) * row_stride + 4 * tp, v0[q][r], v1[q][r]);
     }
-    h_twiddle_dft<R0, L, 1, 0, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, 1, P0::Q>(v0, v1, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_h(lds, (j * R0 + r) * kBS + t, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_h2(lds, (j * R0 + r) * kBS + 2 * tp, v0[q][r], v1[q][r]);
       }
     }
   }
   __syncthreads();
   // ---------------- pass 1: LDS -> registers -> A (bf16, [h][re 0..95 | im 96..191])
   {
-    float2 v[P1::Q][R1];
+    float2 v0[P1::Q][R1], v1[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_h(lds, (j + r * P1::LR) * kBS + t);
+        for (int r = 0; r < R1; ++r) ld_h2(lds, (j + r * P1::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, R0, 0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, R0, P1::Q>(v0, v1, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int t = bb % kBS, j = bb / kBS;  // last pass: outputs at n = j + r * R0
+        const int tp = bb % kNP, j = bb / kNP;  // last pass: outputs at n = j + r * R0
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          A[n * kAPitch + t] = f2bf16(v[q][r].x);
-          A[n * kAPitch + kBS + t] = f2bf16(v[q][r].y);
+          uint32_t* row = reinterpret_cast<uint32_t*>(A + n * kAPitch);
+          row[tp] = static_cast<uint32_t>(f2bf16(v0[q][r].x)) | (static_cast<uint32_t>(f2bf16(v1[q][r].x)) << 16);
+          row[kNP + tp] = static_cast<uint32_t>(f2bf16(v0[q][r].y)) | (static_cast<uint32_t>(f2bf16(v1[q][r].y)) << 16);
         }
       }
     }
@@ -246,7 +295,7 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
         const int m = mi * 16 + 4 * (lane >> 4) + i;
         if (m < L) {
           const float v = acc[mi][nj][i] + bias;
-          const float s = v > lam ? v - lam : (v < -lam ? v + lam : 0.f);
+          const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
           X[(m * kBS + c) * 2 + part] = static_cast<_Float16>(sgn * s);
         }
       }
@@ -254,51 +303,52 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
   __syncthreads();
   // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
   {
-    float2 v[P0::Q][R0];
+    float2 v0[P0::Q][R0], v1[P0::Q][R0];
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_h(lds, (j + r * P0::LR) * kBS + t);
+        for (int r = 0; r < R0; ++r) ld_h2(lds, (j + r * P0::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R0, L, 1, 0, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, 1, P0::Q>(v0, v1, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_h(lds, (j * R0 + r) * kBS + t, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_h2(lds, (j * R0 + r) * kBS + 2 * tp, v0[q][r], v1[q][r]);
       }
     }
   }
   __syncthreads();
   // ---------------- pass 1: LDS -> registers -> global (conj back)
   {
-    float2 v[P1::Q][R1];
+    float2 v0[P1::Q][R1], v1[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_h(lds, (j + r * P1::LR) * kBS + t);
+        for (int r = 0; r < R1; ++r) ld_h2(lds, (j + r * P1::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
       }
     }
-    h_twiddle_dft<R1, L, R0, 0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, R0, P1::Q>(v0, v1, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int t = bb % kBS, j = bb / kBS;
+        const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          stc<BFO>(yout, n * row_stride + 2 * t, make_float2(v[q][r].x, -v[q][r].y));
+          stc2<BFO>(yout, n * row_stride + 4 * tp, make_float2(v0[q][r].x, -v0[q][r].y),
+                    make_float2(v1[q][r].x, -v1[q][r].y));
         }
       }
     }
@@ -317,6 +367,8 @@ int64_t afno_spectral_lds_bytes(int H) {
 
 void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   if (!afno_spectral_supported(p.H, p.C / p.NB)) throw std::runtime_error("amd_dft: afno_spectral: unsupported shape");
+  if (static_cast<int64_t>(p.H) * p.KM * p.C * 2 >= (int64_t(1) << 31))
+    throw std::runtime_error("amd_dft: afno_spectral: per-batch spectrum exceeds 32-bit offsets");
   AfnoArgs a;
   a.x = p.x;
   a.y = p.y;
