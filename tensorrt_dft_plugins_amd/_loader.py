@@ -16,7 +16,7 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
+_LIB_PATH = os.environ.get("MI_DFT_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
 _lock = threading.Lock()
 _loaded = False
 
