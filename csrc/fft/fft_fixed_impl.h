@@ -423,6 +423,8 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
         const int32_t off = x.i0c * a.Si_out + k * a.Sn_out;
         if constexpr (PV) {
           if (x.ok0) st_c2<BFO>(x.out, off, xa, xb);
+        } else if (a.vec_out && x.ok1) {  // paired outputs adjacent (transposed rfft2 intermediate)
+          st_c2<BFO>(x.out, off, xa, xb);
         } else {
           if (x.ok0) st_c<BFO>(x.out, off, xa);
           if (x.ok1) st_c<BFO>(x.out, x.i1c * a.Si_out + k * a.Sn_out, xb);
