@@ -15,6 +15,12 @@ struct GemmLaunch {
   const float* ln_c1 = nullptr;        // [N] fp32: sum_k W'[n, k] (required with ln_stats)
   int M = 0, N = 0, K = 0;
   int act = 0;               // 0 none, 1 GELU (erf)
+  // Patch-embedding gather (x is an image [B, gC, gh*8, gw*8]; token t = (b, i, j) reads its
+  // 8x8 patch of every channel, feature order (c, py, px): one 16-byte chunk per (c, py)).
+  int gC = 0, gh = 0, gw = 0;
+  int res_rows = 0;          // > 0: residual row = token % res_rows (broadcast over the batch)
+  // Un-patchify scatter (y is an image [B, sC, sh*8, sw*8]; feature order (c, py, px)).
+  int sC = 0, sh = 0, sw = 0;
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 void launch_gemm(const GemmLaunch& p, void* stream);

@@ -81,11 +81,14 @@ __device__ __forceinline__ int region_row(int r) {
   else return (r >> 5) * 64 + 32 + (r & 31);
 }
 
-// DMA one region (2 x 1 KB per wave: 8 rows x 128 B per instruction, lane-linear in LDS)
-template <int REG>
+// DMA one region (2 x 1 KB per wave: 8 rows x 128 B per instruction, lane-linear in LDS).
+// MODE 1 (patch embedding): the token operand is gathered straight from the image -- K-tile kt
+// is channel kt and the 16-byte chunk c of a token row is patch row py = c (8 pixels), so the
+// un-patchified tensor never exists.
+template <int REG, int MODE>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
-                                             int lane) {
+                                             int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
   char* dst = stage + REG * kRegion;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -95,11 +98,12 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
     const int tr = region_row<REG>(row);
     const uint16_t* g;
     if constexpr (REG == 0 || REG == 3) {
-      g = W + static_cast<int64_t>(f0 + tr) * K;
+      g = W + static_cast<int64_t>(f0 + tr) * K + kt * kBK + chunk * 8;
+    } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
+      g = X + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
     } else {
-      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * K;
+      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * K + kt * kBK + chunk * 8;
     }
-    g += kt * kBK + chunk * 8;
     __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
   }
 }
@@ -152,7 +156,7 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN>
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
   const uint16_t* __restrict__ W = p.w;
@@ -182,13 +186,29 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   auto tgt = [](int P) { return (P >> 2) + 1 + ((P & 3) == 3 ? 1 : 0); };
   auto issued = [&](int P) { return tgt(P) < KT ? 1 : 0; };
 
+  // MODE 1: per-lane token base offsets of the gathered image rows (regions 1, 2 x 2 pieces)
+  int gb[2][2] = {{0, 0}, {0, 0}};
+  if constexpr (MODE == 1) {
+    const int hw = p.gh * p.gw, rowlen = p.gw * 8;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wave * 2 + i) * 8 + (lane >> 3);
+        const int tr = r == 0 ? region_row<1>(row) : region_row<2>(row);
+        const int t = min(t0 + tr, M - 1);
+        const int b = t / hw, rem = t - b * hw;
+        const int ii = rem / p.gw, jj = rem - ii * p.gw;
+        gb[r][i] = (b * p.gC * (p.gh * 8) + ii * 8) * rowlen + jj * 8;
+      }
+  }
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
-  stage_region<0>(W, X, K, f0, t0, M, 0, smem, wave, lane);
-  stage_region<1>(W, X, K, f0, t0, M, 0, smem, wave, lane);
-  stage_region<2>(W, X, K, f0, t0, M, 0, smem, wave, lane);
-  stage_region<3>(W, X, K, f0, t0, M, 0, smem, wave, lane);
+  stage_region<0, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<1, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<2, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<3, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
   if (KT > 1) {
-    stage_region<0>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane);
+    stage_region<0, MODE>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane, p, gb);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
   } else {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -204,7 +224,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     const int P = 4 * t;
     // ---- phase 0: quadrant (mi 0, ni 0)
     wait_regions(issued(P - 2) + issued(P - 1));
-    if (issued(P)) stage_region<1>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    if (issued(P)) stage_region<1, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     read_b<1>(b0, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -212,7 +232,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 1: (0, 1)
     wait_regions(issued(P - 1) + issued(P));
-    if (issued(P + 1)) stage_region<2>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    if (issued(P + 1)) stage_region<2, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     read_b<2>(b1, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -220,7 +240,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 2: (1, 1)
     wait_regions(issued(P) + issued(P + 1));
-    if (issued(P + 2)) stage_region<3>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane);
+    if (issued(P + 2)) stage_region<3, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     read_a<3>(a1, cur, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -228,7 +248,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
     wait_regions(issued(P + 1) + issued(P + 2));
-    if (issued(P + 3)) stage_region<0>(W, X, K, f0, t0, M, t + 2, cur, wave, lane);
+    if (issued(P + 3)) stage_region<0, MODE>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
     if (t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -275,9 +295,17 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         v[e] = a + bv[e];
         if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
       }
-      const int64_t off = static_cast<int64_t>(t) * N + f;
+      int64_t off = static_cast<int64_t>(t) * N + f;
+      if constexpr (MODE == 2) {  // un-patchify: feature f = (c, py, px), 4 consecutive px
+        const int hw = p.sh * p.sw;
+        const int b = t / hw, rem = t - b * hw;
+        const int ii = rem / p.sw, jj = rem - ii * p.sw;
+        off = (static_cast<int64_t>(b * p.sC + (f >> 6)) * (p.sh * 8) + ii * 8 + ((f >> 3) & 7)) * (p.sw * 8) +
+              jj * 8 + (f & 7);
+      }
       if constexpr (RES) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
+        const int64_t roff = (MODE == 1 && p.res_rows > 0) ? static_cast<int64_t>(t % p.res_rows) * N + f : off;
+        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + roff);
         v[0] += __uint_as_float(rr.x << 16);
         v[1] += __uint_as_float(rr.x & 0xffff0000u);
         v[2] += __uint_as_float(rr.y << 16);
@@ -288,16 +316,16 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   }
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN>
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE = 0>
 void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, RES, LN>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm attr: ") + hipGetErrorString(e));
     attr_done = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, RES, LN>), grid, dim3(kThreads), kLds, st, p);
+  hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE>), grid, dim3(kThreads), kLds, st, p);
 }
 
 template <int ACT, bool BIAS, bool RES>
@@ -326,6 +354,25 @@ void launch_gemm(const GemmLaunch& p, void* stream) {
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool bias = p.bias != nullptr;
+  if (p.gC > 0 || p.sC > 0) {  // patch-embedding gather / un-patchify scatter (no activation, no LN)
+    if (p.act != 0 || p.ln_stats) throw std::runtime_error("amd_dft: gemm: patch modes take no activation / LN");
+    if (p.gC > 0) {
+      if (p.K != p.gC * 64 || static_cast<int64_t>(p.M) % (static_cast<int64_t>(p.gh) * p.gw) != 0)
+        throw std::runtime_error("amd_dft: gemm: patch gather needs K = C*64 and M = B*h*w");
+      if (bias && p.residual) launch_one<0, true, true, false, 1>(p, st, grid);
+      else if (bias) launch_one<0, true, false, false, 1>(p, st, grid);
+      else if (p.residual) launch_one<0, false, true, false, 1>(p, st, grid);
+      else launch_one<0, false, false, false, 1>(p, st, grid);
+    } else {
+      if (p.N != p.sC * 64 || p.residual || static_cast<int64_t>(p.M) % (static_cast<int64_t>(p.sh) * p.sw) != 0)
+        throw std::runtime_error("amd_dft: gemm: un-patchify scatter needs N = C*64, M = B*h*w, no residual");
+      if (bias) launch_one<0, true, false, false, 2>(p, st, grid);
+      else launch_one<0, false, false, false, 2>(p, st, grid);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm launch: ") + hipGetErrorString(e));
+    return;
+  }
   if (p.act == 1) {
     if (bias) launch_res<1, true>(p, st, grid);
     else launch_res<1, false>(p, st, grid);

@@ -116,6 +116,103 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
   return y;
 }
 
+// ------------------------------------------------------------------ patch embedding / head
+// patch_linear: tokens = patchify(x) @ w^T + bias + pos[token % (h*w)]  ([B*h*w, N] bf16)
+// linear_unpatch: image = unpatchify(t @ w^T + bias)                     ([B, C, h*p, w*p])
+// CUDA with p == 8 and bf16: one MFMA GEMM each, the (un)patchify folded into its operand
+// gather / output scatter (csrc/nn/gemm.hip MODE 1 / 2).  The reference conv / linear +
+// permute path is the CPU implementation.
+at::Tensor patch_linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                            const c10::optional<at::Tensor>& pos, int64_t p) {
+  at::Tensor t = patchify_cpu(x, p);
+  at::Tensor y = linear_ref(t, w, bias, 0, c10::nullopt).to(at::kFloat);
+  if (pos.has_value() && pos->defined()) {
+    const int64_t hw = (x.size(2) / p) * (x.size(3) / p);
+    y = (y.reshape({-1, hw, w.size(0)}) + pos->to(at::kFloat).reshape({1, hw, w.size(0)})).reshape({-1, w.size(0)});
+  }
+  return y.to(x.scalar_type()).contiguous();
+}
+
+at::Tensor patch_linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
+                             const c10::optional<at::Tensor>& pos, int64_t p) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() == 4 && x_.size(2) % p == 0 && x_.size(3) % p == 0, "patch_linear: x must be [B, C, h*p, w*p]");
+  TORCH_CHECK(w_.dim() == 2 && w_.size(1) == x_.size(1) * p * p, "patch_linear: w must be [N, C*p*p]");
+  const int64_t B = x_.size(0), C = x_.size(1), h = x_.size(2) / p, w = x_.size(3) / p, N = w_.size(0);
+  const int64_t M = B * h * w, K = C * p * p;
+  const bool native = p == 8 && x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
+                      gemm_supported(M, N, K) && x_.numel() < (int64_t(1) << 31);
+  if (!native) return patch_linear_cpu(x_, w_, bias, pos, p);  // ATen ops on the device tensors
+  at::Tensor x = x_.contiguous(), wc = w_.contiguous();
+  at::Tensor y = at::empty({M, N}, x.options());
+  at::Tensor b, r;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->numel() == h * w * N, "patch_linear: pos must be [h*w, N]");
+    r = pos->to(at::kBFloat16).contiguous();
+  }
+  GemmLaunch g;
+  g.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  g.w = reinterpret_cast<const uint16_t*>(wc.data_ptr());
+  g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  g.residual = r.defined() ? reinterpret_cast<const uint16_t*>(r.data_ptr()) : nullptr;
+  g.res_rows = static_cast<int>(h * w);
+  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.gC = static_cast<int>(C);
+  g.gh = static_cast<int>(h);
+  g.gw = static_cast<int>(w);
+  launch_gemm(g, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor patch_linear_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>&,
+                             const c10::optional<at::Tensor>&, int64_t p) {
+  return at::empty({x.size(0) * (x.size(2) / p) * (x.size(3) / p), w.size(0)}, x.options());
+}
+
+at::Tensor linear_unpatch_cpu(const at::Tensor& t, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                              int64_t C, int64_t h, int64_t wd, int64_t p) {
+  return unpatchify_cpu(linear_ref(t, w, bias, 0, c10::nullopt), C, h, wd, p);
+}
+
+at::Tensor linear_unpatch_cuda(const at::Tensor& t_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
+                               int64_t C, int64_t h, int64_t wd, int64_t p) {
+  const c10::DeviceGuard guard(t_.device());
+  TORCH_CHECK(w_.dim() == 2 && t_.size(-1) == w_.size(1) && w_.size(0) == C * p * p,
+              "linear_unpatch: t [..., K], w [C*p*p, K] in (c, py, px) feature order");
+  const int64_t K = w_.size(1), N = w_.size(0), M = t_.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(M % (h * wd) == 0, "linear_unpatch: token count must be a multiple of h*w");
+  const bool native = p == 8 && t_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
+                      gemm_supported(M, N, K) && M * N < (int64_t(1) << 31);
+  if (!native) return linear_unpatch_cpu(t_, w_, bias, C, h, wd, p);
+  at::Tensor t = t_.contiguous(), wc = w_.contiguous();
+  const int64_t B = M / (h * wd);
+  at::Tensor y = at::empty({B, C, h * p, wd * p}, t.options());
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  GemmLaunch g;
+  g.x = reinterpret_cast<const uint16_t*>(t.data_ptr());
+  g.w = reinterpret_cast<const uint16_t*>(wc.data_ptr());
+  g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.sC = static_cast<int>(C);
+  g.sh = static_cast<int>(h);
+  g.sw = static_cast<int>(wd);
+  launch_gemm(g, c10::hip::getCurrentHIPStream(t.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear_unpatch_meta(const at::Tensor& t, const at::Tensor& w, const c10::optional<at::Tensor>&, int64_t C,
+                               int64_t h, int64_t wd, int64_t p) {
+  return at::empty({t.numel() / w.size(1) / (h * wd), C, h * p, wd * p}, t.options());
+}
+
 at::Tensor linear_meta(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>&, int64_t,
                        const c10::optional<at::Tensor>&) {
   std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
@@ -130,19 +227,27 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("patchify(Tensor x, int p) -> Tensor");
   m.def("unpatchify(Tensor t, int C, int h, int w, int p) -> Tensor");
   m.def("linear(Tensor x, Tensor w, Tensor? bias=None, int act=0, Tensor? residual=None) -> Tensor");
+  m.def("patch_linear(Tensor x, Tensor w, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
+  m.def("linear_unpatch(Tensor t, Tensor w, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("patchify", &amd_dft::patchify_cuda);
   m.impl("unpatchify", &amd_dft::unpatchify_cuda);
   m.impl("linear", &amd_dft::linear_cuda);
+  m.impl("patch_linear", &amd_dft::patch_linear_cuda);
+  m.impl("linear_unpatch", &amd_dft::linear_unpatch_cuda);
 }
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("patchify", &amd_dft::patchify_cpu);
   m.impl("unpatchify", &amd_dft::unpatchify_cpu);
   m.impl("linear", &amd_dft::linear_cpu);
+  m.impl("patch_linear", &amd_dft::patch_linear_cpu);
+  m.impl("linear_unpatch", &amd_dft::linear_unpatch_cpu);
 }
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("patchify", &amd_dft::patchify_meta);
   m.impl("unpatchify", &amd_dft::unpatchify_meta);
   m.impl("linear", &amd_dft::linear_meta);
+  m.impl("patch_linear", &amd_dft::patch_linear_meta);
+  m.impl("linear_unpatch", &amd_dft::linear_unpatch_meta);
 }

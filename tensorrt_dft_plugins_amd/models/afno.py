@@ -214,14 +214,16 @@ class AFNONet(nn.Module):
             from .._loader import load_plugins
 
             load_plugins()
-            # conv with kernel == stride is a GEMM over non-overlapping patches (vectorised
-            # patchify kernel instead of a strided permute copy)
-            xp = torch.ops.amd_dft.patchify(x, p)
+            # conv with kernel == stride is a GEMM over non-overlapping patches: one MFMA GEMM
+            # gathers the 8x8 patches straight from the image, bias + position embedding in its
+            # epilogue (no patchified copy, no separate add)
             wmat = self.patch_embed.weight.reshape(cfg.embed_dim, -1)
-            t = F.linear(xp, wmat, self.patch_embed.bias).reshape(B, cfg.h * cfg.w, cfg.embed_dim)
+            t = torch.ops.amd_dft.patch_linear(x, wmat, self.patch_embed.bias,
+                                               self.pos_embed.reshape(cfg.h * cfg.w, cfg.embed_dim), p)
+            t = t.reshape(B, cfg.h, cfg.w, cfg.embed_dim)
         else:
             t = self.patch_embed(x).flatten(2).transpose(1, 2)
-        t = (t + self.pos_embed).reshape(B, cfg.h, cfg.w, cfg.embed_dim)
+            t = (t + self.pos_embed).reshape(B, cfg.h, cfg.w, cfg.embed_dim)
         if self.backend == "amd":
             from ..ops import spectral as S
 
@@ -231,22 +233,23 @@ class AFNONet(nn.Module):
                 pending = None
                 for blk in self.blocks:
                     t, pending = S.afno_block_amd(blk, t, pending)
+                hb = None
                 if pending is not None and pending.dim() == 1:
                     # per-channel residual bias left by the LN-fused blocks: folded into the
                     # head GEMM's bias, head(t + p) = head(t) + W_head p
-                    return torch.ops.amd_dft.unpatchify(
-                        F.linear(t, self._head_weight_cpp(), self._head_bias_cpp(pending)), cfg.out_chans, cfg.h,
-                        cfg.w, p)
-                if pending is not None:
+                    hb = self._head_bias_cpp(pending)
+                elif pending is not None:
                     t = t + pending
+                # head GEMM with the un-patchify folded into its output scatter
+                return torch.ops.amd_dft.linear_unpatch(t.reshape(-1, cfg.embed_dim), self._head_weight_cpp(), hb,
+                                                        cfg.out_chans, cfg.h, cfg.w, p)
         else:
             for blk in self.blocks:
                 t = blk(t)
         if self.backend == "amd":
-            # head GEMM with its output features permuted to (c_out, p1, p2) so the un-patchify
-            # is a vectorised 16-byte remap
-            t = F.linear(t, self._head_weight_cpp())
-            return torch.ops.amd_dft.unpatchify(t, cfg.out_chans, cfg.h, cfg.w, p)
+            # head GEMM (features permuted to (c_out, p1, p2)) with the un-patchify in its scatter
+            return torch.ops.amd_dft.linear_unpatch(t.reshape(-1, cfg.embed_dim), self._head_weight_cpp(), None,
+                                                    cfg.out_chans, cfg.h, cfg.w, p)
         t = self.head(t)  # [B, h, w, out*p*p], feature order (p1, p2, c_out) as FourCastNet
         t = t.reshape(B, cfg.h, cfg.w, p, p, cfg.out_chans).permute(0, 5, 1, 3, 2, 4)
         return t.reshape(B, cfg.out_chans, cfg.h * p, cfg.w * p)
@@ -298,7 +301,7 @@ class AFNONet(nn.Module):
         key = (w.data_ptr(), w._version, pre.data_ptr(), pre._version, w.dtype)
         if getattr(self, "_hb_key", None) != key:
             with torch.no_grad():
-                self._hb = (w.float() @ pre.float()).to(w.dtype)
+                self._hb = w.float() @ pre.float()  # fp32 bias (GEMM epilogue adds in fp32)
             self._hb_key = key
         return self._hb
 
