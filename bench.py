@@ -83,6 +83,8 @@ def main(argv=None) -> int:
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--streams", type=int, default=1, help="micro-batches on concurrent HIP streams per GPU")
+    ap.add_argument("--no-gemm-table", action="store_true",
+                    help="hipBLASLt default heuristics instead of tensorrt_dft_plugins_amd/tuning/*.csv")
     a = ap.parse_args(argv)
 
     rank, world, local = init_distributed()
@@ -94,6 +96,16 @@ def main(argv=None) -> int:
         torch.cuda.set_device(dev)
     tdp.load_plugins()
     torch.manual_seed(1234 + rank)
+    gemm_table = None
+    if cuda and not a.no_gemm_table:
+        # one GPU: fastest hipBLASLt solutions; DP: no stream-K GEMMs, which stall while the
+        # all-gather's RCCL blocks hold CUs (tensorrt_dft_plugins_amd/utils/gemm_tables.py)
+        from tensorrt_dft_plugins_amd.utils.gemm_tables import table_for_world, use_gemm_table
+
+        path = table_for_world(world)
+        if use_gemm_table(path):
+            gemm_table = os.path.basename(path)
+        log(f"GEMM solution table: {gemm_table}")
 
     if a.tiny:
         cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
@@ -168,6 +180,7 @@ def main(argv=None) -> int:
                 "hipgraph": runner.cap.use_graph,
                 "output_allgather": runner.gather,
                 "streams": a.streams,
+                "gemm_table": gemm_table,
             },
             "model_tflops_per_s": round(tflops, 2),
         }

@@ -8,6 +8,7 @@ filter bias (and the block residual) fused into its store.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -17,7 +18,7 @@ from .._loader import load_plugins
 from . import dft as D
 
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
-           "afno_block_amd", "afno_block_fused", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
+           "afno_block_amd", "afno_block_fused", "set_mlp_backend", "mlp_on_hand_gemm", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
 
 
 def _ops():
@@ -162,12 +163,35 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
     yn, _ = layer_norm(x1, blk.norm2)
     m = blk.mlp
+    if mlp_on_hand_gemm():
+        # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
+        # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL
+        # collective blocks), which stall hipBLASLt's persistent stream-K grid
+        hid = ops.linear(yn.reshape(-1, C), m.fc1.weight, m.fc1.bias, 1, None)
+        x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
+        return x1, m.fc2.bias
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
     if torch.jit.is_tracing():
         x1 = torch.addmm(x1.reshape(-1, C), hid, m.fc2.weight.t()).reshape(B, H, W, C)
     else:
         x1.view(-1, C).addmm_(hid, m.fc2.weight.t())
     return x1, m.fc2.bias
+
+
+_MLP_HAND: Optional[bool] = None
+
+
+def set_mlp_backend(hand: Optional[bool]) -> None:
+    """Force the FourCastNet MLP GEMMs onto the hand MFMA kernel (True) or hipBLASLt (False);
+    None = environment / default (MI_DFT_MLP=hand|blas, default blas)."""
+    global _MLP_HAND
+    _MLP_HAND = hand
+
+
+def mlp_on_hand_gemm() -> bool:
+    if _MLP_HAND is not None:
+        return _MLP_HAND
+    return os.environ.get("MI_DFT_MLP", "blas") == "hand"
 
 
 def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
