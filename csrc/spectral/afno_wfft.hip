@@ -34,7 +34,10 @@ namespace {
 constexpr int kL = 180, kA = 12, kB = 15;  // n = kB * n1 + n2, k = k1 + kA * k2
 constexpr int kPPL = 2;                     // packed pairs per lane (4 channels)
 constexpr int kCh = 2 * kPPL;               // channels per lane
-constexpr int kG = 16;                      // lanes per row: 64 channels / workgroup
+#ifndef AFNO_W_G
+#define AFNO_W_G 16
+#endif
+constexpr int kG = AFNO_W_G;                // lanes per row (16: 64 channels / workgroup)
 constexpr int kSlab = kCh * kG;             // 64
 constexpr int kPairs = kPPL * kG;           // packed pairs per workgroup
 constexpr int kPitch = kPairs + 2;          // float2 per LDS position (+16 B: spreads the k1 stride)
