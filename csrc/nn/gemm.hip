@@ -218,38 +218,41 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   read_a<0>(a0, smem, wr, r16, kq);
   if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
 
+#ifndef GEMM_ABLATE
+#define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads
+#endif
   for (int t = 0; t < KT; ++t) {
     char* cur = smem + (t & 1) * kStage;
     char* nxt = smem + ((t + 1) & 1) * kStage;
     const int P = 4 * t;
     // ---- phase 0: quadrant (mi 0, ni 0)
     wait_regions(issued(P - 2) + issued(P - 1));
-    if (issued(P)) stage_region<1, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    read_b<1>(b0, cur, wc, r16, kq);
+    if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     mfma_quadrant<0, 0>(acc, a0, b0);
     barrier();
     // ---- phase 1: (0, 1)
     wait_regions(issued(P - 1) + issued(P));
-    if (issued(P + 1)) stage_region<2, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    read_b<2>(b1, cur, wc, r16, kq);
+    if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     mfma_quadrant<0, 1>(acc, a0, b1);
     barrier();
     // ---- phase 2: (1, 1)
     wait_regions(issued(P) + issued(P + 1));
-    if (issued(P + 2)) stage_region<3, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    read_a<3>(a1, cur, wr, r16, kq);
+    if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     mfma_quadrant<1, 1>(acc, a1, b1);
     barrier();
     // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
     wait_regions(issued(P + 1) + issued(P + 2));
-    if (issued(P + 3)) stage_region<0, MODE>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
-    if (t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
+    if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     mfma_quadrant<1, 0>(acc, a1, b0);
