@@ -16,6 +16,7 @@ namespace amd_dft {
 
 __device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 c_neg(float2 a) { return make_float2(-a.x, -a.y); }
 __device__ __forceinline__ float2 c_mul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -26,14 +27,38 @@ __device__ __forceinline__ float2 c_mul_w(float2 a, float c, float s) {
 __device__ __forceinline__ float2 c_mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // -i*a
 __device__ __forceinline__ float2 c_mul_posi(float2 a) { return make_float2(-a.y, a.x); }  //  i*a
 __device__ __forceinline__ float2 c_scale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 c_fmas(float s, float2 a, float2 acc) {  // acc + s * a
+  return make_float2(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y));
+}
+
+// Two complex signals that share every twiddle (e.g. two adjacent channels of a batched FFT),
+// held as planes: re = (re0, re1), im = (im0, im1).  Every butterfly op is then one packed
+// fp32 instruction (v_pk_add/mul/fma_f32) per plane with no re/im shuffles, and a quarter
+// turn (+-i) is a free plane swap -- half the VALU issue of two scalar float2 signals.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct cpair {
+  f2v re, im;
+};
+__device__ __forceinline__ cpair make_cpair(float2 a, float2 b) { return cpair{f2v{a.x, b.x}, f2v{a.y, b.y}}; }
+__device__ __forceinline__ float2 cpair_lo(const cpair& v) { return make_float2(v.re[0], v.im[0]); }
+__device__ __forceinline__ float2 cpair_hi(const cpair& v) { return make_float2(v.re[1], v.im[1]); }
+__device__ __forceinline__ cpair c_add(cpair a, cpair b) { return cpair{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cpair c_sub(cpair a, cpair b) { return cpair{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cpair c_neg(cpair a) { return cpair{-a.re, -a.im}; }
+__device__ __forceinline__ cpair c_mul(cpair a, float2 w) { return cpair{a.re * w.x - a.im * w.y, a.re * w.y + a.im * w.x}; }
+__device__ __forceinline__ cpair c_mul_w(cpair a, float c, float s) { return cpair{a.re * c + a.im * s, a.im * c - a.re * s}; }
+__device__ __forceinline__ cpair c_mul_negi(cpair a) { return cpair{a.im, -a.re}; }
+__device__ __forceinline__ cpair c_mul_posi(cpair a) { return cpair{-a.im, a.re}; }
+__device__ __forceinline__ cpair c_scale(cpair a, float s) { return cpair{a.re * s, a.im * s}; }
+__device__ __forceinline__ cpair c_fmas(float s, cpair a, cpair acc) { return cpair{s * a.re + acc.re, s * a.im + acc.im}; }
 
 // Multiply by w_R^m = e^{-2 pi i m / R}, exact for the quarter turns.
-template <int R>
-__device__ __forceinline__ float2 c_rot(float2 a, int m) {
+template <int R, class T>
+__device__ __forceinline__ T c_rot(T a, int m) {
   m %= R;
   if (m == 0) return a;
   if (4 * m == R) return c_mul_negi(a);
-  if (2 * m == R) return make_float2(-a.x, -a.y);
+  if (2 * m == R) return c_neg(a);
   if (4 * m == 3 * R) return c_mul_posi(a);
   return c_mul_w(a, RootTab<R>::c[m], RootTab<R>::s[m]);
 }
@@ -43,13 +68,15 @@ struct Dft;
 
 template <>
 struct Dft<1> {
-  __device__ __forceinline__ static void run(float2*) {}
+  template <class T>
+  __device__ __forceinline__ static void run(T*) {}
 };
 
 template <>
 struct Dft<2> {
-  __device__ __forceinline__ static void run(float2* v) {
-    const float2 a = v[0], b = v[1];
+  template <class T>
+  __device__ __forceinline__ static void run(T* v) {
+    const T a = v[0], b = v[1];
     v[0] = c_add(a, b);
     v[1] = c_sub(a, b);
   }
@@ -57,9 +84,10 @@ struct Dft<2> {
 
 template <>
 struct Dft<4> {
-  __device__ __forceinline__ static void run(float2* v) {
-    const float2 y0 = c_add(v[0], v[2]), y1 = c_sub(v[0], v[2]);
-    const float2 y2 = c_add(v[1], v[3]), y3 = c_mul_negi(c_sub(v[1], v[3]));
+  template <class T>
+  __device__ __forceinline__ static void run(T* v) {
+    const T y0 = c_add(v[0], v[2]), y1 = c_sub(v[0], v[2]);
+    const T y2 = c_add(v[1], v[3]), y3 = c_mul_negi(c_sub(v[1], v[3]));
     v[0] = c_add(y0, y2);
     v[2] = c_sub(y0, y2);
     v[1] = c_add(y1, y3);
@@ -69,18 +97,19 @@ struct Dft<4> {
 
 template <>
 struct Dft<8> {
-  __device__ __forceinline__ static void run(float2* v) {
+  template <class T>
+  __device__ __forceinline__ static void run(T* v) {
     constexpr float r = 0.70710678118654752f;
-    float2 e[4], o[4];
+    T e[4], o[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       e[n] = c_add(v[n], v[n + 4]);
       o[n] = c_sub(v[n], v[n + 4]);
     }
     // o[n] *= w8^n
-    o[1] = make_float2((o[1].x + o[1].y) * r, (o[1].y - o[1].x) * r);
+    o[1] = c_scale(c_add(o[1], c_mul_negi(o[1])), r);  // ((x + y) r, (y - x) r)
     o[2] = c_mul_negi(o[2]);
-    o[3] = make_float2((o[3].y - o[3].x) * r, -(o[3].x + o[3].y) * r);
+    o[3] = c_scale(c_sub(c_mul_negi(o[3]), o[3]), r);  // ((y - x) r, -(x + y) r)
     Dft<4>::run(e);
     Dft<4>::run(o);
 #pragma unroll
@@ -94,33 +123,32 @@ struct Dft<8> {
 // Odd prime radix: pairwise symmetric form (R-1)^2/2 real FMAs per component.
 template <int R>
 struct DftOdd {
-  __device__ __forceinline__ static void run(float2* v) {
+  template <class T>
+  __device__ __forceinline__ static void run(T* v) {
     constexpr int H = (R - 1) / 2;
-    float2 t[H], d[H];
+    T t[H], d[H];
 #pragma unroll
     for (int m = 1; m <= H; ++m) {
       t[m - 1] = c_add(v[m], v[R - m]);
       d[m - 1] = c_sub(v[m], v[R - m]);
     }
-    const float2 x0 = v[0];
-    float2 sum = x0;
+    const T x0 = v[0];
+    T sum = x0;
 #pragma unroll
     for (int m = 0; m < H; ++m) sum = c_add(sum, t[m]);
 #pragma unroll
     for (int q = 1; q <= H; ++q) {
-      float2 re = x0, im = make_float2(0.f, 0.f);
+      T re = c_fmas(RootTab<R>::c[q % R], t[0], x0);
+      T im = c_scale(d[0], RootTab<R>::s[q % R]);
 #pragma unroll
-      for (int m = 1; m <= H; ++m) {
+      for (int m = 2; m <= H; ++m) {
         const int idx = (m * q) % R;
-        const float c = RootTab<R>::c[idx], s = RootTab<R>::s[idx];
-        re.x = fmaf(c, t[m - 1].x, re.x);
-        re.y = fmaf(c, t[m - 1].y, re.y);
-        im.x = fmaf(s, d[m - 1].x, im.x);
-        im.y = fmaf(s, d[m - 1].y, im.y);
+        re = c_fmas(RootTab<R>::c[idx], t[m - 1], re);
+        im = c_fmas(RootTab<R>::s[idx], d[m - 1], im);
       }
       // X_q = re - i*im ; X_{R-q} = re + i*im
-      v[q] = make_float2(re.x + im.y, re.y - im.x);
-      v[R - q] = make_float2(re.x - im.y, re.y + im.x);
+      v[q] = c_add(re, c_mul_negi(im));
+      v[R - q] = c_sub(re, c_mul_negi(im));
     }
     v[0] = sum;
   }
@@ -135,21 +163,22 @@ template <> struct Dft<13> : DftOdd<13> {};
 // Composite A*B: n = B*n1 + n2, k = k1 + A*k2.
 template <int A, int B>
 struct DftComp {
-  __device__ __forceinline__ static void run(float2* v) {
+  template <class T>
+  __device__ __forceinline__ static void run(T* v) {
     constexpr int R = A * B;
-    float2 y[R];
+    T y[R];
 #pragma unroll
     for (int n2 = 0; n2 < B; ++n2) {
-      float2 s[A];
+      T s[A];
 #pragma unroll
       for (int n1 = 0; n1 < A; ++n1) s[n1] = v[B * n1 + n2];
       Dft<A>::run(s);
 #pragma unroll
-      for (int k1 = 0; k1 < A; ++k1) y[k1 * B + n2] = c_rot<R>(s[k1], n2 * k1);
+      for (int k1 = 0; k1 < A; ++k1) y[k1 * B + n2] = c_rot<R, T>(s[k1], n2 * k1);
     }
 #pragma unroll
     for (int k1 = 0; k1 < A; ++k1) {
-      float2 s[B];
+      T s[B];
 #pragma unroll
       for (int n2 = 0; n2 < B; ++n2) s[n2] = y[k1 * B + n2];
       Dft<B>::run(s);

@@ -29,7 +29,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kNT = 256;      // threads
 constexpr int kBS = 96;       // channels per AFNO block
 constexpr int kK = 2 * kBS;   // real-block GEMM K = N = 192
-constexpr int kAPitch = kK + 8;  // bf16 elements per A row (+16 B pad: ds_read_b128 spread)
+constexpr int kAPitch = kK + 8;
+#ifndef AFNO_BPF
+#define AFNO_BPF 2  // k-steps of B-fragment prefetch in the block-MLP GEMMs
+#endif
+#ifndef AFNO_OCC
+#define AFNO_OCC 3  // workgroups (waves) per SIMD the register budget is sized for
+#endif  // bf16 elements per A row (+16 B pad: ds_read_b128 spread)
 
 __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 
@@ -45,14 +51,13 @@ __device__ __forceinline__ float2 ld_h(const h2_t* p, int i) {
 
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 // two adjacent channels' complex values (fp16 LDS staging)
-__device__ __forceinline__ void st_h2(h2_t* p, int i, float2 a, float2 b) {
-  *reinterpret_cast<h4_t*>(p + i) = h4_t{static_cast<_Float16>(a.x), static_cast<_Float16>(a.y),
-                                        static_cast<_Float16>(b.x), static_cast<_Float16>(b.y)};
+__device__ __forceinline__ void st_hp(h2_t* p, int i, const cpair& v) {
+  *reinterpret_cast<h4_t*>(p + i) = h4_t{static_cast<_Float16>(v.re[0]), static_cast<_Float16>(v.im[0]),
+                                        static_cast<_Float16>(v.re[1]), static_cast<_Float16>(v.im[1])};
 }
-__device__ __forceinline__ void ld_h2(const h2_t* p, int i, float2& a, float2& b) {
+__device__ __forceinline__ cpair ld_hp(const h2_t* p, int i) {
   const h4_t h = *reinterpret_cast<const h4_t*>(p + i);
-  a = make_float2(static_cast<float>(h[0]), static_cast<float>(h[1]));
-  b = make_float2(static_cast<float>(h[2]), static_cast<float>(h[3]));
+  return cpair{f2v{static_cast<float>(h[0]), static_cast<float>(h[2])}, f2v{static_cast<float>(h[1]), static_cast<float>(h[3])}};
 }
 // two adjacent channels' complex values in global memory (off in scalars)
 template <bool BF>
@@ -99,7 +104,8 @@ __device__ __forceinline__ void stc(void* p, int64_t off, float2 v) {
 
 // Stockham pass over 96 interleaved signals in LDS (layout [n][96]) with register staging:
 // gather -> barrier -> twiddle/DFT -> scatter.  A work item is one butterfly of a PAIR of
-// adjacent channels (8-byte global / LDS accesses, twiddles shared by the pair).
+// adjacent channels (8-byte global / LDS accesses, twiddles shared by the pair), held as a
+// cpair (radix.h) so every butterfly op is one packed fp32 instruction for both channels.
 constexpr int kNP = kBS / 2;  // channel pairs per row
 template <int R, int L>
 struct HPass {
@@ -109,7 +115,7 @@ struct HPass {
 };
 
 template <int R, int L, int Ns, int Q>
-__device__ __forceinline__ void h_twiddle_dft(float2 (&v0)[Q][R], float2 (&v1)[Q][R], const float2* __restrict__ tw) {
+__device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
   using P = HPass<R, L>;
   static_assert(P::Q == Q, "pass geometry");
 #pragma unroll
@@ -121,13 +127,10 @@ __device__ __forceinline__ void h_twiddle_dft(float2 (&v0)[Q][R], float2 (&v1)[Q
         const int k = j % Ns;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          const float2 w = tw[(r - 1) * Ns + k];
-          v0[q][r] = c_mul(v0[q][r], w);
-          v1[q][r] = c_mul(v1[q][r], w);
+          v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
         }
       }
-      Dft<R>::run(v0[q]);
-      Dft<R>::run(v1[q]);
+      Dft<R>::run(v[q]);
     }
     __builtin_amdgcn_sched_barrier(0);  // one item at a time: bounds the live registers
   }
@@ -156,20 +159,21 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
   for (int mi = 0; mi < 6; ++mi)
 #pragma unroll
     for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B fragments stream from L2 two k-steps ahead (a full preload would need 72 VGPRs)
-  bf16x8 bq[3][3];
+  // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 72 VGPRs)
+  constexpr int D = AFNO_BPF, NQ = AFNO_BPF + 1;
+  bf16x8 bq[NQ][3];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
+  for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
     for (int nj = 0; nj < 3; ++nj)
       bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + s2 * 32 + kq * 8);
 #pragma unroll
   for (int ks = 0; ks < 6; ++ks) {
-    if (ks + 2 < 6) {
+    if (ks + D < 6) {
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj)
-        bq[(ks + 2) % 3][nj] =
-            *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + (ks + 2) * 32 + kq * 8);
+        bq[(ks + D) % NQ][nj] =
+            *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + (ks + D) * 32 + kq * 8);
     }
     bf16x8 afr[6];
 #pragma unroll
@@ -179,12 +183,12 @@ __device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, cons
     for (int mi = 0; mi < 6; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj)
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % 3][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
   }
 }
 
 template <int L, int R0, int R1, bool BFI, bool BFO>
-__global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a) {
+__global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const AfnoArgs a) {
   static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
   extern __shared__ __attribute__((aligned(16))) h2_t lds[];  // [L][96] complex fp16 (34.5 KB at L=90)
   uint16_t* A = reinterpret_cast<uint16_t*>(lds);             // aliases lds: [96][kAPitch] bf16 (38.4 KB)
@@ -202,7 +206,7 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
 
   // ---------------- forward FFT_H: pass 0 straight from global
   {
-    float2 v0[P0::Q][R0], v1[P0::Q][R0];
+    cpair v[P0::Q][R0];
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -210,34 +214,38 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
       const int bc = ok ? bb : 0;
       const int tp = bc % kNP, j = bc / kNP;
 #pragma unroll
-      for (int r = 0; r < R0; ++r) ldc2<BFI>(xin, (j + r * P0::LR) * row_stride + 4 * tp, v0[q][r], v1[q][r]);
+      for (int r = 0; r < R0; ++r) {
+        float2 c0, c1;
+        ldc2<BFI>(xin, (j + r * P0::LR) * row_stride + 4 * tp, c0, c1);
+        v[q][r] = make_cpair(c0, c1);
+      }
     }
-    h_twiddle_dft<R0, L, 1, P0::Q>(v0, v1, a.tw);
+    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_h2(lds, (j * R0 + r) * kBS + 2 * tp, v0[q][r], v1[q][r]);
+        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
       }
     }
   }
   __syncthreads();
   // ---------------- pass 1: LDS -> registers -> A (bf16, [h][re 0..95 | im 96..191])
   {
-    float2 v0[P1::Q][R1], v1[P1::Q][R1];
+    cpair v[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) ld_h2(lds, (j + r * P1::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * kBS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, R0, P1::Q>(v0, v1, a.tw);
+    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -247,8 +255,8 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
           uint32_t* row = reinterpret_cast<uint32_t*>(A + n * kAPitch);
-          row[tp] = static_cast<uint32_t>(f2bf16(v0[q][r].x)) | (static_cast<uint32_t>(f2bf16(v1[q][r].x)) << 16);
-          row[kNP + tp] = static_cast<uint32_t>(f2bf16(v0[q][r].y)) | (static_cast<uint32_t>(f2bf16(v1[q][r].y)) << 16);
+          row[tp] = static_cast<uint32_t>(f2bf16(v[q][r].re[0])) | (static_cast<uint32_t>(f2bf16(v[q][r].re[1])) << 16);
+          row[kNP + tp] = static_cast<uint32_t>(f2bf16(v[q][r].im[0])) | (static_cast<uint32_t>(f2bf16(v[q][r].im[1])) << 16);
         }
       }
     }
@@ -303,42 +311,42 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
   __syncthreads();
   // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
   {
-    float2 v0[P0::Q][R0], v1[P0::Q][R0];
+    cpair v[P0::Q][R0];
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) ld_h2(lds, (j + r * P0::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_hp(lds, (j + r * P0::LR) * kBS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R0, L, 1, P0::Q>(v0, v1, a.tw);
+    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_h2(lds, (j * R0 + r) * kBS + 2 * tp, v0[q][r], v1[q][r]);
+        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
       }
     }
   }
   __syncthreads();
   // ---------------- pass 1: LDS -> registers -> global (conj back)
   {
-    float2 v0[P1::Q][R1], v1[P1::Q][R1];
+    cpair v[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int tp = bb % kNP, j = bb / kNP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) ld_h2(lds, (j + r * P1::LR) * kBS + 2 * tp, v0[q][r], v1[q][r]);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * kBS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, R0, P1::Q>(v0, v1, a.tw);
+    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -347,8 +355,8 @@ __global__ void __launch_bounds__(kNT, 3) afno_spectral_kernel(const AfnoArgs a)
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          stc2<BFO>(yout, n * row_stride + 4 * tp, make_float2(v0[q][r].x, -v0[q][r].y),
-                    make_float2(v1[q][r].x, -v1[q][r].y));
+          stc2<BFO>(yout, n * row_stride + 4 * tp, make_float2(v[q][r].re[0], -v[q][r].im[0]),
+                    make_float2(v[q][r].re[1], -v[q][r].im[1]));
         }
       }
     }

@@ -117,25 +117,25 @@ __device__ __forceinline__ void ld_pair(const h2_t* l, int i, float2& a, float2&
 
 // pass 0 epilogue: 12-point DFTs, twiddle W_180^{n2 k1}, store s[k1] at LDS position k1 * 15 + n2
 template <class T>
-__device__ __forceinline__ void pass0_store(float2 (&v)[kPPL][kA], int n2, int g, T* lds) {
-#pragma unroll
-  for (int p = 0; p < kPPL; ++p) Dft<kA>::run(v[p]);
+__device__ __forceinline__ void pass0_store(cpair (&v)[kA], int n2, int g, T* lds) {
+  Dft<kA>::run(v);
 #pragma unroll
   for (int k1 = 0; k1 < kA; ++k1) {
-    const float2 w = kW180[n2 * k1];  // n2 * k1 <= 154
-    const float2 t0 = k1 == 0 ? v[0][0] : c_mul(v[0][k1], w);
-    const float2 t1 = k1 == 0 ? v[1][0] : c_mul(v[1][k1], w);
-    st_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, t0, t1);
+    const cpair t = k1 == 0 ? v[0] : c_mul(v[k1], kW180[n2 * k1]);  // n2 * k1 <= 154
+    st_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, cpair_lo(t), cpair_hi(t));
   }
 }
 
 // pass 1: 15-point DFTs of row k1; result u[p][k2] = X[k1 + 12 k2]
 template <class T>
-__device__ __forceinline__ void pass1(int k1, int g, const T* lds, float2 (&u)[kPPL][kB]) {
+__device__ __forceinline__ void pass1(int k1, int g, const T* lds, cpair (&u)[kB]) {
 #pragma unroll
-  for (int n2 = 0; n2 < kB; ++n2) ld_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, u[0][n2], u[1][n2]);
-#pragma unroll
-  for (int p = 0; p < kPPL; ++p) Dft<kB>::run(u[p]);
+  for (int n2 = 0; n2 < kB; ++n2) {
+    float2 a, b;
+    ld_pair(lds, (k1 * kB + n2) * kPitch + kPPL * g, a, b);
+    u[n2] = make_cpair(a, b);
+  }
+  Dft<kB>::run(u);
 }
 
 template <int KM>
@@ -160,24 +160,23 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
   }
   ChanParams cp;
   load_params(a, c0, cp);
-  float2 v[kPPL][kA];
+  cpair v[kA];  // the lane's two packed channel pairs (h0 + i h1, h2 + i h3) as one cpair
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
     float xp[kCh], h[kCh];
     ln4(raw[n1], sv[n1], cp, xp, h);
-#pragma unroll
-    for (int p = 0; p < kPPL; ++p) v[p][n1] = make_float2(h[2 * p], h[2 * p + 1]);
+    v[n1] = cpair{f2v{h[0], h[2]}, f2v{h[1], h[3]}};
   }
   pass0_store(v, n2, g, lds);
   __syncthreads();
   // ---- pass 1 (threads k1 < 12), result back to LDS in natural order k = k1 + 12 k2
-  float2 u[kPPL][kB];
+  cpair u[kB];
   const int k1 = n2;
   if (k1 < kA) pass1(k1, g, lds, u);
   __syncthreads();
   if (k1 < kA) {
 #pragma unroll
-    for (int k2 = 0; k2 < kB; ++k2) st_pair(lds, (k1 + kA * k2) * kPitch + kPPL * g, u[0][k2], u[1][k2]);
+    for (int k2 = 0; k2 < kB; ++k2) st_pair(lds, (k1 + kA * k2) * kPitch + kPPL * g, cpair_lo(u[k2]), cpair_hi(u[k2]));
   }
   __syncthreads();
   // ---- separate the packed pairs: X_a[k] = (Z[k] + conj Z[L-k]) / 2, X_b[k] = (Z[k] - conj Z[L-k]) / 2i
@@ -239,13 +238,12 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
       raw[n1] = *reinterpret_cast<const uint4*>(sb + (kc * C + kCh * g) * 2);
     }
   }
-  float2 v[kPPL][kA];
+  cpair v[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
     const int kind = c2r_load_kind<KM>(n1);
     if (kind == 0) {
-#pragma unroll
-      for (int p = 0; p < kPPL; ++p) v[p][n1] = make_float2(0.f, 0.f);
+      v[n1] = cpair{f2v{0.f, 0.f}, f2v{0.f, 0.f}};
       continue;
     }
     const int n = n2 + kB * n1;
@@ -255,6 +253,7 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     float f[8];
     unpack4(make_uint2(raw[n1].x, raw[n1].y), *reinterpret_cast<float(*)[4]>(f));
     unpack4(make_uint2(raw[n1].z, raw[n1].w), *reinterpret_cast<float(*)[4]>(f + 4));
+    float2 zp[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
       // channel pair (c0 + 2p, c0 + 2p + 1): A = X_a[kk], B = X_b[kk] (complex)
@@ -269,8 +268,9 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
         B.y = -B.y;
       }
       const float2 z = make_float2(A.x - B.y, -(A.y + B.x));  // conj(A + iB)
-      v[p][n1] = ok ? z : make_float2(0.f, 0.f);
+      zp[p] = ok ? z : make_float2(0.f, 0.f);
     }
+    v[n1] = make_cpair(zp[0], zp[1]);
   }
   pass0_store(v, n2, g, lds);
   __syncthreads();
@@ -279,10 +279,12 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
   // pass-1 operands from LDS, then the residual-stream addends (their latency hides under the
   // 15-point DFTs); sched barriers keep the compiler from hoisting the 30 addend loads above
   // the LDS reads (register pressure -> occupancy)
-  float2 u[kPPL][kB];
+  cpair u[kB];
 #pragma unroll
   for (int n2i = 0; n2i < kB; ++n2i) {
-    ld_pair(lds, (k1 * kB + n2i) * kPitch + kPPL * g, u[0][n2i], u[1][n2i]);
+    float2 pa, pb;
+    ld_pair(lds, (k1 * kB + n2i) * kPitch + kPPL * g, pa, pb);
+    u[n2i] = make_cpair(pa, pb);
   }
   __builtin_amdgcn_sched_barrier(0);
   // workgroup-uniform bases + 32-bit lane offsets (SGPR base + VGPR offset addressing)
@@ -299,9 +301,7 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
   ChanParams cp;
   load_params(a, c0, cp);
   __builtin_amdgcn_sched_barrier(0);
-  Dft<kB>::run(u[0]);
-  __builtin_amdgcn_sched_barrier(0);
-  Dft<kB>::run(u[1]);
+  Dft<kB>::run(u);
   __builtin_amdgcn_sched_barrier(0);
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
   uint16_t* ob = a.out + static_cast<int64_t>(o) * kL * C + slab * kSlab;
@@ -313,8 +313,8 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     uint32_t w[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
-      const float ya = u[p][k2].x * sc + xp[2 * p] + h[2 * p];
-      const float yb = -u[p][k2].y * sc + xp[2 * p + 1] + h[2 * p + 1];
+      const float ya = u[k2].re[p] * sc + xp[2 * p] + h[2 * p];
+      const float yb = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
       w[p] = bfpack(ya, yb);
     }
     *reinterpret_cast<uint2*>(ob + lo + kA * k2 * C) = make_uint2(w[0], w[1]);
