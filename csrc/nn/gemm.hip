@@ -29,6 +29,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "../fft/dev_check.h"
 #include "gemm.h"
 
 namespace amd_dft {
@@ -172,6 +173,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
   const int f0 = ft * kBF, t0 = tt * kBT;
   const int KT = K / kBK;
+  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && KT * kBK == K && KT > 0, "gemm_bf16_kernel");
   const int r16 = lane & 15, kq = lane >> 4;
 
   f32x4 acc[8][4];

@@ -30,6 +30,7 @@
 #include <string>
 #include <unordered_map>
 
+#include "trace.h"
 #include "../fft/fft_fixed.h"
 #include "../fft/fft_plan.h"
 #include "../spectral/dft_gemm.h"
@@ -961,25 +962,25 @@ TORCH_LIBRARY(amd_dft, m) {
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
-  m.impl("r2c", &amd_dft::r2c_cuda);
-  m.impl("c2r", &amd_dft::c2r_cuda);
-  m.impl("c2c", &amd_dft::c2c_cuda);
-  m.impl("c2r_add", &amd_dft::c2r_add_cuda);
-  m.impl("c2c_axis", &amd_dft::c2c_axis_cuda);
-  m.impl("dftw_r2c", &amd_dft::dftw_r2c_cuda);
-  m.impl("r2c_ln", &amd_dft::r2c_ln_cuda);
-  m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_cuda);
+  m.impl("r2c", AMD_DFT_TRACED("amd_dft::r2c", amd_dft::r2c_cuda));
+  m.impl("c2r", AMD_DFT_TRACED("amd_dft::c2r", amd_dft::c2r_cuda));
+  m.impl("c2c", AMD_DFT_TRACED("amd_dft::c2c", amd_dft::c2c_cuda));
+  m.impl("c2r_add", AMD_DFT_TRACED("amd_dft::c2r_add", amd_dft::c2r_add_cuda));
+  m.impl("c2c_axis", AMD_DFT_TRACED("amd_dft::c2c_axis", amd_dft::c2c_axis_cuda));
+  m.impl("dftw_r2c", AMD_DFT_TRACED("amd_dft::dftw_r2c", amd_dft::dftw_r2c_cuda));
+  m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cuda));
+  m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cuda));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
-  m.impl("r2c", &amd_dft::r2c_cpu);
-  m.impl("c2r", &amd_dft::c2r_cpu);
-  m.impl("c2c", &amd_dft::c2c_cpu);
-  m.impl("c2r_add", &amd_dft::c2r_add_cpu);
-  m.impl("c2c_axis", &amd_dft::c2c_axis_cpu);
-  m.impl("dftw_r2c", &amd_dft::dftw_r2c_cpu);
-  m.impl("r2c_ln", &amd_dft::r2c_ln_cpu);
-  m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_cpu);
+  m.impl("r2c", AMD_DFT_TRACED("amd_dft::r2c", amd_dft::r2c_cpu));
+  m.impl("c2r", AMD_DFT_TRACED("amd_dft::c2r", amd_dft::c2r_cpu));
+  m.impl("c2c", AMD_DFT_TRACED("amd_dft::c2c", amd_dft::c2c_cpu));
+  m.impl("c2r_add", AMD_DFT_TRACED("amd_dft::c2r_add", amd_dft::c2r_add_cpu));
+  m.impl("c2c_axis", AMD_DFT_TRACED("amd_dft::c2c_axis", amd_dft::c2c_axis_cpu));
+  m.impl("dftw_r2c", AMD_DFT_TRACED("amd_dft::dftw_r2c", amd_dft::dftw_r2c_cpu));
+  m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cpu));
+  m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cpu));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 
+#include "trace.h"
 #include "../nn/gemm.h"
 
 namespace amd_dft {
@@ -231,18 +232,18 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("linear_unpatch(Tensor t, Tensor w, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
-  m.impl("patchify", &amd_dft::patchify_cuda);
-  m.impl("unpatchify", &amd_dft::unpatchify_cuda);
-  m.impl("linear", &amd_dft::linear_cuda);
-  m.impl("patch_linear", &amd_dft::patch_linear_cuda);
-  m.impl("linear_unpatch", &amd_dft::linear_unpatch_cuda);
+  m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cuda));
+  m.impl("unpatchify", AMD_DFT_TRACED("amd_dft::unpatchify", amd_dft::unpatchify_cuda));
+  m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cuda));
+  m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cuda));
+  m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cuda));
 }
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
-  m.impl("patchify", &amd_dft::patchify_cpu);
-  m.impl("unpatchify", &amd_dft::unpatchify_cpu);
-  m.impl("linear", &amd_dft::linear_cpu);
-  m.impl("patch_linear", &amd_dft::patch_linear_cpu);
-  m.impl("linear_unpatch", &amd_dft::linear_unpatch_cpu);
+  m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cpu));
+  m.impl("unpatchify", AMD_DFT_TRACED("amd_dft::unpatchify", amd_dft::unpatchify_cpu));
+  m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cpu));
+  m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cpu));
+  m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cpu));
 }
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("patchify", &amd_dft::patchify_meta);

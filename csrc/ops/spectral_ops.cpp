@@ -7,6 +7,7 @@
 #include <ATen/core/dispatch/Dispatcher.h>
 #include <torch/library.h>
 
+#include "trace.h"
 #include "../spectral/dft_gemm.h"
 #include "../spectral/spectral.h"
 #include "checks.h"
@@ -367,21 +368,21 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
-  m.impl("afno_spectral", &amd_dft::afno_spectral_cuda);
-  m.impl("layer_norm", &amd_dft::layer_norm_cuda);
-  m.impl("ln_stats", &amd_dft::ln_stats_cuda);
-  m.impl("fno_mix", &amd_dft::fno_mix_cuda);
-  m.impl("fno_pointwise", &amd_dft::fno_pointwise_cuda);
-  m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cuda);
+  m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cuda));
+  m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cuda));
+  m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cuda));
+  m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cuda));
+  m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cuda));
+  m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cuda));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
-  m.impl("afno_spectral", &amd_dft::afno_spectral_cpu);
-  m.impl("layer_norm", &amd_dft::layer_norm_cpu);
-  m.impl("ln_stats", &amd_dft::ln_stats_cpu);
-  m.impl("fno_mix", &amd_dft::fno_mix_cpu);
-  m.impl("fno_pointwise", &amd_dft::fno_pointwise_cpu);
-  m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_cpu);
+  m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cpu));
+  m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cpu));
+  m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cpu));
+  m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cpu));
+  m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cpu));
+  m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cpu));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {

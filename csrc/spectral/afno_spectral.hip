@@ -17,6 +17,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "../fft/dev_check.h"
 #include "../fft/radix.h"
 #include "spectral.h"
 
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
   const int bk = blockIdx.x / a.NB;  // b * KM + kw
   const int kw = bk % a.KM;
   const int b = bk / a.KM;
+  AMD_DFT_DEV_CHECK((blk + 1) * kBS <= a.C && kw < a.KM && L == a.H, "afno_spectral_kernel");
   const int row_stride = a.KM * a.C * 2;  // scalars between consecutive h (host-checked: 32-bit offsets)
   const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
   const void* xin = static_cast<const char*>(a.x) + base * (BFI ? 2 : 4);

@@ -24,6 +24,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "../fft/dev_check.h"
 #include "../fft/radix.h"
 #include "spectral.h"
 #include "w180_table.h"
@@ -143,6 +144,7 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
   // fp16 staging (the output is bf16): 24.5 KB -> 6 workgroups per CU
   __shared__ __attribute__((aligned(16))) h2_t lds[kL * kPitch];
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
+  AMD_DFT_DEV_CHECK((slab + 1) * kSlab <= a.C, "afno_w_kernel");
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
@@ -222,6 +224,7 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
   __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
+  AMD_DFT_DEV_CHECK((slab + 1) * kSlab <= a.C, "afno_w_kernel");
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;

@@ -84,6 +84,9 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
         # afno 561->537 us, rfft2 18.8->17.9 us, AFNO R2C-W 387->320 us).
         cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize"]
         cmd += _file_flags(src) + os.environ.get("MI_DFT_HIPCC_EXTRA", "").split()
+        if os.environ.get("MI_DFT_DEVICE_CHECKS", "0") not in ("", "0"):
+            # debug build: device-side bounds checks (csrc/fft/dev_check.h); rebuild with --force
+            cmd += ["-DAMD_DFT_DEVICE_CHECKS=1"]
     else:
         # host-only C++ that includes HIP runtime headers (torch's c10/hip)
         rocm = os.environ.get("ROCM_PATH", "/opt/rocm")

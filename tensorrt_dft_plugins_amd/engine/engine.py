@@ -24,6 +24,9 @@ from .._loader import load_plugins
 from ..onnx import exporter as onnx_export
 from ..onnx import proto as P
 from ..onnx.runner import OnnxGraph
+from ..utils.trace import get_logger, trace_range
+
+_log = get_logger("engine")
 
 ENGINE_MAGIC = b"AMDDFTENG\x00"
 ENGINE_FORMAT_VERSION = 1
@@ -101,8 +104,12 @@ class Engine:
         self.static_outputs = self._run_eager()
         if self.use_graph:
             self._capture(warmup)
+        built_for = header.arch if header is not None else ""
         self.header = header or EngineHeader()
         self.header.arch = _device_arch(self.device)
+        if built_for and built_for != self.header.arch:
+            # plans and graphs are rebuilt on load, so this is informational, not an error
+            _log.warning("engine was built for %s, running on %s", built_for, self.header.arch)
         self.header.use_graph = self.use_graph
         self.header.bindings = (
             [Binding(n, s, _dtype_name(t.dtype), True)
@@ -165,7 +172,8 @@ class Engine:
             if list(x.shape) != list(si.shape):
                 raise ValueError(f"input shape {list(x.shape)} != engine binding {list(si.shape)} (static shapes)")
             si.copy_(x, non_blocking=True)
-        self.enqueue()
+        with trace_range("engine.enqueue"):
+            self.enqueue()
         return [o.clone() for o in self.static_outputs] if copy_outputs else list(self.static_outputs)
 
     __call__ = infer
@@ -199,8 +207,10 @@ class Engine:
         return ENGINE_MAGIC + struct.pack("<I", len(h)) + h + struct.pack("<Q", len(self.onnx_bytes)) + self.onnx_bytes
 
     def save(self, path: str) -> None:
+        data = self.serialize()
         with open(path, "wb") as f:
-            f.write(self.serialize())
+            f.write(data)
+        _log.info("saved engine %s (%d bytes, arch %s)", path, len(data), self.header.arch)
 
     @classmethod
     def deserialize(cls, data: bytes, device=None, use_graph: Optional[bool] = None) -> "Engine":
@@ -217,6 +227,8 @@ class Engine:
         if header.format_version != ENGINE_FORMAT_VERSION or header.plugin_version != PLUGIN_VERSION:
             raise ValueError(f"engine format {header.format_version}/plugin {header.plugin_version} not supported")
         ins = [b for b in header.bindings if b.is_input]
+        _log.info("deserialising engine: %d inputs, built for %s, graph=%s", len(ins), header.arch or "?",
+                  header.use_graph)
         return cls(onnx_bytes, [b.shape for b in ins], [b.torch_dtype() for b in ins], device=device,
                    use_graph=header.use_graph if use_graph is None else use_graph, header=header)
 

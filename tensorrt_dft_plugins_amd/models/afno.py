@@ -27,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import dft as D
+from ..utils.trace import trace_range
 
 
 @dataclass
@@ -231,8 +232,9 @@ class AFNONet(nn.Module):
                 t = self._blocks_microbatched(t)
             else:
                 pending = None
-                for blk in self.blocks:
-                    t, pending = S.afno_block_amd(blk, t, pending)
+                for i, blk in enumerate(self.blocks):
+                    with trace_range(f"afno.block{i}"):
+                        t, pending = S.afno_block_amd(blk, t, pending)
                 hb = None
                 if pending is not None and pending.dim() == 1:
                     # per-channel residual bias left by the LN-fused blocks: folded into the

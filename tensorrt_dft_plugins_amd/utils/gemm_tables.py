@@ -23,6 +23,8 @@ from typing import Optional
 
 import torch
 
+from .trace import get_logger
+
 TABLE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
 _loaded: Optional[str] = None
 
@@ -47,6 +49,10 @@ def use_gemm_table(path: str) -> bool:
     # results are only read, never written back
     tunable.set_filename(os.path.join("/tmp", f"amd_dft_tunable_unused_{os.getpid()}.csv"))
     ok = bool(tunable.read_file(path))
+    log = get_logger("gemm_tables")
     if ok:
         _loaded = path
+        log.info("hipBLASLt solution table %s accepted", os.path.basename(path))
+    else:
+        log.warning("hipBLASLt solution table %s rejected (validator mismatch): default heuristics", path)
     return ok
