@@ -91,7 +91,8 @@ def main(argv=None) -> int:
     if world != a.gpus and world > 1:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     cuda = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if cuda else torch.device("cpu")
+    # local % count: lets a Gloo rehearsal (MI_DFT_DIST_BACKEND=gloo) put several ranks on one GPU
+    dev = torch.device("cuda", local % torch.cuda.device_count()) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(dev)
     tdp.load_plugins()

@@ -23,7 +23,8 @@ from ..engine.capture import CapturedModule
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> tuple[int, int, int]:
     """Initialise the default process group from torchrun env vars; returns (rank, world, local_rank).
 
-    backend: "nccl" (= RCCL on ROCm) when a GPU is present, else "gloo".
+    backend: "nccl" (= RCCL on ROCm) when a GPU is present, else "gloo"; ``MI_DFT_DIST_BACKEND``
+    overrides (e.g. ``gloo`` to rehearse several ranks on ONE GPU, which RCCL refuses).
     """
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -32,7 +33,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("MI_DFT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s), device_id=torch.device("cuda", local))

@@ -18,15 +18,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, device="cpu"):
     try:
-        _worker_body(rank, world, port, q)
+        _worker_body(rank, world, port, q, device)
     except BaseException as e:  # surface failures instead of a queue timeout
         q.put((rank, repr(e), None))
         raise
 
 
-def _worker_body(rank, world, port, q):
+def _worker_body(rank, world, port, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
@@ -38,28 +38,28 @@ def _worker_body(rank, world, port, q):
     init_distributed("gloo")
     torch.manual_seed(0)  # same weights on every rank
     cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
-    model = AFNONet(cfg, backend="amd").eval()
+    model = AFNONet(cfg, backend="amd").eval().to(device)
     g = torch.Generator().manual_seed(100 + rank)
-    x = torch.randn(2, cfg.in_chans, *cfg.img_size, generator=g)
-    dp = DataParallelInference(model, x, gather=True, use_graph=False)
+    x = torch.randn(2, cfg.in_chans, *cfg.img_size, generator=g).to(device)
+    dp = DataParallelInference(model, x, gather=True, use_graph=device != "cpu")
     outs = []
     for _ in range(3):
         outs.append(dp.step())
     dp.drain()
-    full = outs[-1].clone()
+    full = outs[-1].clone().cpu()
     with torch.no_grad():
-        local = model(x)
+        local = model(x).cpu()
     q.put((rank, full, local))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_allgather_gloo_world2():
+def _run_dp(device):
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, device)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -74,6 +74,17 @@ def test_dp_allgather_gloo_world2():
     for r in range(world):
         assert res[r][0].shape == expected.shape
         assert torch.allclose(res[r][0], expected, atol=1e-5)
+
+
+def test_dp_allgather_gloo_world2():
+    _run_dp("cpu")
+
+
+@pytest.mark.gpu
+def test_dp_allgather_gloo_world2_on_one_gpu():
+    """Two ranks share the one GPU (Gloo; RCCL refuses duplicate devices): hipGraph replays on
+    two output buffers, the gather on the communication stream, event/stream ordering."""
+    _run_dp("cuda")
 
 
 def test_bench_harness_torchrun_gloo():
