@@ -43,6 +43,18 @@ constexpr int kSlab = kCh * kG;             // 64
 constexpr int kPairs = kPPL * kG;           // packed pairs per workgroup
 constexpr int kPitch = kPairs + 2;          // float2 per LDS position (+16 B: spreads the k1 stride)
 constexpr int kThreads = kB * kG;           // 240
+#ifndef AFNO_C2R_XLDS
+#define AFNO_C2R_XLDS 1  // C2R: residual tile + stats DMA'd into LDS at kernel start, fp16 FFT staging
+#endif
+// C2R addend image in LDS: [x tile: 180 positions x 128 B | stats: 180 x 8 B | pad], DMA'd
+// (global_load_lds, no VGPRs) in 7 rounds of 3 full waves x 1 KB + the 48-lane wave x 768 B --
+// the same instruction count in every wave and no branches.  Issued just BEFORE the spectrum
+// loads: the compiler treats LDS DMA and plain loads as unordered and waits vmcnt(0) before
+// the first use of the spectrum anyway, so both transfers share one memory round trip (the
+// addends used to be a second, dependent one after pass 0).
+constexpr int kXBytes = kL * 128, kSBytes = kL * 8;
+constexpr int kRound = 3 * 1024 + 768, kRounds = (kXBytes + kSBytes + kRound - 1) / kRound;  // 7
+typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ void unpack4(uint2 u, float (&f)[4]) {
   f[0] = __uint_as_float(u.x << 16);
@@ -222,13 +234,40 @@ constexpr int c2r_load_kind(int n1) {
 template <int KM>
 __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
+#if AFNO_C2R_XLDS
+  // fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its LN
+  // statistics: 49.6 KB -> still 3 workgroups per CU, and the addends need no VGPRs
+  __shared__ __attribute__((aligned(16))) h2_t lds[kL * kPitch];
+  __shared__ __attribute__((aligned(16))) char dimg[kRounds * kRound];  // x tile + stats (26.9 KB)
+  const uint2* xt = reinterpret_cast<const uint2*>(dimg);                 // [pos][16 lanes x 4 ch] bf16
+  const float2* stl = reinterpret_cast<const float2*>(dimg + kXBytes);    // [pos] (mean, rstd)
+#else
   __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
+#endif
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
   AMD_DFT_DEV_CHECK((slab + 1) * kSlab <= a.C, "afno_w_kernel");
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
   const uint16_t* sb = a.spec + (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
+  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const float2* st = a.stats + static_cast<int64_t>(o) * kL;
+#if AFNO_C2R_XLDS
+  {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const char* xbc = reinterpret_cast<const char*>(xb);
+    const char* stc = reinterpret_cast<const char*>(st);
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int b = r * kRound + wave * 1024 + lane * 16;  // byte of the image this lane fills
+      const int bx = min(b, kXBytes - 16);
+      const char* src_x = xbc + (bx >> 7) * (2 * C) + (bx & 127);
+      const char* src_s = stc + min(max(b - kXBytes, 0), kSBytes - 16);
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(b < kXBytes ? src_x : src_s),
+                                       (lds_void*)(dimg + r * kRound + wave * 1024), 16, 0, 0);
+    }
+  }
+#endif
   // ---- pass 0: Hermitian assembly of the packed pair spectrum Z = X_a + i X_b, conjugated
   // (inverse transform as conj(FFT(conj Z))); only the stored modes are loaded
   uint4 raw[kA];
@@ -241,6 +280,8 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
       raw[n1] = *reinterpret_cast<const uint4*>(sb + (kc * C + kCh * g) * 2);
     }
   }
+#if AFNO_C2R_XLDS
+#endif
   cpair v[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
@@ -276,6 +317,9 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     v[n1] = make_cpair(zp[0], zp[1]);
   }
   pass0_store(v, n2, g, lds);
+#if AFNO_C2R_XLDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS DMA landed before the barrier publishes it
+#endif
   __syncthreads();
   const int k1 = n2;
   if (k1 >= kA) return;
@@ -290,10 +334,8 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     u[n2i] = make_cpair(pa, pb);
   }
   __builtin_amdgcn_sched_barrier(0);
-  // workgroup-uniform bases + 32-bit lane offsets (SGPR base + VGPR offset addressing)
-  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
-  const float2* st = a.stats + static_cast<int64_t>(o) * kL;
-  const int lo = k1 * C + kCh * g;
+  const int lo = k1 * C + kCh * g;  // 32-bit lane offset from the workgroup-uniform base
+#if !AFNO_C2R_XLDS
   uint2 xraw[kB];
   float2 sv[kB];
 #pragma unroll
@@ -301,6 +343,7 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     xraw[k2] = *reinterpret_cast<const uint2*>(xb + lo + kA * k2 * C);
     sv[k2] = st[k1 + kA * k2];
   }
+#endif
   ChanParams cp;
   load_params(a, c0, cp);
   __builtin_amdgcn_sched_barrier(0);
@@ -312,7 +355,12 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
     float xp[kCh], h[kCh];
+#if AFNO_C2R_XLDS
+    const int n = k1 + kA * k2;
+    ln4(xt[n * kG + g], stl[n], cp, xp, h);
+#else
     ln4(xraw[k2], sv[k2], cp, xp, h);
+#endif
     uint32_t w[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
