@@ -25,3 +25,11 @@ r["patchify"] = time_graph(lambda: ops.patchify(img, 8), 5)
 r["unpatchify"] = time_graph(lambda: ops.unpatchify(t, 20, 90, 180, 8), 5)
 r["pos_add"] = time_graph(lambda: e + pos, 5)
 print({k: round(v, 1) for k, v in r.items()})
+wmat = (torch.randn(768, 1280, device="cuda") * 0.02).to(torch.bfloat16)
+be = torch.randn(768, device="cuda") * 0.02
+pos2 = pos.reshape(16200, 768)
+r2 = {"embed_fused_amd": time_graph(lambda: ops.patch_linear(img, wmat, be, pos2, 8), 5)}
+wh = (torch.randn(1280, 768, device="cuda") * 0.02).to(torch.bfloat16)
+bh = torch.randn(1280, device="cuda") * 0.02
+r2["head_fused_amd"] = time_graph(lambda: ops.linear_unpatch(e.reshape(-1, 768), wh, bh, 20, 90, 180, 8), 5)
+print({k: round(v, 1) for k, v in r2.items()})
