@@ -118,3 +118,15 @@ def test_rccl_sweep_harness_gloo():
 
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and lines[0]["world"] == 2 and lines[0]["backend"] == "gloo"
+
+
+@pytest.mark.gpu
+def test_rccl_world1_capture_and_gather_gpu():
+    """hipGraph capture while an RCCL (nccl backend) process group and its watchdog are live, and
+    all_gather_into_tensor on the communication stream (scripts/rccl_capture_probe.py; a world-
+    size-1 communicator, since one GPU cannot host two RCCL ranks)."""
+    env = dict(os.environ, MASTER_PORT=str(_free_port()), MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_capture_probe.py")], capture_output=True,
+                       text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "rccl capture probe ok" in r.stdout
