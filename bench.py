@@ -1,14 +1,21 @@
 """Headline benchmark (driver contract): FourCastNet AFNO batch-DP inference samples/s on N
 MI355X GPUs (one process per GPU, RCCL all-gather of the outputs over xGMI, hipGraph-captured
-per-step forward), plus the rfft2 / irfft2 720x1440 fp32 single-op latency (us).
+per-step forward), plus the rfft2 / irfft2 720x1440 fp32 single-op latency (us) and the FNO
+SpectralConv2d block (BASELINE config 3) as extra keys.
 
 Metric/config from BASELINE.json: "rfft2 720x1440 us + FourCastNet-FNO samples/sec at 1/2/4/8
 MI355X"; FourCastNet AFNO (720x1440, patch 8, embed 768, depth 12, 8 AFNO blocks), batch 32
-per GPU (weak scaling), bf16 activations/weights (FFTs fp32 internally), synthetic inputs,
-random-init weights.  Every timed step runs the full forward (all 12 blocks) and the output
-all-gather; K steps are bracketed by barrier + synchronize, the max over ranks is reported.
+per GPU (weak scaling), synthetic inputs, random-init weights.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+Headline precision = fp32, the reference's only precision (its plugins accept kFLOAT only,
+/root/reference/src/dft_plugins/dft_plugins.cpp:101-102): fp32 activations / residual stream /
+spectra / FFTs; GEMMs as 3-product bf16 splits with fp32 accumulation (bf16x3: ~5e-6 relative
+error per GEMM, vs ~3e-7 for fp32 FMA and ~1e-3 for TF32).  The bf16 model (bf16 activations,
+bf16 MFMA) is reported as ``bf16_samples_per_s``.  Every timed step runs the full forward (all
+12 blocks) and the output all-gather; K steps are bracketed by barrier + synchronize, and the
+max over ranks is reported.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 """
@@ -32,42 +39,116 @@ from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet, flops_per_sampl
 from tensorrt_dft_plugins_amd.parallel import DataParallelInference, init_distributed, world_info  # noqa: E402
 
 METRIC = "rfft2 720×1440 µs + FourCastNet-FNO samples/sec at 1/2/4/8 MI355X"
+DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
+COMM_ENV = ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "RCCL_MSCCL_ENABLE",
+            "NCCL_P2P_LEVEL", "MI_DFT_GATHER")
 
 
 def log(msg: str) -> None:
-    rank = int(os.environ.get("RANK", "0"))
-    if rank == 0:
+    if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def _graph_us(fn, iters: int, rounds: int) -> float:
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1000.0 / iters)
+    return round(sorted(ts)[len(ts) // 2], 3)
+
+
 def time_fft_us(iters: int = 50, rounds: int = 5) -> dict:
-    """rfft2 / irfft2 720x1440 fp32 batch 1 (contrib Rfft/Irfft ops), hipGraph of `iters` calls."""
+    """rfft2 / irfft2 720x1440 fp32 batch 1 (contrib Rfft/Irfft ops), hipGraph of `iters` calls.
+    Warm: one input/output reused (both stay in the 256 MB Infinity Cache).  Cold: the calls
+    rotate over 80 distinct inputs and outputs (660 MB > the Infinity Cache)."""
     x = torch.randn(1, 720, 1440, device="cuda")
     y = tdp.contrib_rfft(x, signal_ndim=2)
-    res = {}
-    for name, fn in (("rfft2_720x1440_us", lambda: tdp.contrib_rfft(x, signal_ndim=2)),
-                     ("irfft2_720x1440_us", lambda: tdp.contrib_irfft(y, signal_ndim=2))):
-        fn()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            fn()
-        torch.cuda.current_stream().wait_stream(s)
-        with torch.cuda.graph(g):
-            for _ in range(iters):
-                fn()
-        ts = []
-        for _ in range(rounds):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            g.replay()
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1000.0 / iters)
-        res[name] = round(sorted(ts)[len(ts) // 2], 3)
+    res = {"rfft2_720x1440_us": _graph_us(lambda: tdp.contrib_rfft(x, signal_ndim=2), iters, rounds),
+           "irfft2_720x1440_us": _graph_us(lambda: tdp.contrib_irfft(y, signal_ndim=2), iters, rounds)}
+    n = 80
+    xs = [torch.randn(1, 720, 1440, device="cuda") for _ in range(n)]
+    ys = [tdp.contrib_rfft(t, signal_ndim=2) for t in xs]
+    it = {"i": 0}
+
+    def cold_r():
+        tdp.contrib_rfft(xs[it["i"] % n], signal_ndim=2)
+        it["i"] += 1
+
+    def cold_i():
+        tdp.contrib_irfft(ys[it["i"] % n], signal_ndim=2)
+        it["i"] += 1
+
+    res["rfft2_720x1440_cold_us"] = _graph_us(cold_r, n, rounds)
+    res["irfft2_720x1440_cold_us"] = _graph_us(cold_i, n, rounds)
     return res
+
+
+def time_fno_block_us(rounds: int = 5) -> dict:
+    """BASELINE config 3: FNO SpectralConv2d block, 20 ch, 720x1440, bf16, modes 32x32, batch 1."""
+    from tensorrt_dft_plugins_amd.models.fno import FNOBlock
+
+    torch.manual_seed(0)
+    blk = FNOBlock(20, 32, 32, backend="amd").cuda().eval()
+    x = torch.randn(1, 20, 720, 1440, device="cuda").to(torch.bfloat16)
+    with torch.no_grad():
+        return {"fno_block_720x1440_bf16_us": _graph_us(lambda: blk(x), 20, rounds)}
+
+
+def run_steps(runner, steps: int, warmup: int, world: int, dev, cuda: bool) -> float:
+    """Seconds for `steps` timed steps (after `warmup`), max over ranks."""
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(warmup):
+        runner.step()
+    runner.drain()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step()
+    runner.drain()
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def build_runner(cfg, dtype, B, dev, a, seed):
+    torch.manual_seed(seed)
+    model = AFNONet(cfg, backend="amd").to(dev).to(dtype).eval()
+    x = torch.randn(B, cfg.in_chans, *cfg.img_size, device=dev).to(dtype)
+    t0 = time.perf_counter()
+    runner = DataParallelInference(model, x, gather=not a.no_gather, use_graph=not a.no_graph)
+    log(f"{dtype}: captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t0:.1f}s")
+    return model, runner
 
 
 def main(argv=None) -> int:
@@ -77,14 +158,13 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="samples per GPU (weak scaling)")
     ap.add_argument("--depth", type=int, default=12)
+    ap.add_argument("--dtype", choices=sorted(DTYPES), default="fp32", help="headline precision")
+    ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of the other-precision extra (0: skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 latency probe")
+    ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 / FNO block probes")
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--streams", type=int, default=1, help="micro-batches on concurrent HIP streams per GPU")
-    ap.add_argument("--no-gemm-table", action="store_true",
-                    help="hipBLASLt default heuristics instead of tensorrt_dft_plugins_amd/tuning/*.csv")
     a = ap.parse_args(argv)
 
     rank, world, local = init_distributed()
@@ -96,11 +176,12 @@ def main(argv=None) -> int:
     if cuda:
         torch.cuda.set_device(dev)
     tdp.load_plugins()
-    torch.manual_seed(1234 + rank)
     gemm_table = None
-    if cuda and not a.no_gemm_table:
-        # one GPU: fastest hipBLASLt solutions; DP: no stream-K GEMMs, which stall while the
-        # all-gather's RCCL blocks hold CUs (tensorrt_dft_plugins_amd/utils/gemm_tables.py)
+    from tensorrt_dft_plugins_amd.ops.spectral import mlp_on_hand_gemm
+
+    if cuda and not mlp_on_hand_gemm():
+        # hipBLASLt comparator path (MI_DFT_MLP=blas): fastest solutions for one GPU, no
+        # stream-K for DP (tensorrt_dft_plugins_amd/utils/gemm_tables.py)
         from tensorrt_dft_plugins_amd.utils.gemm_tables import table_for_world, use_gemm_table
 
         path = table_for_world(world)
@@ -112,51 +193,34 @@ def main(argv=None) -> int:
         cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
     else:
         cfg = AFNOConfig(depth=a.depth)
-    dtype = torch.bfloat16 if cuda else torch.float32
-    model = AFNONet(cfg, backend="amd").to(dev).to(dtype).eval()
+    head_dt = DTYPES[a.dtype] if cuda else torch.float32
     B = a.batch if not a.tiny else min(a.batch, 2)
-    x = torch.randn(B, cfg.in_chans, *cfg.img_size, device=dev).to(dtype)
 
-    fft = {}
+    extra = {}
     if cuda and not a.no_fft and not a.tiny and rank == 0:
-        fft = time_fft_us()
-        log(f"fft probe: {fft}")
+        extra.update(time_fft_us())
+        extra.update(time_fno_block_us())
+        log(f"single-op probes: {extra}")
 
-    t_build = time.perf_counter()
-    model.micro_batches = max(1, a.streams)
-    runner = DataParallelInference(model, x, gather=not a.no_gather, use_graph=not a.no_graph)
-    log(f"captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t_build:.1f}s; "
-        f"world={world} batch/GPU={B}")
-
-    def sync():
-        if cuda:
-            torch.cuda.synchronize(dev)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    for _ in range(a.warmup):
-        runner.step()
-    runner.drain()
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        runner.step()
-    runner.drain()
-    sync()
-    barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if cuda else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    _, runner = build_runner(cfg, head_dt, B, dev, a, 1234 + rank)
+    log(f"world={world} batch/GPU={B} dtype={head_dt}")
+    elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
+    gathered = runner.gather
+    del runner
+    if cuda:
+        torch.cuda.empty_cache()
     ms = elapsed * 1000.0 / a.steps
     samples_per_s = world * B / (elapsed / a.steps)
     tflops = samples_per_s * flops_per_sample(cfg) / 1e12
+
+    if cuda and a.extra_steps > 0 and not a.tiny:
+        other = "bf16" if a.dtype == "fp32" else "fp32"
+        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 4321 + rank)
+        e2 = run_steps(r2, a.extra_steps, 2, world, dev, cuda)
+        extra[f"{other}_samples_per_s"] = round(world * B / (e2 / a.extra_steps), 3)
+        extra[f"{other}_ms_per_step"] = round(e2 * 1000.0 / a.extra_steps, 3)
+        del r2
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -169,7 +233,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "dtype": "bf16" if head_dt == torch.bfloat16 else "fp32",
             "data": "synthetic inputs, random-init weights",
             "config": {
                 "model": "FourCastNet AFNO (720x1440, patch 8, embed 768, depth %d, 8 AFNO blocks)" % cfg.depth
@@ -178,14 +242,17 @@ def main(argv=None) -> int:
                 "seq_len": cfg.h * cfg.w,
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
-                "hipgraph": runner.cap.use_graph,
-                "output_allgather": runner.gather,
-                "streams": a.streams,
+                "hipgraph": not a.no_graph and cuda,
+                "output_allgather": gathered,
+                "gather_backend": ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()) if world > 1 else None,
+                "gemm": "hipblaslt" if gemm_table or (cuda and not mlp_on_hand_gemm()) else "hand-mfma",
+                "gemm_precision": "bf16x3 split, fp32 accumulate" if head_dt == torch.float32 else "bf16, fp32 accumulate",
                 "gemm_table": gemm_table,
+                "comm_env": {k: os.environ[k] for k in COMM_ENV if k in os.environ},
             },
             "model_tflops_per_s": round(tflops, 2),
         }
-        out.update(fft)
+        out.update(extra)
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:

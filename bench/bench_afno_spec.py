@@ -26,12 +26,15 @@ def main(argv=None):
     bs = C // nb
     w1, w2 = 0.02 * torch.randn(2, nb, bs, bs, generator=g), 0.02 * torch.randn(2, nb, bs, bs, generator=g)
     b1, b2 = 0.02 * torch.randn(2, nb, bs, generator=g), 0.02 * torch.randn(2, nb, bs, generator=g)
-    w1t, w2t, b1p, b2p = [t.cuda() for t in S.pack_afno_weights(w1, b1, w2, b2)]
-    xw = torch.randn(B, H, KM, C, 2, device="cuda").to(torch.bfloat16)
-    f = lambda: torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)  # noqa: E731
-    f()
-    t = min(time_graph(f, 10) for _ in range(5))
-    r = {"us": round(t, 1), "GBps": round(2 * xw.numel() * 2 / t / 1e3, 1)}
+    r = {}
+    for split in (False, True):  # bf16 MFMA operands / bf16x3 split (fp32 spectrum)
+        w1t, w2t, b1p, b2p = [t.cuda() for t in S.pack_afno_weights(w1, b1, w2, b2, split=split)]
+        xw = torch.randn(B, H, KM, C, 2, device="cuda").to(torch.float32 if split else torch.bfloat16)
+        f = lambda: torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)  # noqa: E731
+        f()
+        t = min(time_graph(f, 10) for _ in range(5))
+        tag = "fp32_x3" if split else "bf16"
+        r[tag] = {"us": round(t, 1), "GBps": round(2 * xw.numel() * xw.element_size() / t / 1e3, 1)}
     print(json.dumps(r))
     return r
 

@@ -9,12 +9,17 @@ struct GemmLaunch {
   const uint16_t* x = nullptr;       // [M, K] bf16 (activations)
   const uint16_t* w = nullptr;       // [N, K] bf16 (weight, F.linear layout)
   const float* bias = nullptr;       // [N] fp32 or nullptr
-  const uint16_t* residual = nullptr;  // [M, N] bf16 or nullptr (added after the activation)
-  uint16_t* y = nullptr;             // [M, N] bf16
+  const void* residual = nullptr;    // [M, N] bf16 (fp32 when out == 1) or nullptr (added after the activation)
+  void* y = nullptr;                 // [M, N] bf16 / fp32 (out == 1) / [M, 2N] split pair (out == 2)
   const float* ln_stats = nullptr;     // [M, 2] (mean, rstd) fp32 or nullptr: LayerNorm fold (see gemm.hip)
   const float* ln_c1 = nullptr;        // [N] fp32: sum_k W'[n, k] (required with ln_stats)
   int M = 0, N = 0, K = 0;
   int act = 0;               // 0 none, 1 GELU (erf)
+  // bf16x3 mode (fp32-class accuracy): x rows are [hi(K) | lo(K)] (row stride 2K; the
+  // gathered image instead has its lo plane x_lo elements after the hi plane), w rows [hi | lo]
+  int split = 0;
+  int out = 0;               // 0 bf16, 1 fp32, 2 split pair [hi(N) | lo(N)] (split mode only)
+  int64_t x_lo = 0;
   // Patch-embedding gather (x is an image [B, gC, gh*8, gw*8]; token t = (b, i, j) reads its
   // 8x8 patch of every channel, feature order (c, py, px): one 16-byte chunk per (c, py)).
   int gC = 0, gh = 0, gw = 0;

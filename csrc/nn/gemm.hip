@@ -23,6 +23,15 @@
 //    bank-conflict free for the ds_read_b128 lane groups;
 //  * blockIdx -> tile remap keeps consecutive tiles (same token panel, different feature
 //    panels) on one XCD so the token panel is served from that XCD's L2.
+//
+// fp32 mode (SPLIT, "bf16x3"): fp32 operands are carried as bf16 pairs a = a_hi + a_lo
+// (a_hi = bf16(a), a_lo = bf16(a - a_hi); 16 significant bits) and the product is
+// A_hi.B_hi + A_lo.B_hi + A_hi.B_lo with fp32 accumulation -- 3 K-segments of the same
+// pipeline (the K loop runs over 3K; each K-tile's source half is remapped in the DMA
+// address).  Relative error ~5e-6 per GEMM (fp32 FMA: ~3e-7, bf16: ~3e-3) at 3x the bf16
+// MFMA work, vs 16x for the exact-f32 MFMA (v_mfma_f32_16x16x4_f32 runs at 1/16 of the bf16
+// rate on gfx950).  Operand rows are [hi(K) | lo(K)]; outputs are fp32 (OUT 1) or a split
+// pair row [hi(N) | lo(N)] ready to be the next GEMM's operand (OUT 2).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -86,11 +95,22 @@ __device__ __forceinline__ int region_row(int r) {
 // MODE 1 (patch embedding): the token operand is gathered straight from the image -- K-tile kt
 // is channel kt and the 16-byte chunk c of a token row is patch row py = c (8 pixels), so the
 // un-patchified tensor never exists.
-template <int REG, int MODE>
+template <int REG, int MODE, bool SPLIT>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
                                              int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
   char* dst = stage + REG * kRegion;
+  // SPLIT: K-tile kt of the 3K loop = segment seg (0: hi.hi, 1: lo.hi, 2: hi.lo) of logical
+  // K-tile kl; operand rows are [hi | lo] (row stride 2K), the gathered image has a lo plane
+  int64_t ld = K, wcol = 0, xcol = 0;
+  if constexpr (SPLIT) {
+    const int KT0 = static_cast<int>(K / kBK);
+    const int seg = kt >= 2 * KT0 ? 2 : (kt >= KT0 ? 1 : 0);
+    kt -= seg * KT0;
+    ld = 2 * K;
+    wcol = seg == 2 ? K : 0;
+    xcol = seg == 1 ? (MODE == 1 ? p.x_lo : K) : 0;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int rb = (wave * 2 + i) * 8;
@@ -99,11 +119,11 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
     const int tr = region_row<REG>(row);
     const uint16_t* g;
     if constexpr (REG == 0 || REG == 3) {
-      g = W + static_cast<int64_t>(f0 + tr) * K + kt * kBK + chunk * 8;
+      g = W + static_cast<int64_t>(f0 + tr) * ld + wcol + kt * kBK + chunk * 8;
     } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
-      g = X + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
+      g = X + xcol + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
     } else {
-      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * K + kt * kBK + chunk * 8;
+      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * ld + xcol + kt * kBK + chunk * 8;
     }
     __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
   }
@@ -157,7 +177,7 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE>
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
   const uint16_t* __restrict__ W = p.w;
@@ -172,8 +192,8 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
   const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
   const int f0 = ft * kBF, t0 = tt * kBT;
-  const int KT = K / kBK;
-  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && KT * kBK == K && KT > 0, "gemm_bf16_kernel");
+  const int KT = (SPLIT ? 3 : 1) * (K / kBK);
+  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && (K / kBK) * kBK == K && KT > 0, "gemm_bf16_kernel");
   const int r16 = lane & 15, kq = lane >> 4;
 
   f32x4 acc[8][4];
@@ -205,12 +225,12 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       }
   }
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
-  stage_region<0, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<1, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<2, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<3, MODE>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
   if (KT > 1) {
-    stage_region<0, MODE>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane, p, gb);
+    stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane, p, gb);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
   } else {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -229,7 +249,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     const int P = 4 * t;
     // ---- phase 0: quadrant (mi 0, ni 0)
     wait_regions(issued(P - 2) + issued(P - 1));
-    if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -237,7 +257,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 1: (0, 1)
     wait_regions(issued(P - 1) + issued(P));
-    if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -245,7 +265,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 2: (1, 1)
     wait_regions(issued(P) + issued(P + 1));
-    if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
     if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -253,7 +273,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
     wait_regions(issued(P + 1) + issued(P + 2));
-    if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
+    if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
     if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -310,33 +330,53 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       }
       if constexpr (RES) {
         const int64_t roff = (MODE == 1 && p.res_rows > 0) ? static_cast<int64_t>(t % p.res_rows) * N + f : off;
-        const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + roff);
-        v[0] += __uint_as_float(rr.x << 16);
-        v[1] += __uint_as_float(rr.x & 0xffff0000u);
-        v[2] += __uint_as_float(rr.y << 16);
-        v[3] += __uint_as_float(rr.y & 0xffff0000u);
+        if constexpr (OUT == 1) {  // fp32 residual (in place allowed: same lane reads, then writes)
+          const float4 rr = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + roff);
+          v[0] += rr.x;
+          v[1] += rr.y;
+          v[2] += rr.z;
+          v[3] += rr.w;
+        } else {
+          const uint2 rr = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + roff);
+          v[0] += __uint_as_float(rr.x << 16);
+          v[1] += __uint_as_float(rr.x & 0xffff0000u);
+          v[2] += __uint_as_float(rr.y << 16);
+          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+        }
       }
-      *reinterpret_cast<uint2*>(p.y + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+      if constexpr (OUT == 1) {
+        *reinterpret_cast<float4*>(static_cast<float*>(p.y) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (OUT == 2) {  // split pair row [hi(N) | lo(N)]
+        float lo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
+        uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + f;
+        *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+        *reinterpret_cast<uint2*>(yr + N) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
+      } else {
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+      }
     }
   }
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE = 0>
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
 void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT>;
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm attr: ") + hipGetErrorString(e));
     attr_done = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE>), grid, dim3(kThreads), kLds, st, p);
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
 }
 
+// bf16 path: every (act, bias, residual, LN) combination of the plain GEMM
 template <int ACT, bool BIAS, bool RES>
 void launch_ln(const GemmLaunch& p, hipStream_t st, dim3 grid) {
-  if (p.ln_stats) launch_one<ACT, BIAS, RES, true>(p, st, grid);
-  else launch_one<ACT, BIAS, RES, false>(p, st, grid);
+  if (p.ln_stats) launch_one<ACT, BIAS, RES, true, 0, false, 0>(p, st, grid);
+  else launch_one<ACT, BIAS, RES, false, 0, false, 0>(p, st, grid);
 }
 
 template <int ACT, bool BIAS>
@@ -345,48 +385,89 @@ void launch_res(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   else launch_ln<ACT, BIAS, false>(p, st, grid);
 }
 
+// split (bf16x3) path: fp32 output (+ fp32 residual) or split-pair output (no residual)
+template <int ACT, bool BIAS>
+void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if (p.out == 2) {
+    if (p.residual) throw std::runtime_error("amd_dft: gemm: split-pair output takes no residual");
+    launch_one<ACT, BIAS, false, false, 0, true, 2>(p, st, grid);
+  } else if (p.residual) {
+    launch_one<ACT, BIAS, true, false, 0, true, 1>(p, st, grid);
+  } else {
+    launch_one<ACT, BIAS, false, false, 0, true, 1>(p, st, grid);
+  }
+}
+
+void throw_last(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ") + what + ": " + hipGetErrorString(e));
+}
+
 }  // namespace
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return M >= 1 && N % kBF == 0 && K % kBK == 0 && K >= kBK && M * K < (int64_t(1) << 31) &&
-         M * N < (int64_t(1) << 31) && N * K < (int64_t(1) << 31);
+  return M >= 1 && N % kBF == 0 && K % kBK == 0 && K >= kBK && M < (int64_t(1) << 31) && N * K < (int64_t(1) << 31);
 }
 
 void launch_gemm(const GemmLaunch& p, void* stream) {
   if (!gemm_supported(p.M, p.N, p.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
   if (p.ln_stats && !p.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
+  if (p.out < 0 || p.out > 2 || (p.out != 0) != (p.split != 0))
+    throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
+  if (p.split && p.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool bias = p.bias != nullptr;
   if (p.gC > 0 || p.sC > 0) {  // patch-embedding gather / un-patchify scatter (no activation, no LN)
     if (p.act != 0 || p.ln_stats) throw std::runtime_error("amd_dft: gemm: patch modes take no activation / LN");
+    if (p.split && p.out != 1) throw std::runtime_error("amd_dft: gemm: split patch modes write fp32");
     if (p.gC > 0) {
       if (p.K != p.gC * 64 || static_cast<int64_t>(p.M) % (static_cast<int64_t>(p.gh) * p.gw) != 0)
         throw std::runtime_error("amd_dft: gemm: patch gather needs K = C*64 and M = B*h*w");
-      if (bias && p.residual) launch_one<0, true, true, false, 1>(p, st, grid);
-      else if (bias) launch_one<0, true, false, false, 1>(p, st, grid);
-      else if (p.residual) launch_one<0, false, true, false, 1>(p, st, grid);
-      else launch_one<0, false, false, false, 1>(p, st, grid);
+      if (static_cast<int64_t>(p.M) * p.K >= (int64_t(1) << 31) || (p.split && p.x_lo + static_cast<int64_t>(p.M) * p.K >= (int64_t(1) << 31)))
+        throw std::runtime_error("amd_dft: gemm: patch gather uses 32-bit offsets");
+      if (p.split) {
+        if (bias && p.residual) launch_one<0, true, true, false, 1, true, 1>(p, st, grid);
+        else if (bias) launch_one<0, true, false, false, 1, true, 1>(p, st, grid);
+        else if (p.residual) launch_one<0, false, true, false, 1, true, 1>(p, st, grid);
+        else launch_one<0, false, false, false, 1, true, 1>(p, st, grid);
+      } else {
+        if (bias && p.residual) launch_one<0, true, true, false, 1, false, 0>(p, st, grid);
+        else if (bias) launch_one<0, true, false, false, 1, false, 0>(p, st, grid);
+        else if (p.residual) launch_one<0, false, true, false, 1, false, 0>(p, st, grid);
+        else launch_one<0, false, false, false, 1, false, 0>(p, st, grid);
+      }
     } else {
       if (p.N != p.sC * 64 || p.residual || static_cast<int64_t>(p.M) % (static_cast<int64_t>(p.sh) * p.sw) != 0)
         throw std::runtime_error("amd_dft: gemm: un-patchify scatter needs N = C*64, M = B*h*w, no residual");
-      if (bias) launch_one<0, true, false, false, 2>(p, st, grid);
-      else launch_one<0, false, false, false, 2>(p, st, grid);
+      if (p.split) {
+        if (bias) launch_one<0, true, false, false, 2, true, 1>(p, st, grid);
+        else launch_one<0, false, false, false, 2, true, 1>(p, st, grid);
+      } else {
+        if (bias) launch_one<0, true, false, false, 2, false, 0>(p, st, grid);
+        else launch_one<0, false, false, false, 2, false, 0>(p, st, grid);
+      }
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm launch: ") + hipGetErrorString(e));
+    throw_last("gemm launch");
     return;
   }
-  if (p.act == 1) {
+  if (p.split) {
+    if (p.act == 1) {
+      if (bias) launch_split<1, true>(p, st, grid);
+      else launch_split<1, false>(p, st, grid);
+    } else {
+      if (bias) launch_split<0, true>(p, st, grid);
+      else launch_split<0, false>(p, st, grid);
+    }
+  } else if (p.act == 1) {
     if (bias) launch_res<1, true>(p, st, grid);
     else launch_res<1, false>(p, st, grid);
   } else {
     if (bias) launch_res<0, true>(p, st, grid);
     else launch_res<0, false>(p, st, grid);
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm launch: ") + hipGetErrorString(e));
+  throw_last("gemm launch");
 }
 
 }  // namespace amd_dft

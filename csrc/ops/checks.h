@@ -7,7 +7,10 @@
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGraphsC10Utils.h>
 
+#include <atomic>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 
 namespace amd_dft {
@@ -27,6 +30,34 @@ inline const at::Tensor& checked(const at::Tensor& out, const char* op) {
     TORCH_CHECK(ok, "amd_dft.", op, ": output contains NaN/Inf (MI_DFT_CHECK_FINITE=1)");
   }
   return out;
+}
+
+// ---- visible fallbacks: every time a GPU op routes to ATen / a vendor
+// library instead of its hand kernel it is counted per op, warned once per op, and raises
+// when MI_DFT_STRICT=1 (tests and benches assert zero fallbacks on the hot paths).
+struct FallbackRegistry {
+  std::mutex mu;
+  std::map<std::string, int64_t> counts;
+  std::atomic<int64_t> total{0};
+};
+inline FallbackRegistry& fallback_registry() {
+  static FallbackRegistry r;
+  return r;
+}
+inline void fallback_note(const char* op, const char* why) {
+  static const bool strict = [] {
+    const char* e = std::getenv("MI_DFT_STRICT");
+    return e && std::string(e) != "0";
+  }();
+  TORCH_CHECK(!strict, "amd_dft.", op, ": no hand kernel for this call (", why, ") and MI_DFT_STRICT=1");
+  auto& r = fallback_registry();
+  bool first = false;
+  {
+    std::lock_guard<std::mutex> g(r.mu);
+    first = r.counts[op]++ == 0;
+  }
+  r.total.fetch_add(1);
+  if (first) TORCH_WARN("amd_dft.", op, ": falling back to ATen (", why, "); counted in amd_dft.fallback_counts()");
 }
 
 }  // namespace amd_dft

@@ -657,7 +657,8 @@ at::Tensor r2c_ln_cuda(const at::Tensor& x_, int64_t dim, double scale, int64_t 
   LnIO ln{stats.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(),
           pre_.has_value() ? pre.data_ptr<float>() : nullptr};
   const int64_t C = x.size(-1);
-  if (x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16 && !std::getenv("MI_DFT_NO_AFNO_W") &&
+  const bool w_f32 = x.scalar_type() == at::kFloat && odt == at::kFloat;
+  if (((x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16) || w_f32) && !std::getenv("MI_DFT_NO_AFNO_W") &&
       afno_w_supported(static_cast<int>(s.n), static_cast<int>(C), static_cast<int>(s.lo)) &&
       x.numel() / (s.n * C) < (int64_t(1) << 31)) {
     AfnoWLaunch p;  // 16-byte-lane two-pass kernel (afno_wfft.hip)
@@ -672,6 +673,7 @@ at::Tensor r2c_ln_cuda(const at::Tensor& x_, int64_t dim, double scale, int64_t 
     p.C = static_cast<int>(C);
     p.KM = static_cast<int>(s.lo);
     p.scale = static_cast<float>(scale);
+    p.f32 = w_f32 ? 1 : 0;
     launch_afno_w_r2c_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
     return checked(out, "r2c_ln");
   }
@@ -680,8 +682,7 @@ at::Tensor r2c_ln_cuda(const at::Tensor& x_, int64_t dim, double scale, int64_t 
                static_cast<int>(s.lo), 0, static_cast<float>(scale), false, nullptr, nullptr, &ln))
     return checked(out, "r2c_ln");
   // no specialised kernel for this shape: normalise with ATen, then the plain R2C
-  TORCH_WARN_ONCE("amd_dft.r2c_ln: no specialised LayerNorm-fused kernel for this shape/dtype; "
-                  "using ATen LayerNorm + the plain R2C");
+  fallback_note("r2c_ln", "no LayerNorm-fused W-transform for this shape/dtype: ATen LayerNorm + the plain R2C");
   at::Tensor h = ln_apply(x, stats, g, b, pre_, nullptr).to(x.scalar_type());
   return r2c_cuda(h, dv, scale, kv, odt);
 }
@@ -719,6 +720,33 @@ at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double 
              b = b_.to(at::kFloat).contiguous();
   at::Tensor pre;
   if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+  TORCH_CHECK(X.sizes().slice(0, axis) == x.sizes().slice(0, axis) && X.size(axis + 1) == x.size(-1) &&
+                  X.size(axis) <= n / 2 + 1,
+              "amd_dft.c2r_ln_add: X must be [..., km, C, 2] with the leading dims and C of x and km <= n/2+1");
+  const bool w_f32 = X.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat;
+  if (w_f32 && X.numel() > 0) {
+    const int64_t C = x.size(-1);
+    if (!std::getenv("MI_DFT_NO_AFNO_W") && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
+        x.numel() / (n * C) < (int64_t(1) << 31)) {
+      at::Tensor out = at::empty_like(x);
+      AfnoWLaunch p;  // fp32 instantiation of the two-pass kernel (afno_wfft.hip)
+      p.x = x.data_ptr();
+      p.stats = stats.data_ptr<float>();
+      p.gamma = g.data_ptr<float>();
+      p.beta = b.data_ptr<float>();
+      p.pre = pre_.has_value() ? pre.data_ptr<float>() : nullptr;
+      p.spec = X.data_ptr();
+      p.out = out.data_ptr();
+      p.O = static_cast<int>(x.numel() / (n * C));
+      p.L = static_cast<int>(n);
+      p.C = static_cast<int>(C);
+      p.KM = static_cast<int>(km);
+      p.scale = static_cast<float>(scale);
+      p.f32 = 1;
+      launch_afno_w_c2r_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+      return checked(out, "c2r_ln_add");
+    }
+  }
   if (X.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && X.numel() > 0) {
     C2RShape sh = c2r_shape(X.sizes(), dv, nv, kv);
     const DimSpec& s = sh.specs[0];
@@ -753,8 +781,7 @@ at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double 
                  static_cast<float>(scale), true, x.data_ptr(), nullptr, &ln))
       return checked(out, "c2r_ln_add");
   }
-  TORCH_WARN_ONCE("amd_dft.c2r_ln_add: no specialised LayerNorm-fused kernel for this shape/dtype; "
-                  "using ATen LayerNorm + the plain C2R");
+  fallback_note("c2r_ln_add", "no LayerNorm-fused W-transform for this shape/dtype: ATen LayerNorm + the plain C2R");
   at::Tensor xp;
   at::Tensor h = ln_apply(x, stats, g, b, pre_, &xp);
   return c2r_add_cuda(X, dv, nv, scale, kv, xp.to(x.scalar_type()).contiguous(), h.to(x.scalar_type()).contiguous(),

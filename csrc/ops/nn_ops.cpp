@@ -9,6 +9,8 @@
 
 #include "trace.h"
 #include "../nn/gemm.h"
+#include "../spectral/spectral.h"
+#include "checks.h"
 
 namespace amd_dft {
 void launch_patch_remap(const void* src, void* dst, int64_t B, int C, int h, int w, bool to_tokens, void* stream);
@@ -36,7 +38,10 @@ at::Tensor patchify_cuda(const at::Tensor& x_, int64_t p) {
   TORCH_CHECK(x_.dim() == 4 && x_.size(2) % p == 0 && x_.size(3) % p == 0, "patchify: x must be [B, C, h*p, w*p]");
   const c10::DeviceGuard guard(x_.device());
   at::Tensor x = x_.contiguous();
-  if (!vec_ok(x, p)) return patchify_cpu(x, p);
+  if (!vec_ok(x, p)) {
+    fallback_note("patchify", "needs bf16, p == 8, 16-byte aligned");
+    return patchify_cpu(x, p);
+  }
   const int64_t B = x.size(0), C = x.size(1), h = x.size(2) / p, w = x.size(3) / p;
   at::Tensor out = at::empty({B * h * w, C * p * p}, x.options());
   launch_patch_remap(x.data_ptr(), out.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(w), true,
@@ -48,7 +53,10 @@ at::Tensor unpatchify_cuda(const at::Tensor& t_, int64_t C, int64_t h, int64_t w
   TORCH_CHECK(t_.numel() % (h * w * C * p * p) == 0, "unpatchify: size mismatch");
   const c10::DeviceGuard guard(t_.device());
   at::Tensor t = t_.contiguous();
-  if (!vec_ok(t, p)) return unpatchify_cpu(t, C, h, w, p);
+  if (!vec_ok(t, p)) {
+    fallback_note("unpatchify", "needs bf16, p == 8, 16-byte aligned");
+    return unpatchify_cpu(t, C, h, w, p);
+  }
   const int64_t B = t.numel() / (h * w * C * p * p);
   at::Tensor out = at::empty({B, C, h * p, w * p}, t.options());
   launch_patch_remap(t.data_ptr(), out.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(w), false,
@@ -91,8 +99,12 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
   TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear: act must be 0 (none) or 1 (gelu)");
   TORCH_CHECK(w_.dim() == 2 && x_.size(-1) == w_.size(1), "amd_dft.linear: x [..., K], w [N, K]");
   const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "amd_dft.linear: bias must have N entries");
   if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K))
+  {
+    fallback_note("linear", "needs bf16 operands, N % 256 == 0, K % 64 == 0 (fp32: use linear3)");
     return linear_ref(x_, w_, bias, act, residual);
+  }
   at::Tensor x = x_.contiguous(), w = w_.contiguous();
   std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
   os.back() = N;
@@ -107,8 +119,8 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
   p.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   p.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
   p.bias = b.defined() ? b.data_ptr<float>() : nullptr;
-  p.residual = r.defined() ? reinterpret_cast<const uint16_t*>(r.data_ptr()) : nullptr;
-  p.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  p.residual = r.defined() ? r.data_ptr() : nullptr;
+  p.y = y.data_ptr();
   p.M = static_cast<int>(M);
   p.N = static_cast<int>(N);
   p.K = static_cast<int>(K);
@@ -141,9 +153,13 @@ at::Tensor patch_linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c
   TORCH_CHECK(w_.dim() == 2 && w_.size(1) == x_.size(1) * p * p, "patch_linear: w must be [N, C*p*p]");
   const int64_t B = x_.size(0), C = x_.size(1), h = x_.size(2) / p, w = x_.size(3) / p, N = w_.size(0);
   const int64_t M = B * h * w, K = C * p * p;
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "patch_linear: bias must have N entries");
   const bool native = p == 8 && x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
                       gemm_supported(M, N, K) && x_.numel() < (int64_t(1) << 31);
-  if (!native) return patch_linear_cpu(x_, w_, bias, pos, p);  // ATen ops on the device tensors
+  if (!native) {  // ATen ops on the device tensors
+    fallback_note("patch_linear", "needs bf16, p == 8, N % 256 == 0 (fp32: use patch_linear3)");
+    return patch_linear_cpu(x_, w_, bias, pos, p);
+  }
   at::Tensor x = x_.contiguous(), wc = w_.contiguous();
   at::Tensor y = at::empty({M, N}, x.options());
   at::Tensor b, r;
@@ -156,9 +172,9 @@ at::Tensor patch_linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c
   g.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
   g.w = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
-  g.residual = r.defined() ? reinterpret_cast<const uint16_t*>(r.data_ptr()) : nullptr;
+  g.residual = r.defined() ? r.data_ptr() : nullptr;
   g.res_rows = static_cast<int>(h * w);
-  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.y = y.data_ptr();
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.K = static_cast<int>(K);
@@ -186,9 +202,13 @@ at::Tensor linear_unpatch_cuda(const at::Tensor& t_, const at::Tensor& w_, const
               "linear_unpatch: t [..., K], w [C*p*p, K] in (c, py, px) feature order");
   const int64_t K = w_.size(1), N = w_.size(0), M = t_.numel() / std::max<int64_t>(K, 1);
   TORCH_CHECK(M % (h * wd) == 0, "linear_unpatch: token count must be a multiple of h*w");
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "linear_unpatch: bias must have N entries");
   const bool native = p == 8 && t_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
                       gemm_supported(M, N, K) && M * N < (int64_t(1) << 31);
-  if (!native) return linear_unpatch_cpu(t_, w_, bias, C, h, wd, p);
+  if (!native) {
+    fallback_note("linear_unpatch", "needs bf16, p == 8, N % 256 == 0 (fp32: use linear_unpatch3)");
+    return linear_unpatch_cpu(t_, w_, bias, C, h, wd, p);
+  }
   at::Tensor t = t_.contiguous(), wc = w_.contiguous();
   const int64_t B = M / (h * wd);
   at::Tensor y = at::empty({B, C, h * p, wd * p}, t.options());
@@ -198,7 +218,7 @@ at::Tensor linear_unpatch_cuda(const at::Tensor& t_, const at::Tensor& w_, const
   g.x = reinterpret_cast<const uint16_t*>(t.data_ptr());
   g.w = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
-  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.y = y.data_ptr();
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.K = static_cast<int>(K);
@@ -221,6 +241,218 @@ at::Tensor linear_meta(const at::Tensor& x, const at::Tensor& w, const c10::opti
   return at::empty(os, x.options());
 }
 
+// ------------------------------------------------------------------ bf16x3 (fp32-class) GEMMs
+// An fp32 operand is carried as a bf16 pair a = hi + lo (hi = bf16(a), lo = bf16(a - hi)):
+// split_bf16 packs rows as [..., 2K] = [hi(K) | lo(K)] (rows=true) or planes [2, ...] (rows=false).
+// linear3 / patch_linear3 / linear_unpatch3 take split operands and run the 3-product GEMM
+// (csrc/nn/gemm.hip SPLIT mode) with fp32 accumulation and fp32 (or split-pair) outputs.
+at::Tensor unsplit_rows(const at::Tensor& xs) {
+  const int64_t K2 = xs.size(-1);
+  TORCH_CHECK(K2 % 2 == 0, "amd_dft: split rows must have an even last dim");
+  return xs.narrow(-1, 0, K2 / 2).to(at::kFloat) + xs.narrow(-1, K2 / 2, K2 / 2).to(at::kFloat);
+}
+
+at::Tensor split_ref(const at::Tensor& x, bool rows) {
+  at::Tensor xf = x.to(at::kFloat);
+  at::Tensor hi = xf.to(at::kBFloat16);
+  at::Tensor lo = (xf - hi.to(at::kFloat)).to(at::kBFloat16);
+  return rows ? at::cat({hi, lo}, -1).contiguous() : at::stack({hi, lo}, 0).contiguous();
+}
+
+at::Tensor split_bf16_cpu(const at::Tensor& x, bool rows) { return split_ref(x, rows); }
+
+at::Tensor split_bf16_cuda(const at::Tensor& x_, bool rows) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kFloat, "amd_dft.split_bf16: x must be float32");
+  TORCH_CHECK(x_.dim() >= 1, "amd_dft.split_bf16: x must have at least one dim");
+  at::Tensor x = x_.contiguous();
+  const int64_t cols = x.size(-1);
+  TORCH_CHECK(x.numel() % 8 == 0 && (!rows || cols % 8 == 0), "amd_dft.split_bf16: needs multiples of 8 elements");
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  if (rows) os.back() = 2 * cols;
+  else os.insert(os.begin(), 2);
+  at::Tensor y = at::empty(os, x.options().dtype(at::kBFloat16));
+  launch_split_bf16(x.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), static_cast<int>(cols),
+                    rows, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor split_bf16_meta(const at::Tensor& x, bool rows) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  if (rows) os.back() = 2 * os.back();
+  else os.insert(os.begin(), 2);
+  return at::empty(os, x.options().dtype(at::kBFloat16));
+}
+
+void check_split_linear(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,
+                        const char* op) {
+  TORCH_CHECK(xs.scalar_type() == at::kBFloat16 && ws.scalar_type() == at::kBFloat16, "amd_dft.", op,
+              ": split operands must be bfloat16 pairs");
+  TORCH_CHECK(ws.dim() == 2 && ws.size(1) % 2 == 0, "amd_dft.", op, ": ws must be [N, 2K] = [hi | lo]");
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == ws.size(0), "amd_dft.", op,
+              ": bias must have N entries");
+}
+
+at::Tensor linear3_cpu(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>& bias, int64_t act,
+                       const c10::optional<at::Tensor>& residual, bool split_out) {
+  check_split_linear(xs, ws, bias, "linear3");
+  TORCH_CHECK(xs.size(-1) == ws.size(1), "amd_dft.linear3: xs [..., 2K], ws [N, 2K]");
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear3: act must be 0 (none) or 1 (gelu)");
+  at::Tensor y = at::linear(unsplit_rows(xs), unsplit_rows(ws),
+                            bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
+                                                                : c10::nullopt);
+  if (act == 1) y = at::gelu(y);
+  if (residual.has_value() && residual->defined()) y = y + residual->to(at::kFloat).reshape(y.sizes());
+  return split_out ? split_ref(y, true) : y.contiguous();
+}
+
+at::Tensor linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10::optional<at::Tensor>& bias,
+                        int64_t act, const c10::optional<at::Tensor>& residual, bool split_out) {
+  const c10::DeviceGuard guard(xs_.device());
+  check_split_linear(xs_, ws_, bias, "linear3");
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear3: act must be 0 (none) or 1 (gelu)");
+  TORCH_CHECK(xs_.size(-1) == ws_.size(1), "amd_dft.linear3: xs [..., 2K], ws [N, 2K]");
+  const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0 (got N=",
+              N, ", K=", K, ")");
+  TORCH_CHECK(!(split_out && residual.has_value() && residual->defined()),
+              "amd_dft.linear3: a split-pair output takes no residual");
+  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = split_out ? 2 * N : N;
+  at::Tensor y = at::empty(os, xs.options().dtype(split_out ? at::kBFloat16 : at::kFloat));
+  at::Tensor b, r;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->numel() == M * N, "amd_dft.linear3: residual must have the output's shape");
+    r = residual->to(at::kFloat).contiguous();
+  }
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(xs.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  p.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  p.residual = r.defined() ? r.data_ptr() : nullptr;
+  p.y = y.data_ptr();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.act = static_cast<int>(act);
+  p.split = 1;
+  p.out = split_out ? 2 : 1;
+  if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>&, int64_t,
+                        const c10::optional<at::Tensor>&, bool split_out) {
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = split_out ? 2 * ws.size(0) : ws.size(0);
+  return at::empty(os, xs.options().dtype(split_out ? at::kBFloat16 : at::kFloat));
+}
+
+// xs = split planes [2, B, C, h*p, w*p] of the fp32 image; ws [N, 2*C*p*p]; fp32 tokens [B*h*w, N]
+at::Tensor patch_linear3_cpu(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,
+                             const c10::optional<at::Tensor>& pos, int64_t p) {
+  check_split_linear(xs, ws, bias, "patch_linear3");
+  TORCH_CHECK(xs.dim() == 5 && xs.size(0) == 2, "amd_dft.patch_linear3: xs must be split planes [2, B, C, H, W]");
+  at::Tensor x = xs.select(0, 0).to(at::kFloat) + xs.select(0, 1).to(at::kFloat);
+  at::Tensor t = patchify_cpu(x, p);
+  at::Tensor y = at::linear(t, unsplit_rows(ws),
+                            bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
+                                                                : c10::nullopt);
+  if (pos.has_value() && pos->defined()) {
+    const int64_t hw = (x.size(2) / p) * (x.size(3) / p);
+    y = (y.reshape({-1, hw, ws.size(0)}) + pos->to(at::kFloat).reshape({1, hw, ws.size(0)})).reshape({-1, ws.size(0)});
+  }
+  return y.contiguous();
+}
+
+at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10::optional<at::Tensor>& bias,
+                              const c10::optional<at::Tensor>& pos, int64_t p) {
+  const c10::DeviceGuard guard(xs_.device());
+  check_split_linear(xs_, ws_, bias, "patch_linear3");
+  TORCH_CHECK(xs_.dim() == 5 && xs_.size(0) == 2 && xs_.size(3) % p == 0 && xs_.size(4) % p == 0,
+              "amd_dft.patch_linear3: xs must be split planes [2, B, C, h*p, w*p]");
+  const int64_t B = xs_.size(1), C = xs_.size(2), h = xs_.size(3) / p, w = xs_.size(4) / p, N = ws_.size(0);
+  const int64_t M = B * h * w, K = C * p * p;
+  TORCH_CHECK(p == 8 && ws_.size(1) == 2 * K && gemm_supported(M, N, K) && xs_.numel() < (int64_t(1) << 31),
+              "amd_dft.patch_linear3: needs p == 8, ws [N, 2*C*64], N % 256 == 0 and < 2^31 image elements");
+  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
+  at::Tensor y = at::empty({M, N}, xs.options().dtype(at::kFloat));
+  at::Tensor b, r;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->numel() == h * w * N, "amd_dft.patch_linear3: pos must be [h*w, N]");
+    r = pos->to(at::kFloat).contiguous();
+  }
+  GemmLaunch g;
+  g.x = reinterpret_cast<const uint16_t*>(xs.data_ptr());
+  g.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  g.residual = r.defined() ? r.data_ptr() : nullptr;
+  g.res_rows = static_cast<int>(h * w);
+  g.y = y.data_ptr();
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.gC = static_cast<int>(C);
+  g.gh = static_cast<int>(h);
+  g.gw = static_cast<int>(w);
+  g.split = 1;
+  g.out = 1;
+  g.x_lo = xs.numel() / 2;
+  launch_gemm(g, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
+  return y;
+}
+
+at::Tensor patch_linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>&,
+                              const c10::optional<at::Tensor>&, int64_t p) {
+  return at::empty({xs.size(1) * (xs.size(3) / p) * (xs.size(4) / p), ws.size(0)}, xs.options().dtype(at::kFloat));
+}
+
+at::Tensor linear_unpatch3_cpu(const at::Tensor& ts, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,
+                               int64_t C, int64_t h, int64_t wd, int64_t p) {
+  check_split_linear(ts, ws, bias, "linear_unpatch3");
+  at::Tensor y = at::linear(unsplit_rows(ts), unsplit_rows(ws),
+                            bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
+                                                                : c10::nullopt);
+  return unpatchify_cpu(y, C, h, wd, p);
+}
+
+at::Tensor linear_unpatch3_cuda(const at::Tensor& ts_, const at::Tensor& ws_, const c10::optional<at::Tensor>& bias,
+                                int64_t C, int64_t h, int64_t wd, int64_t p) {
+  const c10::DeviceGuard guard(ts_.device());
+  check_split_linear(ts_, ws_, bias, "linear_unpatch3");
+  const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = ts_.numel() / std::max<int64_t>(2 * K, 1);
+  TORCH_CHECK(ts_.size(-1) == 2 * K && N == C * p * p && p == 8 && M % (h * wd) == 0 && gemm_supported(M, N, K),
+              "amd_dft.linear_unpatch3: ts [..., 2K], ws [C*64, 2K] in (c, py, px) order, p == 8");
+  at::Tensor ts = ts_.contiguous(), ws = ws_.contiguous();
+  const int64_t B = M / (h * wd);
+  at::Tensor y = at::empty({B, C, h * p, wd * p}, ts.options().dtype(at::kFloat));
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  GemmLaunch g;
+  g.x = reinterpret_cast<const uint16_t*>(ts.data_ptr());
+  g.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  g.y = y.data_ptr();
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.sC = static_cast<int>(C);
+  g.sh = static_cast<int>(h);
+  g.sw = static_cast<int>(wd);
+  g.split = 1;
+  g.out = 1;
+  launch_gemm(g, c10::hip::getCurrentHIPStream(ts.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear_unpatch3_meta(const at::Tensor& ts, const at::Tensor& ws, const c10::optional<at::Tensor>&, int64_t C,
+                                int64_t h, int64_t wd, int64_t p) {
+  return at::empty({ts.numel() / ws.size(1) / (h * wd), C, h * p, wd * p}, ts.options().dtype(at::kFloat));
+}
+
 }  // namespace
 }  // namespace amd_dft
 
@@ -230,6 +462,10 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("linear(Tensor x, Tensor w, Tensor? bias=None, int act=0, Tensor? residual=None) -> Tensor");
   m.def("patch_linear(Tensor x, Tensor w, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
   m.def("linear_unpatch(Tensor t, Tensor w, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
+  m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
+  m.def("linear3(Tensor xs, Tensor ws, Tensor? bias=None, int act=0, Tensor? residual=None, bool split_out=False) -> Tensor");
+  m.def("patch_linear3(Tensor xs, Tensor ws, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
+  m.def("linear_unpatch3(Tensor ts, Tensor ws, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cuda));
@@ -237,6 +473,10 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cuda));
   m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cuda));
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cuda));
+  m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
+  m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cuda));
+  m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cuda));
+  m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cuda));
 }
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cpu));
@@ -244,6 +484,10 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cpu));
   m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cpu));
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cpu));
+  m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
+  m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cpu));
+  m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cpu));
+  m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cpu));
 }
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("patchify", &amd_dft::patchify_meta);
@@ -251,4 +495,8 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("linear", &amd_dft::linear_meta);
   m.impl("patch_linear", &amd_dft::patch_linear_meta);
   m.impl("linear_unpatch", &amd_dft::linear_unpatch_meta);
+  m.impl("split_bf16", &amd_dft::split_bf16_meta);
+  m.impl("linear3", &amd_dft::linear3_meta);
+  m.impl("patch_linear3", &amd_dft::patch_linear3_meta);
+  m.impl("linear_unpatch3", &amd_dft::linear_unpatch3_meta);
 }

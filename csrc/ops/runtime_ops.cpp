@@ -6,6 +6,8 @@
 #include <ATen/ATen.h>
 #include <torch/library.h>
 
+#include "checks.h"
+
 namespace amd_dft {
 namespace {
 
@@ -20,6 +22,26 @@ at::Tensor wrap_host_ptr(int64_t ptr, at::IntArrayRef shape, at::ScalarType dtyp
   return at::from_blob(reinterpret_cast<void*>(ptr), shape, at::TensorOptions().dtype(dtype));
 }
 
+// fallback_counts(): (op names, counts) of every GPU op call that ran without its hand kernel
+std::tuple<std::vector<std::string>, std::vector<int64_t>> fallback_counts() {
+  auto& r = fallback_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  std::vector<std::string> names;
+  std::vector<int64_t> counts;
+  for (const auto& kv : r.counts) {
+    names.push_back(kv.first);
+    counts.push_back(kv.second);
+  }
+  return {names, counts};
+}
+
+void fallback_reset() {
+  auto& r = fallback_registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  r.counts.clear();
+  r.total.store(0);
+}
+
 }  // namespace
 }  // namespace amd_dft
 
@@ -27,4 +49,6 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("wrap_device_ptr(int ptr, int[] shape, ScalarType dtype, int device_index) -> Tensor",
         &amd_dft::wrap_device_ptr);
   m.def("wrap_host_ptr(int ptr, int[] shape, ScalarType dtype) -> Tensor", &amd_dft::wrap_host_ptr);
+  m.def("fallback_counts() -> (str[], int[])", &amd_dft::fallback_counts);
+  m.def("fallback_reset() -> ()", &amd_dft::fallback_reset);
 }

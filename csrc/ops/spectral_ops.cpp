@@ -25,8 +25,10 @@ void check_afno(const at::Tensor& xw, const at::Tensor& w1t, const at::Tensor& w
   TORCH_CHECK(xw.dim() == 5 && xw.size(4) == 2 &&
                   (xw.scalar_type() == at::kFloat || xw.scalar_type() == at::kBFloat16),
               "afno_spectral: x must be [B, H, KM, C, 2] float32 or bfloat16");
+  TORCH_CHECK(w1t.dim() == 3, "afno_spectral: bad weight shapes");
   const int64_t NB = w1t.size(0), K = w1t.size(1);
-  TORCH_CHECK(w1t.dim() == 3 && w1t.size(2) == K && w2t.sizes() == w1t.sizes(), "afno_spectral: bad weight shapes");
+  TORCH_CHECK((w1t.size(2) == K || w1t.size(2) == 2 * K) && w2t.sizes() == w1t.sizes(),
+              "afno_spectral: weights must be [NB, 2BS, 2BS] (bf16) or split [NB, 2BS, 2*2BS] (bf16x3, fp32 path)");
   TORCH_CHECK(NB * K == 2 * xw.size(3), "afno_spectral: NB * 2 * block_size must equal 2 * C");
   TORCH_CHECK(b1.sizes() == at::IntArrayRef({NB, K}) && b2.sizes() == b1.sizes(), "afno_spectral: bad bias shapes");
 }
@@ -39,8 +41,13 @@ at::Tensor afno_spectral_cpu(const at::Tensor& xw, const at::Tensor& w1t, const 
   at::Tensor X = at::fft_fft(at::view_as_complex(xw.to(at::kFloat).contiguous()), std::nullopt, 1, "backward");
   at::Tensor Xr = at::view_as_real(X).reshape({B, H, KM, NB, BS, 2});
   at::Tensor A = at::cat({Xr.select(-1, 0), Xr.select(-1, 1)}, -1);  // [..., NB, 2BS]
-  at::Tensor W1 = w1t.to(at::kFloat).transpose(1, 2);                // [NB, k, n]
-  at::Tensor W2 = w2t.to(at::kFloat).transpose(1, 2);
+  auto unsplit = [&](const at::Tensor& w) {
+    if (w.size(2) == w.size(1)) return w.to(at::kFloat);
+    const int64_t k = w.size(1);
+    return w.narrow(2, 0, k).to(at::kFloat) + w.narrow(2, k, k).to(at::kFloat);
+  };
+  at::Tensor W1 = unsplit(w1t).transpose(1, 2);                      // [NB, k, n]
+  at::Tensor W2 = unsplit(w2t).transpose(1, 2);
   at::Tensor H1 = at::relu(at::einsum("...bk,bkn->...bn", {A, W1}) + b1);
   at::Tensor O = at::einsum("...bk,bkn->...bn", {H1, W2}) + b2;
   O = at::softshrink(O, lam);
@@ -59,10 +66,13 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   const int64_t B = xw.size(0), H = xw.size(1), KM = xw.size(2), C = xw.size(3), NB = w1t.size(0);
   TORCH_CHECK(afno_spectral_supported(static_cast<int>(H), static_cast<int>(C / NB)),
               "afno_spectral: fused kernel supports H == 90 and block size 96 (use the generic path)");
+  const bool x3 = w1t.size(2) == 2 * w1t.size(1);
+  TORCH_CHECK(!x3 || xw.scalar_type() == at::kFloat, "afno_spectral: split (bf16x3) weights go with a float32 spectrum");
   at::Tensor y = at::empty_like(xw);
   if (xw.numel() == 0) return y;
   auto dp = get_plan(H, xw.device());
   AfnoLaunch p;
+  p.x3 = x3 ? 1 : 0;
   p.x = xw.data_ptr();
   p.y = y.data_ptr();
   p.bf16_in = p.bf16_out = xw.scalar_type() == at::kBFloat16;
@@ -107,7 +117,10 @@ at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
                   w_.size(2) == x_.size(2),
               "fno_mix: x [B, Cin, M, 2], w [Cin, Cout, M, 2]");
   const int64_t B = x_.size(0), Cin = x_.size(1), M = x_.size(2), Cout = w_.size(1);
-  if (!fno_mix_fits(B, Cin, Cout)) return fno_mix_cpu(x_, w_);  // ATen on the device tensors
+  if (!fno_mix_fits(B, Cin, Cout)) {  // ATen on the device tensors
+    fallback_note("fno_mix", "operand tiles exceed the 160 KB LDS");
+    return fno_mix_cpu(x_, w_);
+  }
   at::Tensor x = x_.to(at::kFloat).contiguous(), w = w_.to(at::kFloat).contiguous();
   at::Tensor y = at::empty({B, Cout, M, 2}, x.options());
   FnoMixLaunch p;
@@ -277,7 +290,26 @@ std::tuple<at::Tensor, at::Tensor> layer_norm_cpu(const at::Tensor& x, const at:
 std::tuple<at::Tensor, at::Tensor> layer_norm_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& b_,
                                                    double eps, const std::optional<at::Tensor>& residual) {
   const c10::DeviceGuard guard(x_.device());
+  if (x_.scalar_type() == at::kFloat && !residual.has_value() && x_.size(-1) % 4 == 0 && x_.size(-1) <= 2048) {
+    at::Tensor x = x_.contiguous();
+    at::Tensor w = w_.to(at::kFloat).contiguous(), b = b_.to(at::kFloat).contiguous();
+    at::Tensor y = at::empty_like(x);
+    LayerNormLaunch p;
+    p.x = x.data_ptr();
+    p.y = y.data_ptr();
+    p.gamma = w.data_ptr();
+    p.beta = b.data_ptr();
+    p.residual = nullptr;
+    p.resid_out = nullptr;
+    p.cols = static_cast<int>(x.size(-1));
+    p.rows = x.numel() / p.cols;
+    p.eps = static_cast<float>(eps);
+    p.bf16 = 0;
+    if (p.rows > 0) launch_layernorm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return {y, x};
+  }
   if (x_.scalar_type() != at::kBFloat16 || x_.size(-1) % 8 != 0 || x_.size(-1) > 2048) {
+    fallback_note("layer_norm", "dtype/shape outside the LayerNorm kernels");
     return layer_norm_cpu(x_, w_, b_, eps, residual);  // ATen ops on the device tensors
   }
   at::Tensor x = x_.contiguous();
@@ -312,6 +344,55 @@ std::tuple<at::Tensor, at::Tensor> layer_norm_meta(const at::Tensor& x, const at
   return {at::empty_like(x), at::empty_like(x)};
 }
 
+// ------------------------------------------------------------------ fp32 LayerNorm -> bf16 split pairs
+// y = [..., 2C] = [hi | lo] of LN(x + pre): the A operand of the bf16x3 fc1 GEMM (fp32 path)
+at::Tensor layer_norm_split_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
+                                const std::optional<at::Tensor>& pre) {
+  at::Tensor xf = x.to(at::kFloat);
+  if (pre.has_value()) xf = xf + pre->to(at::kFloat);
+  at::Tensor y = at::layer_norm(xf, {x.size(-1)}, w.to(at::kFloat), b.to(at::kFloat), eps);
+  at::Tensor hi = y.to(at::kBFloat16);
+  return at::cat({hi, (y - hi.to(at::kFloat)).to(at::kBFloat16)}, -1).contiguous();
+}
+
+at::Tensor layer_norm_split_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& b_, double eps,
+                                 const std::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(x_.device());
+  const int64_t C = x_.size(-1);
+  TORCH_CHECK(x_.scalar_type() == at::kFloat && C % 4 == 0 && C <= 2048,
+              "amd_dft.layer_norm_split: x must be float32 with C % 4 == 0 and C <= 2048");
+  TORCH_CHECK(w_.numel() == C && b_.numel() == C && (!pre_.has_value() || pre_->numel() == C),
+              "amd_dft.layer_norm_split: weight/bias/pre must have C entries");
+  at::Tensor x = x_.contiguous();
+  at::Tensor w = w_.to(at::kFloat).contiguous(), b = b_.to(at::kFloat).contiguous(), pre;
+  if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = 2 * C;
+  at::Tensor y = at::empty(os, x.options().dtype(at::kBFloat16));
+  LayerNormLaunch p;
+  p.x = x.data_ptr();
+  p.y = y.data_ptr();
+  p.gamma = w.data_ptr();
+  p.beta = b.data_ptr();
+  p.residual = nullptr;
+  p.resid_out = nullptr;
+  p.cols = static_cast<int>(C);
+  p.rows = x.numel() / C;
+  p.eps = static_cast<float>(eps);
+  p.bf16 = 0;
+  p.split_out = 1;
+  p.pre = pre.defined() ? pre.data_ptr<float>() : nullptr;
+  if (p.rows > 0) launch_layernorm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor layer_norm_split_meta(const at::Tensor& x, const at::Tensor&, const at::Tensor&, double,
+                                 const std::optional<at::Tensor>&) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = 2 * os.back();
+  return at::empty(os, x.options().dtype(at::kBFloat16));
+}
+
 // ------------------------------------------------------------------ LayerNorm statistics only
 // (mean, rstd) per row of x' = x + pre: the AFNO W-transforms apply LN(x') on load.
 at::Tensor ln_stats_cpu(const at::Tensor& x, const std::optional<at::Tensor>& pre, double eps) {
@@ -325,7 +406,11 @@ at::Tensor ln_stats_cpu(const at::Tensor& x, const std::optional<at::Tensor>& pr
 at::Tensor ln_stats_cuda(const at::Tensor& x_, const std::optional<at::Tensor>& pre_, double eps) {
   const c10::DeviceGuard guard(x_.device());
   const int64_t C = x_.size(-1);
-  if (x_.scalar_type() != at::kBFloat16 || C % 8 != 0 || C > 2048) return ln_stats_cpu(x_, pre_, eps);
+  const bool f32 = x_.scalar_type() == at::kFloat && C % 4 == 0 && C <= 2048;
+  if (!f32 && (x_.scalar_type() != at::kBFloat16 || C % 8 != 0 || C > 2048)) {
+    fallback_note("ln_stats", "dtype/shape outside the LayerNorm kernels");
+    return ln_stats_cpu(x_, pre_, eps);
+  }
   at::Tensor x = x_.contiguous();
   at::Tensor pre;
   if (pre_.has_value()) {
@@ -341,6 +426,7 @@ at::Tensor ln_stats_cuda(const at::Tensor& x_, const std::optional<at::Tensor>& 
   p.rows = rows;
   p.cols = static_cast<int>(C);
   p.eps = static_cast<float>(eps);
+  p.f32 = f32 ? 1 : 0;
   if (rows > 0) launch_ln_stats(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
   return checked(st, "ln_stats");
 }
@@ -362,6 +448,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral_supported(int H, int block_size) -> bool", &amd_dft::afno_spectral_ok);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
+  m.def("layer_norm_split(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? pre=None) -> Tensor");
   m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
   m.def("fno_c2r_pw(Tensor yw, Tensor x, Tensor wc, Tensor? bias=None, bool gelu=True) -> Tensor");
@@ -371,6 +458,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cuda));
   m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cuda));
   m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cuda));
+  m.impl("layer_norm_split", AMD_DFT_TRACED("amd_dft::layer_norm_split", amd_dft::layer_norm_split_cuda));
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cuda));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cuda));
   m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cuda));
@@ -380,6 +468,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cpu));
   m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cpu));
   m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cpu));
+  m.impl("layer_norm_split", AMD_DFT_TRACED("amd_dft::layer_norm_split", amd_dft::layer_norm_split_cpu));
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cpu));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cpu));
   m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cpu));
@@ -389,6 +478,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_meta);
   m.impl("layer_norm", &amd_dft::layer_norm_meta);
   m.impl("ln_stats", &amd_dft::ln_stats_meta);
+  m.impl("layer_norm_split", &amd_dft::layer_norm_split_meta);
   m.impl("fno_mix", &amd_dft::fno_mix_meta);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);
   m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_meta);

@@ -1,4 +1,15 @@
+// amd_dft-build-flags: -O1
 // Fused AFNO spectral filter along H (FourCastNet AFNO2D, K5 in SURVEY §2.5).
+//
+// Built at -O1: at -O2/-O3 (hipcc, ROCm 7.2) both kernels of this file return wrong values
+// for a few workgroups of a launch, differently from launch to launch, but only when two or
+// more workgroups share a CU (bench grid B*KM*NB >> 256): e.g. rel-L2 2e-3 instead of 6e-6
+// for the bf16x3 kernel at B=2, KM=46, while every launch with <= 1 workgroup per CU (small
+// grids, or the LDS request padded to 1 per CU) is exact and deterministic.  The same source
+// at -O1 is exact at every grid (scripts/diag/afno_race_diag.py, profiles/afno_o1_fix_r2.txt).
+// The LDS images, index ranges and barriers were audited (no out-of-range access, every phase
+// barrier-separated; a standalone LDS-isolation test of co-resident workgroups is clean), so
+// the -O2 code generation is the suspect; the unit is kept at -O1 until that is isolated.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H (=90),
 // c < 96, complex fp32, produced by the W-direction R2C pass.  In one launch it runs
@@ -14,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -365,6 +377,253 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
   }
 }
 
+// ================================================================== fp32 variant (bf16x3)
+// Same structure for the fp32 FourCastNet path: fp32 spectrum in/out, fp32 LDS staging of the
+// H-FFT, and the two block-MLP GEMMs as 3-product split GEMMs -- an fp32 operand is the bf16
+// pair hi + lo and A.B = Ah.Bh + Al.Bh + Ah.Bl with fp32 accumulation (relative error ~5e-6,
+// the exact-f32 MFMA would cost 16x the bf16 rate, this 3x).  The A operand is split into two
+// bf16 planes [96][kAPitch] (hi, lo) when it is written to LDS; the weights arrive pre-split as
+// [NB][192 n][hi 192 k | lo 192 k].  76.8 KB of LDS: 2 workgroups per CU.
+constexpr int kK2 = 2 * kK;  // split weight row: [hi | lo]
+
+__device__ __forceinline__ void st_fp(float2* p, int i, const cpair& v) {
+  *reinterpret_cast<float4*>(p + i) = make_float4(v.re[0], v.im[0], v.re[1], v.im[1]);
+}
+__device__ __forceinline__ cpair ld_fp(const float2* p, int i) {
+  const float4 q = *reinterpret_cast<const float4*>(p + i);
+  return cpair{f2v{q.x, q.z}, f2v{q.y, q.w}};
+}
+__device__ __forceinline__ void put_split(uint16_t* Ahi, uint16_t* Alo, int idx, float v) {
+  const uint16_t h = f2bf16(v);
+  Ahi[idx] = h;
+  Alo[idx] = f2bf16(v - __uint_as_float(static_cast<uint32_t>(h) << 16));
+}
+__device__ __forceinline__ void put_split2(uint16_t* Ahi, uint16_t* Alo, int idx2, float a, float b) {
+  const uint16_t ha = f2bf16(a), hb = f2bf16(b);
+  reinterpret_cast<uint32_t*>(Ahi)[idx2] = static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16);
+  reinterpret_cast<uint32_t*>(Alo)[idx2] =
+      static_cast<uint32_t>(f2bf16(a - __uint_as_float(static_cast<uint32_t>(ha) << 16))) |
+      (static_cast<uint32_t>(f2bf16(b - __uint_as_float(static_cast<uint32_t>(hb) << 16))) << 16);
+}
+
+// [96 x 192] = (Ah + Al) x (Bh + Bl)^T without Al.Bl; wave w owns N-tiles 3w..3w+2
+__device__ __forceinline__ void gemm_96x192_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
+                                               const uint16_t* __restrict__ Bt, f32x4 (&acc)[6][3]) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bh[2][3], bl[2][3];
+#pragma unroll
+  for (int nj = 0; nj < 3; ++nj) {
+    const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + kq * 8;
+    bh[0][nj] = *reinterpret_cast<const bf16x8*>(row);
+    bl[0][nj] = *reinterpret_cast<const bf16x8*>(row + kK);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 6; ++ks) {
+    if (ks + 1 < 6) {
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj) {
+        const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + (ks + 1) * 32 + kq * 8;
+        bh[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row);
+        bl[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row + kK);
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi) {
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ah + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Al + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
+#pragma unroll
+      for (int nj = 0; nj < 3; ++nj) {
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks & 1][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
+      }
+    }
+  }
+}
+
+constexpr int kX3Plane = kBS * kAPitch;  // bf16 elements per A plane
+
+template <int L, int R0, int R1>
+__global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs a) {
+  static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
+  extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][96] complex fp32 (69 KB at L=90)
+  uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [96][kAPitch] bf16 hi
+  uint16_t* Al = Ah + kX3Plane;                                  //          [96][kAPitch] bf16 lo
+  const int tid = threadIdx.x;
+  const int blk = blockIdx.x % a.NB;
+  const int bk = blockIdx.x / a.NB;
+  const int kw = bk % a.KM;
+  const int b = bk / a.KM;
+  AMD_DFT_DEV_CHECK((blk + 1) * kBS <= a.C && kw < a.KM && L == a.H, "afno_spectral_x3_kernel");
+  const int row_stride = a.KM * a.C * 2;
+  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
+  const float* xin = static_cast<const float*>(a.x) + base;
+  float* yout = static_cast<float*>(a.y) + base;
+  using P0 = HPass<R0, L>;
+  using P1 = HPass<R1, L>;
+  // ---------------- forward FFT_H: pass 0 straight from global
+  {
+    cpair v[P0::Q][R0];
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
+      const int bc = ok ? bb : 0;
+      const int tp = bc % kNP, j = bc / kNP;
+#pragma unroll
+      for (int r = 0; r < R0; ++r) {
+        float2 c0, c1;
+        ldc2<false>(xin, (j + r * P0::LR) * row_stride + 4 * tp, c0, c1);
+        v[q][r] = make_cpair(c0, c1);
+      }
+    }
+    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> A planes ([h][re 0..95 | im 96..191], hi / lo)
+  {
+    cpair v[P1::Q][R1];
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * kBS + 2 * tp);
+      }
+    }
+    __syncthreads();
+    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          const int n = j + r * R0;
+          put_split2(Ah, Al, (n * kAPitch) / 2 + tp, v[q][r].re[0], v[q][r].re[1]);
+          put_split2(Ah, Al, (n * kAPitch) / 2 + kNP + tp, v[q][r].im[0], v[q][r].im[1]);
+        }
+      }
+    }
+  }
+  // rows L..95 of A (GEMM M padding) are never written: their outputs are discarded
+  __syncthreads();
+  const int lane = tid & 63, w = tid >> 6;
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * kK * kK2;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * kK * kK2;
+  const float* b1 = a.b1 + blk * kK;
+  const float* b2 = a.b2 + blk * kK;
+  f32x4 acc[6][3];
+  gemm_96x192_x3(Ah, Al, w1t, acc);
+  __syncthreads();
+#pragma unroll
+  for (int nj = 0; nj < 3; ++nj) {
+    const int n = (3 * w + nj) * 16 + (lane & 15);
+    const float bias = b1[n];
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mi * 16 + 4 * (lane >> 4) + i;
+        put_split(Ah, Al, m * kAPitch + n, fmaxf(acc[mi][nj][i] + bias, 0.f));
+      }
+  }
+  __syncthreads();
+  gemm_96x192_x3(Ah, Al, w2t, acc);
+  __syncthreads();
+  float* X = reinterpret_cast<float*>(ldsf);
+  const float lam = a.lambda;
+#pragma unroll
+  for (int nj = 0; nj < 3; ++nj) {
+    const int n = (3 * w + nj) * 16 + (lane & 15);
+    const float bias = b2[n];
+    const int c = n < kBS ? n : n - kBS;
+    const int part = n < kBS ? 0 : 1;
+    const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
+#pragma unroll
+    for (int mi = 0; mi < 6; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mi * 16 + 4 * (lane >> 4) + i;
+        if (m < L) {
+          const float v = acc[mi][nj][i] + bias;
+          const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
+          X[(m * kBS + c) * 2 + part] = sgn * s;
+        }
+      }
+  }
+  __syncthreads();
+  // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
+  {
+    cpair v[P0::Q][R0];
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp(ldsf, (j + r * P0::LR) * kBS + 2 * tp);
+      }
+    }
+    __syncthreads();
+    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P0::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> global (conj back)
+  {
+    cpair v[P1::Q][R1];
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * kBS + 2 * tp);
+      }
+    }
+    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % kNP, j = bb / kNP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          const int n = j + r * R0;
+          stc2<false>(yout, n * row_stride + 4 * tp, make_float2(v[q][r].re[0], -v[q][r].im[0]),
+                      make_float2(v[q][r].re[1], -v[q][r].im[1]));
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 bool afno_spectral_supported(int H, int block_size) { return H == 90 && block_size == kBS; }
@@ -394,7 +653,20 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   a.lambda = p.lambda;
   const int64_t nblocks = static_cast<int64_t>(p.B) * p.KM * p.NB;
   if (nblocks <= 0) return;
-  const size_t lds = static_cast<size_t>(afno_spectral_lds_bytes(p.H));
+  if (p.x3) {
+    if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
+    const int64_t staging = static_cast<int64_t>(p.H) * kBS * 8, planes = 2LL * kX3Plane * 2;
+    size_t lds = static_cast<size_t>(staging > planes ? staging : planes);
+    auto kern = afno_spectral_x3_kernel<90, 9, 10>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(lds));
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), lds, static_cast<hipStream_t>(stream), a);
+    e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral launch: ") + hipGetErrorString(e));
+    return;
+  }
+  size_t lds = static_cast<size_t>(afno_spectral_lds_bytes(p.H));
   auto kern = p.bf16_in ? (p.bf16_out ? afno_spectral_kernel<90, 9, 10, true, true> : afno_spectral_kernel<90, 9, 10, true, false>)
                         : (p.bf16_out ? afno_spectral_kernel<90, 9, 10, false, true> : afno_spectral_kernel<90, 9, 10, false, false>);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -16,6 +16,9 @@
 //    stream straight from registers to global;
 //  * the C2R input is the pruned half spectrum: which of the 12 pass-0 inputs can be non-zero
 //    is resolved at compile time from KM (6 of 12 loads at KM = 46), the rest are constants.
+//  * fp32 instantiation (F32, the fp32 FourCastNet path): fp32 residual stream and spectrum,
+//    fp32 LDS staging, addends loaded to registers (the bf16 LDS image of the x tile would not
+//    fit beside an fp32 staging buffer at 3 workgroups per CU).
 // Reference: the AFNO filter runs rfft2/irfft2 on the whole [B, C, H, W] tensor after a
 // separate LayerNorm kernel (FourCastNet AFNO2D; this repo's SURVEY.md §2.5 K5/K1e).
 #include <hip/hip_runtime.h>
@@ -23,6 +26,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include "../fft/dev_check.h"
 #include "../fft/radix.h"
@@ -71,13 +75,13 @@ __device__ __forceinline__ uint32_t bfpack(float a, float b) {
 }
 
 struct WArgs {
-  const uint16_t* x;     // [O, 180, C] bf16 (stored residual stream)
+  const void* x;         // [O, 180, C] bf16 / fp32 (stored residual stream)
   const float2* stats;   // [O, 180] (mean, rstd) of x'
   const float* gamma;    // [C]
   const float* beta;     // [C]
   const float* pre;      // [C] or nullptr
-  const uint16_t* spec;  // C2R input [O, KM, C, 2] bf16
-  uint16_t* out;         // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
+  const void* spec;      // C2R input [O, KM, C, 2] bf16 / fp32
+  void* out;             // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
   int C, nslab;
   float scale;
 };
@@ -99,6 +103,32 @@ __device__ __forceinline__ void load_params(const WArgs& a, int c0, ChanParams& 
 __device__ __forceinline__ void ln4(const uint2 raw, const float2 st, const ChanParams& cp, float (&xp)[kCh],
                                     float (&h)[kCh]) {
   unpack4(raw, xp);
+#pragma unroll
+  for (int i = 0; i < kCh; ++i) {
+    xp[i] += cp.p[i];
+    h[i] = (xp[i] - st.x) * st.y * cp.g[i] + cp.b[i];
+  }
+}
+
+// 4 consecutive channels of one token, bf16 (8 bytes) or fp32 (16 bytes); off in elements
+template <bool F32>
+__device__ __forceinline__ void ldx4(const void* base, int64_t off, float (&f)[4]) {
+  if constexpr (F32) {
+    const float4 q = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+    f[0] = q.x; f[1] = q.y; f[2] = q.z; f[3] = q.w;
+  } else {
+    unpack4(*reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(base) + off), f);
+  }
+}
+template <bool F32>
+__device__ __forceinline__ void stx4(void* base, int64_t off, float a, float b, float c, float d) {
+  if constexpr (F32) {
+    *reinterpret_cast<float4*>(static_cast<float*>(base) + off) = make_float4(a, b, c, d);
+  } else {
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(base) + off) = make_uint2(bfpack(a, b), bfpack(c, d));
+  }
+}
+__device__ __forceinline__ void ln4f(float (&xp)[kCh], const float2 st, const ChanParams& cp, float (&h)[kCh]) {
 #pragma unroll
   for (int i = 0; i < kCh; ++i) {
     xp[i] += cp.p[i];
@@ -151,25 +181,29 @@ __device__ __forceinline__ void pass1(int k1, int g, const T* lds, cpair (&u)[kB
   Dft<kB>::run(u);
 }
 
-template <int KM>
+template <int KM, bool F32>
 __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) {
-  // fp16 staging (the output is bf16): 24.5 KB -> 6 workgroups per CU
-  __shared__ __attribute__((aligned(16))) h2_t lds[kL * kPitch];
+  // bf16 output: fp16 staging (24.5 KB -> 6 workgroups per CU); fp32: fp32 staging (49 KB)
+  using ST = typename std::conditional<F32, float2, h2_t>::type;
+  __shared__ __attribute__((aligned(16))) ST lds[kL * kPitch];
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
   AMD_DFT_DEV_CHECK((slab + 1) * kSlab <= a.C, "afno_w_kernel");
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
   // workgroup-uniform bases + 32-bit lane offsets (SGPR base + VGPR offset addressing)
-  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const int64_t xbase = static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const void* xb = F32 ? static_cast<const void*>(static_cast<const float*>(a.x) + xbase)
+                       : static_cast<const void*>(static_cast<const uint16_t*>(a.x) + xbase);
   const float2* st = a.stats + static_cast<int64_t>(o) * kL;
   const int lo = n2 * C + kCh * g;
   // ---- pass 0: n = n2 + 15 n1 straight from global, LayerNorm on load
-  uint2 raw[kA];
+  using Raw = typename std::conditional<F32, float4, uint2>::type;  // raw until use (bf16: 2 VGPRs)
+  Raw raw[kA];
   float2 sv[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
-    raw[n1] = *reinterpret_cast<const uint2*>(xb + lo + kB * n1 * C);
+    raw[n1] = *(reinterpret_cast<const Raw*>(static_cast<const char*>(xb) + static_cast<int64_t>(lo + kB * n1 * C) * (F32 ? 4 : 2)));
     sv[n1] = st[n2 + kB * n1];
   }
   ChanParams cp;
@@ -177,8 +211,13 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
   cpair v[kA];  // the lane's two packed channel pairs (h0 + i h1, h2 + i h3) as one cpair
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
-    float xp[kCh], h[kCh];
-    ln4(raw[n1], sv[n1], cp, xp, h);
+    float xr[kCh], h[kCh];
+    if constexpr (F32) {
+      xr[0] = raw[n1].x; xr[1] = raw[n1].y; xr[2] = raw[n1].z; xr[3] = raw[n1].w;
+    } else {
+      unpack4(raw[n1], xr);
+    }
+    ln4f(xr, sv[n1], cp, h);
     v[n1] = cpair{f2v{h[0], h[2]}, f2v{h[1], h[3]}};
   }
   pass0_store(v, n2, g, lds);
@@ -195,7 +234,7 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
   __syncthreads();
   // ---- separate the packed pairs: X_a[k] = (Z[k] + conj Z[L-k]) / 2, X_b[k] = (Z[k] - conj Z[L-k]) / 2i
   const float hs = 0.5f * a.scale;
-  uint16_t* ob = a.out + (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
+  const int64_t obase = (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
   constexpr int kItems = KM * kG;
 #pragma unroll
   for (int it = 0; it < (kItems + kThreads - 1) / kThreads; ++it) {
@@ -206,16 +245,23 @@ __global__ void __launch_bounds__(kThreads) afno_w_r2c_ln_kernel(const WArgs a) 
     float2 Zk[2], Zm[2];
     ld_pair(lds, k * kPitch + kPPL * gg, Zk[0], Zk[1]);
     ld_pair(lds, km * kPitch + kPPL * gg, Zm[0], Zm[1]);
-    uint32_t w[4];
+    float w[8];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
-      const float2 xa = make_float2((Zk[p].x + Zm[p].x) * hs, (Zk[p].y - Zm[p].y) * hs);
-      const float2 xb = make_float2((Zk[p].y + Zm[p].y) * hs, (Zm[p].x - Zk[p].x) * hs);
-      w[2 * p] = bfpack(xa.x, xa.y);
-      w[2 * p + 1] = bfpack(xb.x, xb.y);
+      w[4 * p + 0] = (Zk[p].x + Zm[p].x) * hs;
+      w[4 * p + 1] = (Zk[p].y - Zm[p].y) * hs;
+      w[4 * p + 2] = (Zk[p].y + Zm[p].y) * hs;
+      w[4 * p + 3] = (Zm[p].x - Zk[p].x) * hs;
     }
-    *reinterpret_cast<uint4*>(ob + (k * C + kCh * gg) * 2) =
-        make_uint4(w[0], w[1], w[2], w[3]);
+    const int64_t off = obase + (k * C + kCh * gg) * 2;
+    if constexpr (F32) {
+      float* op = static_cast<float*>(a.out) + off;
+      *reinterpret_cast<float4*>(op) = make_float4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<float4*>(op + 4) = make_float4(w[4], w[5], w[6], w[7]);
+    } else {
+      *reinterpret_cast<uint4*>(static_cast<uint16_t*>(a.out) + off) =
+          make_uint4(bfpack(w[0], w[1]), bfpack(w[2], w[3]), bfpack(w[4], w[5]), bfpack(w[6], w[7]));
+    }
   }
 }
 
@@ -231,31 +277,34 @@ constexpr int c2r_load_kind(int n1) {
   return all ? 1 : (any ? 2 : 0);
 }
 
-template <int KM>
+template <int KM, bool F32>
 __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
-#if AFNO_C2R_XLDS
-  // fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its LN
-  // statistics: 49.6 KB -> still 3 workgroups per CU, and the addends need no VGPRs
-  __shared__ __attribute__((aligned(16))) h2_t lds[kL * kPitch];
-  __shared__ __attribute__((aligned(16))) char dimg[kRounds * kRound];  // x tile + stats (26.9 KB)
-  const uint2* xt = reinterpret_cast<const uint2*>(dimg);                 // [pos][16 lanes x 4 ch] bf16
-  const float2* stl = reinterpret_cast<const float2*>(dimg + kXBytes);    // [pos] (mean, rstd)
-#else
-  __shared__ __attribute__((aligned(16))) float2 lds[kL * kPitch];
-#endif
+  // bf16 (XLDS): fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its
+  // LN statistics: 49.6 KB -> still 3 workgroups per CU, and the addends need no VGPRs.
+  // fp32: fp32 staging (49 KB), addends loaded to registers.
+  constexpr bool XLDS = AFNO_C2R_XLDS && !F32;
+  using ST = typename std::conditional<XLDS, h2_t, float2>::type;
+  constexpr int kStageBytes = kL * kPitch * static_cast<int>(sizeof(ST));
+  constexpr int kImgBytes = XLDS ? kRounds * kRound : 0;
+  __shared__ __attribute__((aligned(16))) char smem[kStageBytes + kImgBytes];
+  ST* lds = reinterpret_cast<ST*>(smem);
+  char* dimg = smem + kStageBytes;
+  const uint2* xt = reinterpret_cast<const uint2*>(dimg);               // [pos][16 lanes x 4 ch] bf16
+  const float2* stl = reinterpret_cast<const float2*>(dimg + kXBytes);  // [pos] (mean, rstd)
   const int o = blockIdx.x / a.nslab, slab = blockIdx.x - o * a.nslab;
   AMD_DFT_DEV_CHECK((slab + 1) * kSlab <= a.C, "afno_w_kernel");
   const int g = threadIdx.x % kG, n2 = threadIdx.x / kG;
   const int c0 = slab * kSlab + kCh * g;
   const int C = a.C;
-  const uint16_t* sb = a.spec + (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
-  const uint16_t* xb = a.x + static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const int64_t sbase = (static_cast<int64_t>(o) * KM * C + slab * kSlab) * 2;
+  const int64_t xbase = static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const void* xb = F32 ? static_cast<const void*>(static_cast<const float*>(a.x) + xbase)
+                       : static_cast<const void*>(static_cast<const uint16_t*>(a.x) + xbase);
   const float2* st = a.stats + static_cast<int64_t>(o) * kL;
-#if AFNO_C2R_XLDS
-  {
+  if constexpr (XLDS) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const char* xbc = reinterpret_cast<const char*>(xb);
+    const char* xbc = static_cast<const char*>(xb);
     const char* stc = reinterpret_cast<const char*>(st);
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
@@ -267,21 +316,21 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
                                        (lds_void*)(dimg + r * kRound + wave * 1024), 16, 0, 0);
     }
   }
-#endif
   // ---- pass 0: Hermitian assembly of the packed pair spectrum Z = X_a + i X_b, conjugated
   // (inverse transform as conj(FFT(conj Z))); only the stored modes are loaded
-  uint4 raw[kA];
+  struct F8 { float4 a, b; };
+  using Raw = typename std::conditional<F32, F8, uint4>::type;  // raw until use (bf16: 4 VGPRs)
+  Raw raw[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
     if (c2r_load_kind<KM>(n1) != 0) {
       const int n = n2 + kB * n1;
       const int kk = 2 * n > kL ? kL - n : n;
       const int kc = kk < KM ? kk : 0;  // clamped: unconditional load, masked below
-      raw[n1] = *reinterpret_cast<const uint4*>(sb + (kc * C + kCh * g) * 2);
+      const int64_t off = sbase + (kc * C + kCh * g) * 2;
+      raw[n1] = *reinterpret_cast<const Raw*>(static_cast<const char*>(a.spec) + off * (F32 ? 4 : 2));
     }
   }
-#if AFNO_C2R_XLDS
-#endif
   cpair v[kA];
 #pragma unroll
   for (int n1 = 0; n1 < kA; ++n1) {
@@ -295,8 +344,13 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     const int kk = upper ? kL - n : n;
     const bool ok = kind == 1 || kk < KM;
     float f[8];
-    unpack4(make_uint2(raw[n1].x, raw[n1].y), *reinterpret_cast<float(*)[4]>(f));
-    unpack4(make_uint2(raw[n1].z, raw[n1].w), *reinterpret_cast<float(*)[4]>(f + 4));
+    if constexpr (F32) {
+      f[0] = raw[n1].a.x; f[1] = raw[n1].a.y; f[2] = raw[n1].a.z; f[3] = raw[n1].a.w;
+      f[4] = raw[n1].b.x; f[5] = raw[n1].b.y; f[6] = raw[n1].b.z; f[7] = raw[n1].b.w;
+    } else {
+      unpack4(make_uint2(raw[n1].x, raw[n1].y), *reinterpret_cast<float(*)[4]>(f));
+      unpack4(make_uint2(raw[n1].z, raw[n1].w), *reinterpret_cast<float(*)[4]>(f + 4));
+    }
     float2 zp[kPPL];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
@@ -317,9 +371,7 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     v[n1] = make_cpair(zp[0], zp[1]);
   }
   pass0_store(v, n2, g, lds);
-#if AFNO_C2R_XLDS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS DMA landed before the barrier publishes it
-#endif
+  if constexpr (XLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS DMA landed before the barrier publishes it
   __syncthreads();
   const int k1 = n2;
   if (k1 >= kA) return;
@@ -335,52 +387,55 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
   }
   __builtin_amdgcn_sched_barrier(0);
   const int lo = k1 * C + kCh * g;  // 32-bit lane offset from the workgroup-uniform base
-#if !AFNO_C2R_XLDS
-  uint2 xraw[kB];
-  float2 sv[kB];
+  float xr[XLDS ? 1 : kB][kCh];
+  float2 sv[XLDS ? 1 : kB];
+  if constexpr (!XLDS) {
 #pragma unroll
-  for (int k2 = 0; k2 < kB; ++k2) {
-    xraw[k2] = *reinterpret_cast<const uint2*>(xb + lo + kA * k2 * C);
-    sv[k2] = st[k1 + kA * k2];
+    for (int k2 = 0; k2 < kB; ++k2) {
+      ldx4<F32>(xb, lo + kA * k2 * C, xr[k2]);
+      sv[k2] = st[k1 + kA * k2];
+    }
   }
-#endif
   ChanParams cp;
   load_params(a, c0, cp);
   __builtin_amdgcn_sched_barrier(0);
   Dft<kB>::run(u);
   __builtin_amdgcn_sched_barrier(0);
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
-  uint16_t* ob = a.out + static_cast<int64_t>(o) * kL * C + slab * kSlab;
+  const int64_t obase = xbase;
+  void* ob = F32 ? static_cast<void*>(static_cast<float*>(a.out) + obase)
+                 : static_cast<void*>(static_cast<uint16_t*>(a.out) + obase);
   const float sc = a.scale;
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
     float xp[kCh], h[kCh];
-#if AFNO_C2R_XLDS
-    const int n = k1 + kA * k2;
-    ln4(xt[n * kG + g], stl[n], cp, xp, h);
-#else
-    ln4(xraw[k2], sv[k2], cp, xp, h);
-#endif
-    uint32_t w[kPPL];
+    if constexpr (XLDS) {
+      const int n = k1 + kA * k2;
+      ln4(xt[n * kG + g], stl[n], cp, xp, h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < kCh; ++i) xp[i] = xr[k2][i];
+      ln4f(xp, sv[k2], cp, h);
+    }
+    float y[kCh];
 #pragma unroll
     for (int p = 0; p < kPPL; ++p) {
-      const float ya = u[k2].re[p] * sc + xp[2 * p] + h[2 * p];
-      const float yb = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
-      w[p] = bfpack(ya, yb);
+      y[2 * p] = u[k2].re[p] * sc + xp[2 * p] + h[2 * p];
+      y[2 * p + 1] = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
     }
-    *reinterpret_cast<uint2*>(ob + lo + kA * k2 * C) = make_uint2(w[0], w[1]);
+    stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
   }
 }
 
 WArgs make_args(const AfnoWLaunch& p) {
   WArgs a;
-  a.x = static_cast<const uint16_t*>(p.x);
+  a.x = p.x;
   a.stats = reinterpret_cast<const float2*>(p.stats);
   a.gamma = p.gamma;
   a.beta = p.beta;
   a.pre = p.pre;
-  a.spec = static_cast<const uint16_t*>(p.spec);
-  a.out = static_cast<uint16_t*>(p.out);
+  a.spec = p.spec;
+  a.out = p.out;
   a.C = p.C;
   a.nslab = p.C / kSlab;
   a.scale = p.scale;
@@ -402,7 +457,8 @@ void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream) {
   check_launch(p, "afno_w_r2c_ln");
   const WArgs a = make_args(p);
   const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
-  hipLaunchKernelGGL(afno_w_r2c_ln_kernel<46>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  if (p.f32) hipLaunchKernelGGL((afno_w_r2c_ln_kernel<46, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  else hipLaunchKernelGGL((afno_w_r2c_ln_kernel<46, false>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_w_r2c_ln launch: ") + hipGetErrorString(e));
 }
@@ -411,7 +467,8 @@ void launch_afno_w_c2r_ln(const AfnoWLaunch& p, void* stream) {
   check_launch(p, "afno_w_c2r_ln");
   const WArgs a = make_args(p);
   const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
-  hipLaunchKernelGGL(afno_w_c2r_ln_kernel<46>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  if (p.f32) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  else hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, false>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_w_c2r_ln launch: ") + hipGetErrorString(e));
 }

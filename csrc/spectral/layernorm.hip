@@ -230,9 +230,129 @@ void launch_stats_n(const LnStatsLaunch& p, hipStream_t st) {
                        p.eps);
 }
 
+// ---- fp32 rows (the fp32 FourCastNet path): one wave per row, 16-byte loads, NCH float4
+// chunks per lane.  STATS: write (mean, rstd) only.  Otherwise y = LN(x + pre) either as fp32
+// or (SPLIT) as a bf16 pair row [hi(cols) | lo(cols)], the operand of the bf16x3 GEMM.
+__device__ __forceinline__ uint32_t bfpack_lo(float a, float b, uint32_t hi) {
+  const float ha = __uint_as_float(hi << 16), hb = __uint_as_float(hi & 0xffff0000u);
+  return bfpack(a - ha, b - hb);
+}
+
+template <int NCH, bool STATS, bool SPLIT, bool PRE>
+__global__ void __launch_bounds__(64 * kWaves) ln_f32_kernel(const float* __restrict__ x, const float* __restrict__ pre,
+                                                             const float* __restrict__ g, const float* __restrict__ b,
+                                                             void* __restrict__ y, float2* __restrict__ st,
+                                                             int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nchunk = cols >> 2;
+  const float* xr = x + row * cols;
+  float v[NCH][4];
+  bool ok[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int ch = lane + 64 * c;
+    ok[c] = ch < nchunk;
+    const int chc = ok[c] ? ch : 0;
+    const float4 q = *reinterpret_cast<const float4*>(xr + chc * 4);
+    v[c][0] = q.x; v[c][1] = q.y; v[c][2] = q.z; v[c][3] = q.w;
+    if constexpr (PRE) {
+      const float4 pp = *reinterpret_cast<const float4*>(pre + chc * 4);
+      v[c][0] += pp.x; v[c][1] += pp.y; v[c][2] += pp.z; v[c][3] += pp.w;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += ok[c] ? v[c][i] : 0.f;
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = v[c][i] - mean;
+      q += ok[c] ? d * d : 0.f;
+    }
+  const float rstd = rsqrtf(wave_sum(q) / cols + eps);
+  if constexpr (STATS) {
+    if (lane == 0) st[row] = make_float2(mean, rstd);
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!ok[c]) continue;
+    const int ch = lane + 64 * c;
+    const float4 g4 = *reinterpret_cast<const float4*>(g + ch * 4);
+    const float4 b4 = *reinterpret_cast<const float4*>(b + ch * 4);
+    float o[4];
+    o[0] = (v[c][0] - mean) * rstd * g4.x + b4.x;
+    o[1] = (v[c][1] - mean) * rstd * g4.y + b4.y;
+    o[2] = (v[c][2] - mean) * rstd * g4.z + b4.z;
+    o[3] = (v[c][3] - mean) * rstd * g4.w + b4.w;
+    if constexpr (SPLIT) {
+      uint16_t* yr = static_cast<uint16_t*>(y) + row * (2 * cols);
+      const uint32_t h0 = bfpack(o[0], o[1]), h1 = bfpack(o[2], o[3]);
+      *reinterpret_cast<uint2*>(yr + ch * 4) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(yr + cols + ch * 4) = make_uint2(bfpack_lo(o[0], o[1], h0), bfpack_lo(o[2], o[3], h1));
+    } else {
+      *reinterpret_cast<float4*>(static_cast<float*>(y) + row * cols + ch * 4) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+template <bool STATS, bool SPLIT>
+void launch_f32(const float* x, const float* pre, const float* g, const float* b, void* y, float2* st, int64_t rows,
+                int cols, float eps, hipStream_t s) {
+  const dim3 grid(static_cast<uint32_t>((rows + kWaves - 1) / kWaves)), blk(64 * kWaves);
+  const int nch = (cols / 4 + 63) / 64;
+#define AMD_DFT_LNF(N)                                                                                       \
+  if (pre) hipLaunchKernelGGL((ln_f32_kernel<N, STATS, SPLIT, true>), grid, blk, 0, s, x, pre, g, b, y, st, rows, cols, eps); \
+  else hipLaunchKernelGGL((ln_f32_kernel<N, STATS, SPLIT, false>), grid, blk, 0, s, x, pre, g, b, y, st, rows, cols, eps);
+  if (nch <= 1) { AMD_DFT_LNF(1) }
+  else if (nch == 2) { AMD_DFT_LNF(2) }
+  else if (nch == 3) { AMD_DFT_LNF(3) }
+  else if (nch <= 4) { AMD_DFT_LNF(4) }
+  else { AMD_DFT_LNF(8) }
+#undef AMD_DFT_LNF
+}
+
+// ---- fp32 -> bf16 split pairs (hi = bf16(x), lo = bf16(x - hi)), 8 elements per thread.
+// ROWS: row-major [rows, cols] -> [rows, 2 cols] rows [hi | lo]; else planes [2, n] (hi, lo).
+template <bool ROWS>
+__global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                         int64_t n, int cols) {
+  const int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  const float4 a = *reinterpret_cast<const float4*>(x + i);
+  const float4 c = *reinterpret_cast<const float4*>(x + i + 4);
+  const uint32_t h0 = bfpack(a.x, a.y), h1 = bfpack(a.z, a.w), h2 = bfpack(c.x, c.y), h3 = bfpack(c.z, c.w);
+  const uint4 hi = make_uint4(h0, h1, h2, h3);
+  const uint4 lo = make_uint4(bfpack_lo(a.x, a.y, h0), bfpack_lo(a.z, a.w, h1), bfpack_lo(c.x, c.y, h2),
+                              bfpack_lo(c.z, c.w, h3));
+  if constexpr (ROWS) {
+    const int64_t r = i / cols, col = i - r * cols;
+    *reinterpret_cast<uint4*>(y + r * 2 * cols + col) = hi;
+    *reinterpret_cast<uint4*>(y + r * 2 * cols + cols + col) = lo;
+  } else {
+    *reinterpret_cast<uint4*>(y + i) = hi;
+    *reinterpret_cast<uint4*>(y + n + i) = lo;
+  }
+}
+
 }  // namespace
 
 void launch_ln_stats(const LnStatsLaunch& p, void* stream) {
+  if (p.f32) {
+    if (p.cols % 4 != 0 || p.cols > 64 * 4 * 8) throw std::runtime_error("amd_dft: ln_stats: fp32 rows need cols % 4 == 0, <= 2048");
+    launch_f32<true, false>(static_cast<const float*>(p.x), p.pre, nullptr, nullptr, nullptr,
+                            reinterpret_cast<float2*>(p.stats), p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ln_stats launch: ") + hipGetErrorString(e));
+    return;
+  }
   if (p.cols % 8 != 0 || p.cols > 64 * 8 * 4)
     throw std::runtime_error("amd_dft: ln_stats kernel supports bf16 rows with cols % 8 == 0 and cols <= 2048");
   if (p.rows > static_cast<int64_t>(0x7fffffff) * kWaves) throw std::runtime_error("amd_dft: ln_stats: too many rows");
@@ -254,6 +374,18 @@ void launch_ln_stats(const LnStatsLaunch& p, void* stream) {
 }
 
 void launch_layernorm(const LayerNormLaunch& p, void* stream) {
+  if (!p.bf16) {
+    if (p.residual || p.cols % 4 != 0 || p.cols > 64 * 4 * 8)
+      throw std::runtime_error("amd_dft: layernorm: fp32 rows need cols % 4 == 0, <= 2048, no residual");
+    const auto* x = static_cast<const float*>(p.x);
+    const auto* g = static_cast<const float*>(p.gamma);
+    const auto* b = static_cast<const float*>(p.beta);
+    if (p.split_out) launch_f32<false, true>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
+    else launch_f32<false, false>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: layernorm launch: ") + hipGetErrorString(e));
+    return;
+  }
   if (!p.bf16 || p.cols % 8 != 0 || p.cols > 64 * 8 * 4)
     throw std::runtime_error("amd_dft: layernorm kernel supports bf16 rows with cols % 8 == 0 and cols <= 2048");
   if (p.rows > static_cast<int64_t>(0x7fffffff) * kWaves) throw std::runtime_error("amd_dft: layernorm: too many rows");
@@ -264,6 +396,16 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
   else launch_bf16<4>(p, st);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: layernorm launch: ") + hipGetErrorString(e));
+}
+
+void launch_split_bf16(const float* x, uint16_t* y, int64_t n, int cols, bool rows, void* stream) {
+  if (n % 8 != 0 || (rows && cols % 8 != 0)) throw std::runtime_error("amd_dft: split_bf16: needs 8-element multiples");
+  if (n == 0) return;
+  const dim3 grid(static_cast<uint32_t>((n / 8 + 255) / 256));
+  if (rows) hipLaunchKernelGGL(split_bf16_kernel<true>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), x, y, n, cols);
+  else hipLaunchKernelGGL(split_bf16_kernel<false>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), x, y, n, cols);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: split_bf16 launch: ") + hipGetErrorString(e));
 }
 
 }  // namespace amd_dft

@@ -10,6 +10,7 @@ struct AfnoLaunch {
   const void* x;        // [B, H, KM, C, 2] fp32/bf16 (W-direction half spectrum, KM kept modes)
   void* y;              // same shape (fp32/bf16)
   int bf16_in = 0, bf16_out = 0;
+  int x3 = 0;           // fp32 bf16x3 variant: fp32 in/out, weights [NB][2*BS][hi 2*BS | lo 2*BS]
   const uint16_t* w1t;  // [NB][2*BS][2*BS] bf16, real-block weight transposed ([n][k])
   const uint16_t* w2t;
   const float* b1;      // [NB][2*BS] = [b_re | b_im]
@@ -55,13 +56,15 @@ struct LayerNormLaunch {
   int64_t rows;
   int cols;
   float eps;
-  int bf16;  // 1: bf16 tensors, 0: fp32
+  int bf16;  // 1: bf16 tensors, 0: fp32 (gamma/beta fp32)
+  int split_out = 0;           // fp32 only: y = [rows, 2 cols] bf16 pair rows [hi | lo]
+  const float* pre = nullptr;  // fp32 only: per-channel addend applied before the statistics
 };
 void launch_layernorm(const LayerNormLaunch& p, void* stream);
 
 // ---- AFNO W-direction transforms with LayerNorm fused into the IO (afno_wfft.hip)
 struct AfnoWLaunch {
-  const void* x = nullptr;        // [O, L, C] bf16 stored residual stream
+  const void* x = nullptr;        // [O, L, C] bf16 (fp32 if f32) stored residual stream
   const float* stats = nullptr;   // [O, L, 2] (mean, rstd) of x + pre
   const float* gamma = nullptr;   // [C] fp32
   const float* beta = nullptr;    // [C] fp32
@@ -70,6 +73,7 @@ struct AfnoWLaunch {
   void* out = nullptr;            // R2C: [O, KM, C, 2] bf16; C2R: [O, L, C] bf16
   int O = 0, L = 0, C = 0, KM = 0;
   float scale = 1.f;
+  int f32 = 0;                    // fp32 residual stream, spectrum and output
 };
 bool afno_w_supported(int L, int C, int KM);
 void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream);
@@ -83,7 +87,12 @@ struct LnStatsLaunch {
   int64_t rows;
   int cols;
   float eps;
+  int f32 = 0;         // x is fp32
 };
 void launch_ln_stats(const LnStatsLaunch& p, void* stream);
+
+// ---- fp32 -> bf16 (hi, lo) split pairs for the bf16x3 GEMM: rows -> [rows, 2 cols] [hi | lo],
+// else planes [2, n]
+void launch_split_bf16(const float* x, uint16_t* y, int64_t n, int cols, bool rows, void* stream);
 
 }  // namespace amd_dft

@@ -110,10 +110,11 @@ class AFNO2D(nn.Module):
             return afno2d_reference(x, self.w1, self.b1, self.w2, self.b2, c.num_blocks, c.sparsity_threshold,
                                     c.hard_thresholding_fraction)
         return afno2d_amd(x, self.w1, self.b1, self.w2, self.b2, c.num_blocks, c.sparsity_threshold,
-                          c.hard_thresholding_fraction)
+                          c.hard_thresholding_fraction, owner=self)
 
 
-def afno2d_amd(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_thresholding_fraction, residual=None):
+def afno2d_amd(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_thresholding_fraction, residual=None,
+               owner=None):
     """MI355X AFNO2D: pruned R2C along W (only kept W-modes), fused [FFT_H -> block MLP ->
     softshrink -> IFFT_H] spectral kernel, pruned C2R along W with the filter bias fused.
     Falls back to pruned FFTs + torch GEMMs when the fused kernel does not apply."""
@@ -128,7 +129,7 @@ def afno2d_amd(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_threshold
         # in registers/LDS)
         sdt = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
         xw = D._ops().r2c(x, [2], scale_f, [km, 0], sdt)
-        yw = S.afno_spectral_h(xw, w1, b1, w2, b2, num_blocks, sparsity_threshold)
+        yw = S.afno_spectral_h(xw, w1, b1, w2, b2, num_blocks, sparsity_threshold, owner=owner)
         # C2R along W from km stored modes, + bias (filter input) fused
         return S.c2r_w_add(yw, x, W, 1.0 / math.sqrt(H * W), residual)
     # generic path: pruned 2-D R2C/C2R + batched real-block GEMMs
@@ -198,7 +199,6 @@ class AFNONet(nn.Module):
         self.pos_embed = nn.Parameter(0.02 * torch.randn(1, cfg.h * cfg.w, cfg.embed_dim))
         self.blocks = nn.ModuleList([Block(cfg, backend) for _ in range(cfg.depth)])
         self.head = nn.Linear(cfg.embed_dim, cfg.out_chans * p * p, bias=False)
-        self.micro_batches = 1  # >1: batch slices on concurrent HIP streams (amd backend, GPU)
 
     def set_backend(self, backend: str) -> "AFNONet":
         self.backend = backend
@@ -211,16 +211,24 @@ class AFNONet(nn.Module):
         cfg = self.cfg
         B = x.shape[0]
         p = cfg.patch_size
+        f32 = self.backend == "amd" and x.is_cuda and x.dtype == torch.float32 and self._f32_native()
         if self.backend == "amd":
             from .._loader import load_plugins
+            from ..ops import spectral as S
 
             load_plugins()
             # conv with kernel == stride is a GEMM over non-overlapping patches: one MFMA GEMM
             # gathers the 8x8 patches straight from the image, bias + position embedding in its
             # epilogue (no patchified copy, no separate add)
-            wmat = self.patch_embed.weight.reshape(cfg.embed_dim, -1)
-            t = torch.ops.amd_dft.patch_linear(x, wmat, self.patch_embed.bias,
-                                               self.pos_embed.reshape(cfg.h * cfg.w, cfg.embed_dim), p)
+            pos = self.pos_embed.reshape(cfg.h * cfg.w, cfg.embed_dim)
+            if f32:  # bf16x3: the image as (hi, lo) planes, split weights, fp32 tokens
+                pe = self.patch_embed
+                ws = S.module_cached(self, "embed_split", (pe.weight,),
+                                     lambda: S.split_bf16(pe.weight.reshape(cfg.embed_dim, -1)))
+                t = torch.ops.amd_dft.patch_linear3(S.split_bf16(x, rows=False), ws, pe.bias, pos, p)
+            else:
+                wmat = self.patch_embed.weight.reshape(cfg.embed_dim, -1)
+                t = torch.ops.amd_dft.patch_linear(x, wmat, self.patch_embed.bias, pos, p)
             t = t.reshape(B, cfg.h, cfg.w, cfg.embed_dim)
         else:
             t = self.patch_embed(x).flatten(2).transpose(1, 2)
@@ -228,95 +236,53 @@ class AFNONet(nn.Module):
         if self.backend == "amd":
             from ..ops import spectral as S
 
-            if self.micro_batches > 1 and t.is_cuda and B >= self.micro_batches and not torch.jit.is_tracing():
-                t = self._blocks_microbatched(t)
-            else:
-                pending = None
-                for i, blk in enumerate(self.blocks):
-                    with trace_range(f"afno.block{i}"):
-                        t, pending = S.afno_block_amd(blk, t, pending)
-                hb = None
-                if pending is not None and pending.dim() == 1:
-                    # per-channel residual bias left by the LN-fused blocks: folded into the
-                    # head GEMM's bias, head(t + p) = head(t) + W_head p
-                    hb = self._head_bias_cpp(pending)
-                elif pending is not None:
-                    t = t + pending
-                # head GEMM with the un-patchify folded into its output scatter
-                return torch.ops.amd_dft.linear_unpatch(t.reshape(-1, cfg.embed_dim), self._head_weight_cpp(), hb,
-                                                        cfg.out_chans, cfg.h, cfg.w, p)
-        else:
-            for blk in self.blocks:
-                t = blk(t)
-        if self.backend == "amd":
-            # head GEMM (features permuted to (c_out, p1, p2)) with the un-patchify in its scatter
-            return torch.ops.amd_dft.linear_unpatch(t.reshape(-1, cfg.embed_dim), self._head_weight_cpp(), None,
-                                                    cfg.out_chans, cfg.h, cfg.w, p)
+            pending = None
+            for i, blk in enumerate(self.blocks):
+                with trace_range(f"afno.block{i}"):
+                    t, pending = S.afno_block_amd(blk, t, pending)
+            hb = None
+            if pending is not None and pending.dim() == 1:
+                # per-channel residual bias left by the LN-fused blocks: folded into the
+                # head GEMM's bias, head(t + p) = head(t) + W_head p
+                hb = self._head_bias_cpp(pending)
+            elif pending is not None:
+                t = t + pending
+            # head GEMM (features permuted to (c_out, p1, p2)) with the un-patchify folded into its
+            # output scatter
+            tt = t.reshape(-1, cfg.embed_dim)
+            if f32:
+                hw = self._head_weight_cpp()
+                ws = S.module_cached(self, "head_split", (hw,), lambda: S.split_bf16(hw))
+                return torch.ops.amd_dft.linear_unpatch3(S.split_bf16(tt), ws, hb, cfg.out_chans, cfg.h, cfg.w, p)
+            return torch.ops.amd_dft.linear_unpatch(tt, self._head_weight_cpp(), hb, cfg.out_chans, cfg.h, cfg.w, p)
+        for blk in self.blocks:
+            t = blk(t)
         t = self.head(t)  # [B, h, w, out*p*p], feature order (p1, p2, c_out) as FourCastNet
         t = t.reshape(B, cfg.h, cfg.w, p, p, cfg.out_chans).permute(0, 5, 1, 3, 2, 4)
         return t.reshape(B, cfg.out_chans, cfg.h * p, cfg.w * p)
 
-    def _blocks_microbatched(self, t: torch.Tensor) -> torch.Tensor:
-        """Blocks over ``micro_batches`` batch slices on their own HIP streams.  The MLP GEMMs of
-        the slices are chained (never two GEMMs at once -- hipBLASLt's stream-K
-        kernels spin on tiles of their own grid and must not share the chip with another
-        spinning GEMM), so one slice's bandwidth-bound spectral kernels run beside the other
-        slice's MFMA-bound GEMMs.  Fork/join via stream waits: captures into one hipGraph.
-        Measured at batch 32 (bench.py --streams 2): 86.4 vs 85.6 ms -- hipBLASLt's GEMM blocks
-        hold every CU's registers/LDS, so the other slice's kernels only fill GEMM tails; off
-        by default."""
-        from ..ops import spectral as S
-
-        n = self.micro_batches
-        cur = torch.cuda.current_stream(t.device)
-        if getattr(self, "_mb_streams", None) is None or len(self._mb_streams) != n:
-            self._mb_streams = [torch.cuda.Stream(t.device) for _ in range(n)]
-        streams = self._mb_streams
-        ts = list(t.chunk(n))
-        pend = [None] * n
-        for s in streams:
-            s.wait_stream(cur)
-        prev = None
-        for blk in self.blocks:
-            for i, s in enumerate(streams):
-                with torch.cuda.stream(s):
-                    x, yn = S.afno_block_spectral(blk, ts[i], pend[i])
-                    if prev is not None and prev is not s:
-                        # chain through the origin stream: a direct wait between two side
-                        # streams crashes ROCm graph capture (scripts/mb_capture_probe.py)
-                        cur.wait_stream(prev)
-                        s.wait_stream(cur)
-                    pend[i] = S.afno_block_mlp(blk, yn)
-                    prev = s
-                    ts[i] = x
-        for i, s in enumerate(streams):
-            with torch.cuda.stream(s):
-                ts[i] = ts[i] + pend[i]
-        for s, x in zip(streams, ts):
-            cur.wait_stream(s)
-            x.record_stream(cur)
-        return torch.cat(ts, 0)
+    def _f32_native(self) -> bool:
+        """fp32 on the hand kernels (bf16x3 GEMMs) needs the embed/MLP/head widths in 256-tiles."""
+        cfg = self.cfg
+        hid = int(cfg.embed_dim * cfg.mlp_ratio)
+        return (cfg.embed_dim % 256 == 0 and hid % 256 == 0 and (cfg.out_chans * cfg.patch_size ** 2) % 256 == 0
+                and cfg.patch_size == 8)
 
     def _head_bias_cpp(self, pre: torch.Tensor) -> torch.Tensor:
-        """W_head(c_out, p1, p2 order) @ pre, cached per (weight, pre) version."""
+        """W_head(c_out, p1, p2 order) @ pre as an fp32 bias, cached on the module."""
+        from ..ops.spectral import module_cached
+
         w = self._head_weight_cpp()
-        key = (w.data_ptr(), w._version, pre.data_ptr(), pre._version, w.dtype)
-        if getattr(self, "_hb_key", None) != key:
-            with torch.no_grad():
-                self._hb = w.float() @ pre.float()  # fp32 bias (GEMM epilogue adds in fp32)
-            self._hb_key = key
-        return self._hb
+        return module_cached(self, "head_bias", (w, pre), lambda: w.float() @ pre.float())
 
     def _head_weight_cpp(self) -> torch.Tensor:
         """Head weight with rows reordered from (p1, p2, c_out) to (c_out, p1, p2); cached."""
+        from ..ops.spectral import module_cached
+
         w = self.head.weight
-        key = (w.data_ptr(), w._version, w.dtype, w.device)
-        if getattr(self, "_hw_key", None) != key:
-            p, co = self.cfg.patch_size, self.cfg.out_chans
-            with torch.no_grad():
-                self._hw = w.reshape(p, p, co, -1).permute(2, 0, 1, 3).reshape(co * p * p, -1).contiguous()
-            self._hw_key = key
-        return self._hw
+        p, co = self.cfg.patch_size, self.cfg.out_chans
+        return module_cached(self, "head_weight", (w,),
+                             lambda: w.reshape(p, p, co, -1).permute(2, 0, 1, 3).reshape(co * p * p, -1).contiguous())
 
 
 def flops_per_sample(cfg: AFNOConfig) -> float:

@@ -1,15 +1,28 @@
 """Fused spectral-layer ops (FourCastNet AFNO, FNO) and fused LayerNorm.
 
 ``afno_spectral_h`` runs the K5 kernel of SURVEY §2.5: FFT along H -> block-diagonal complex
-MLP on MFMA (bf16 operands, fp32 accumulation) -> softshrink -> inverse FFT along H, one
-launch, spectrum kept in LDS.  ``c2r_w_add`` is the W-direction C2R pass with the AFNO
-filter bias (and the block residual) fused into its store.
+MLP on MFMA -> softshrink -> inverse FFT along H, one launch, spectrum kept in LDS.
+``c2r_w_add`` is the W-direction C2R pass with the AFNO filter bias (and the block residual)
+fused into its store.
+
+Two precisions of the FourCastNet block run on the hand kernels:
+
+* bf16 (``afno_block_fused``): bf16 activations, bf16 MFMA operands, fp32 accumulation.
+* fp32 (``afno_block_fused_f32``, the reference's precision -- its plugins accept only
+  ``kFLOAT``, /root/reference/src/dft_plugins/dft_plugins.cpp:101-102): fp32 residual stream,
+  fp32 spectra and FFTs, and every GEMM as a 3-product bf16 split ("bf16x3": a = hi + lo,
+  A.B = Ah.Bh + Al.Bh + Ah.Bl, fp32 accumulation; ~5e-6 relative error per GEMM against fp32
+  FMA's ~3e-7 and TF32's ~1e-3) -- 3x the bf16 MFMA work, where the exact-f32 MFMA would be 16x.
+
+Packed / split weights are cached ON THE OWNING MODULE, keyed by the parameters' storage
+pointers and versions: their lifetime follows the module (a captured hipGraph that reads them
+stays valid while the module lives), and a new model can never hit another model's entry.
 """
 from __future__ import annotations
 
 import math
 import os
-from typing import Optional, Tuple
+from typing import Callable, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -18,7 +31,9 @@ from .._loader import load_plugins
 from . import dft as D
 
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
-           "afno_block_amd", "afno_block_fused", "set_mlp_backend", "mlp_on_hand_gemm", "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix"]
+           "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
+           "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
+           "fallback_counts", "fallback_reset"]
 
 
 def _ops():
@@ -26,7 +41,44 @@ def _ops():
     return torch.ops.amd_dft
 
 
-_pack_cache: dict = {}
+def module_cached(owner, name: str, params: Sequence[torch.Tensor], build: Callable[[], object]):
+    """``build()`` cached on ``owner`` (an nn.Module) under ``name``, rebuilt when any of ``params``
+    changes storage, version, dtype or device.  Superseded values stay referenced by the module
+    (at most 4 per name) so graphs captured against them never read freed memory."""
+    key = tuple((p.data_ptr(), p._version, p.dtype, str(p.device)) for p in params)
+    cache = owner.__dict__.setdefault("_amd_packed", {})
+    hit = cache.get(name)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        val = build()
+    if hit is not None:
+        retired = owner.__dict__.setdefault("_amd_retired", {}).setdefault(name, [])
+        retired.append(hit[1])
+        del retired[:-4]
+    cache[name] = (key, val)
+    return val
+
+
+def fallback_counts() -> dict:
+    """{op: calls that ran without the op's hand kernel} since the last ``fallback_reset()``."""
+    names, counts = _ops().fallback_counts()
+    return dict(zip(names, counts))
+
+
+def fallback_reset() -> None:
+    _ops().fallback_reset()
+
+
+def split_bf16(t: torch.Tensor, rows: bool = True) -> torch.Tensor:
+    """fp32 -> bf16 pair (hi = bf16(t), lo = bf16(t - hi)): rows [..., 2K] = [hi | lo], or planes
+    [2, ...] (``rows=False``)."""
+    if t.is_cuda:
+        return _ops().split_bf16(t.float().contiguous(), rows)
+    t = t.float()
+    hi = t.to(torch.bfloat16)
+    lo = (t - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, lo], -1) if rows else torch.stack([hi, lo], 0)
 
 
 def _real_block(w: torch.Tensor) -> torch.Tensor:
@@ -36,24 +88,21 @@ def _real_block(w: torch.Tensor) -> torch.Tensor:
     return torch.cat([top, bot], dim=1)
 
 
-def pack_afno_weights(w1, b1, w2, b2) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Pack AFNO2D parameters for the fused kernel: transposed real-block bf16 weights ([n][k])
-    and concatenated fp32 biases.  Cached per parameter tensor version (graph-capture safe once
-    warmed up)."""
-    key = tuple((id(t), t.data_ptr(), t._version, str(t.device), t.dtype) for t in (w1, b1, w2, b2))
-    hit = _pack_cache.get(key)
-    if hit is not None:
-        return hit
+def pack_afno_weights(w1, b1, w2, b2, split: bool = False) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor,
+                                                                     torch.Tensor]:
+    """AFNO2D parameters in the fused kernel's layout: transposed real-block weights ([n][k]) as
+    bf16 -- or, ``split=True`` (fp32 path), as bf16 pairs [NB, n, hi k | lo k] -- and concatenated
+    fp32 biases.  Pure function; callers cache the result (``module_cached``)."""
     with torch.no_grad():
-        w1t = _real_block(w1.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
-        w2t = _real_block(w2.float()).transpose(1, 2).contiguous().to(torch.bfloat16)
+        w1t = _real_block(w1.float()).transpose(1, 2).contiguous()
+        w2t = _real_block(w2.float()).transpose(1, 2).contiguous()
+        if split:
+            w1t, w2t = split_bf16(w1t), split_bf16(w2t)
+        else:
+            w1t, w2t = w1t.to(torch.bfloat16), w2t.to(torch.bfloat16)
         b1p = torch.cat([b1[0], b1[1]], dim=1).float().contiguous()
         b2p = torch.cat([b2[0], b2[1]], dim=1).float().contiguous()
-    packed = (w1t, w2t, b1p, b2p)
-    if len(_pack_cache) > 256:
-        _pack_cache.clear()
-    _pack_cache[key] = packed
-    return packed
+    return w1t, w2t, b1p, b2p
 
 
 def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:
@@ -63,8 +112,16 @@ def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:
     return bool(_ops().afno_spectral_supported(H, C // num_blocks))
 
 
-def afno_spectral_h(xw: torch.Tensor, w1, b1, w2, b2, num_blocks: int, lam: float) -> torch.Tensor:
-    w1t, w2t, b1p, b2p = pack_afno_weights(w1, b1, w2, b2)
+def afno_spectral_h(xw: torch.Tensor, w1, b1, w2, b2, num_blocks: int, lam: float, owner=None) -> torch.Tensor:
+    """Fused H-filter on the W half spectrum ``xw`` [B, H, KM, C, 2]: bf16 MFMA operands for a
+    bf16 spectrum, the bf16x3 split GEMMs for an fp32 spectrum."""
+    split = xw.dtype == torch.float32
+    if owner is not None:
+        packed = module_cached(owner, f"afno_w{'3' if split else ''}", (w1, b1, w2, b2),
+                               lambda: pack_afno_weights(w1, b1, w2, b2, split))
+    else:
+        packed = pack_afno_weights(w1, b1, w2, b2, split)
+    w1t, w2t, b1p, b2p = packed
     return _ops().afno_spectral(xw, w1t, w2t, b1p, b2p, float(lam))
 
 
@@ -82,12 +139,11 @@ def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm, residual: Optional[torch
 
 
 def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
-    """fc + GELU with the activation fused into the GEMM epilogue (hipBLASLt) when available.
+    """fc + GELU on hipBLASLt (the ``MI_DFT_MLP=blas`` comparator path).
 
     hipBLASLt's GELU epilogue is the tanh approximation (measured, bench/probe_gelu.py: fp32
-    max |fused - gelu_tanh| = 4.8e-7, |fused - gelu_erf| = 4.7e-4, i.e. below one bf16 ulp of
-    the bf16 hidden activations for |h| > 0.06).  FourCastNet's nn.GELU is the erf form; the
-    erf-exact path is the hand MFMA GEMM (``MI_DFT_MLP=hand``, erf via A&S 7.1.26, |err| < 2e-7).
+    max |fused - gelu_tanh| = 4.8e-7, |fused - gelu_erf| = 4.7e-4).  FourCastNet's nn.GELU is
+    the erf form, which the default hand MFMA GEMM computes (erf via A&S 7.1.26, |err| < 2e-7).
     """
     if y2.is_cuda and fc.bias is not None and hasattr(torch, "_addmm_activation"):
         return torch._addmm_activation(fc.bias, y2, fc.weight.t(), use_gelu=True)
@@ -95,32 +151,26 @@ def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
 
 
 def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
-    """One FourCastNet block on the MI355X path (bf16 activations).
+    """One FourCastNet block on the MI355X path.
 
     Residual-stream fusion: the block returns ``(x, p)`` with the true block output being
-    ``x + p``.  ``p`` is either a per-channel vector (the fc2 bias; LayerNorm-fused path, see
-    :func:`afno_block_fused`) or a full tensor (the fc2 output; generic path, where the addition
-    is fused into the next block's LN1).
+    ``x + p``.  ``p`` is either a per-channel vector (the fc2 bias; LayerNorm-fused paths, see
+    :func:`afno_block_fused` / :func:`afno_block_fused_f32`) or a full tensor (the fc2 output;
+    generic path, where the addition is fused into the next block's LN1).
     """
     if pending is not None and pending.dim() == 1 and not _ln_fused_ok(blk, x):
         x, pending = x + pending, None
     if (pending is None or pending.dim() == 1) and _ln_fused_ok(blk, x):
+        if x.dtype == torch.float32:
+            return afno_block_fused_f32(blk, x, pending)
         return afno_block_fused(blk, x, pending)
     x, yn = afno_block_spectral(blk, x, pending)
     return x, afno_block_mlp(blk, yn)
 
 
-def _f32(t: torch.Tensor) -> torch.Tensor:
-    """fp32 contiguous copy of a small parameter, cached per tensor version (capture safe)."""
-    key = ("f32", id(t), t.data_ptr(), t._version, str(t.device), t.dtype)
-    hit = _pack_cache.get(key)
-    if hit is None:
-        with torch.no_grad():
-            hit = t.detach().float().contiguous()
-        if len(_pack_cache) > 256:
-            _pack_cache.clear()
-        _pack_cache[key] = hit
-    return hit
+def _f32(owner, name: str, t: torch.Tensor) -> torch.Tensor:
+    """fp32 contiguous copy of a small parameter, cached on its module (capture safe)."""
+    return module_cached(owner, name, (t,), lambda: t.detach().float().contiguous())
 
 
 def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
@@ -128,15 +178,18 @@ def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
 
     f = blk.filter
     c = f.cfg
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[-1] % 8 == 0):
+    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.shape[-1] % 8 == 0):
         return False
     B, H, W, C = x.shape
-    r0, r1, _ = kept_window(H, W, c.hard_thresholding_fraction)
+    r0, r1, km = kept_window(H, W, c.hard_thresholding_fraction)
+    if x.dtype == torch.float32 and not (C % 256 == 0 and (4 * C) % 256 == 0):
+        return False  # the bf16x3 MLP GEMMs tile 256 features
     return r0 == 0 and r1 == H and afno_fused_available(x, c.num_blocks)
 
 
 def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
-    """FourCastNet block with LN1 fused into the AFNO W-transforms and fc2 accumulated in place.
+    """FourCastNet block (bf16) with LN1 fused into the AFNO W-transforms and fc2 accumulated
+    in place.
 
     The residual stream is carried as ``(xs, pre)`` with true x = xs + pre (pre = the previous
     block's fc2 bias, per channel, or None):
@@ -145,12 +198,11 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
       X_w   = R2C_W(LN1(x))                      LN applied on load (no normalised copy in HBM)
       Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral (MFMA)
       x1    = C2R_W(Y_w) + LN1(x) + x            both skips from one read of xs
-      yn    = LN2(x1); h = GELU(fc1(yn))         hipBLASLt, GELU epilogue
-      x1   += h @ W2^T                           hipBLASLt beta = 1, in place (no bias pass)
+      yn    = LN2(x1); h = GELU(fc1(yn))         hand MFMA GEMM, erf GELU in the epilogue
+      x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue
 
     Returns (x1, fc2.bias): the bias is folded into the next block's statistics and loads
-    (or the head GEMM's bias).  Saves the LN1 kernel's normalised write + residual write and
-    one full-tensor read in the C2R versus :func:`afno_block_spectral`.
+    (or the head GEMM's bias).
     """
     from ..models.afno import kept_window
 
@@ -161,14 +213,14 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     _, _, km = kept_window(H, W, c.hard_thresholding_fraction)
     scale = 1.0 / math.sqrt(H * W)
     ops = _ops()
-    pre32 = None if pre is None else _f32(pre)
-    g1, be1 = _f32(n1.weight), _f32(n1.bias)
+    m = blk.mlp
+    pre32 = None if pre is None else _f32(blk, "pre", pre)
+    g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
     stats = ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.bfloat16)
-    yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold)
+    yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
     x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
     yn, _ = layer_norm(x1, blk.norm2)
-    m = blk.mlp
     if mlp_on_hand_gemm():
         # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
         # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL
@@ -184,12 +236,48 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     return x1, m.fc2.bias
 
 
+def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
+    """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
+
+      stats = (mean, rstd) of x                  ln_stats (fp32 rows)
+      X_w   = R2C_W(LN1(x))                      afno_wfft fp32 instantiation, fp32 spectrum
+      Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral bf16x3 variant (fp32 staging)
+      x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32
+      yn    = split(LN2(x1))                     layer_norm_split: [hi | lo] bf16 pair rows
+      h     = split(GELU(yn W1^T + b1))          bf16x3 GEMM, erf GELU, split-pair epilogue
+      x1    = x1 + h W2^T                        bf16x3 GEMM, fp32 residual epilogue
+
+    Returns (x1, fc2.bias) like :func:`afno_block_fused`."""
+    from ..models.afno import kept_window
+
+    f = blk.filter
+    c = f.cfg
+    n1, n2, m = blk.norm1, blk.norm2, blk.mlp
+    B, H, W, C = xs.shape
+    _, _, km = kept_window(H, W, c.hard_thresholding_fraction)
+    scale = 1.0 / math.sqrt(H * W)
+    ops = _ops()
+    pre32 = None if pre is None else _f32(blk, "pre", pre)
+    g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
+    stats = ops.ln_stats(xs, pre32, n1.eps)
+    xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
+    yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
+    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    yn = ops.layer_norm_split(x1.reshape(-1, C), n2.weight, n2.bias, n2.eps, None)
+    w1s = module_cached(m, "fc1_split", (m.fc1.weight,), lambda: split_bf16(m.fc1.weight))
+    w2s = module_cached(m, "fc2_split", (m.fc2.weight,), lambda: split_bf16(m.fc2.weight))
+    b1 = _f32(m, "fc1_b", m.fc1.bias)
+    hid = ops.linear3(yn, w1s, b1, 1, None, True)
+    x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
+    return x1, m.fc2.bias
+
+
 _MLP_HAND: Optional[bool] = None
 
 
 def set_mlp_backend(hand: Optional[bool]) -> None:
-    """Force the FourCastNet MLP GEMMs onto the hand MFMA kernel (True) or hipBLASLt (False);
-    None = environment / default (MI_DFT_MLP=hand|blas, default blas)."""
+    """Force the bf16 FourCastNet MLP GEMMs onto the hand MFMA kernel (True) or hipBLASLt
+    (False); None = environment / default (MI_DFT_MLP=hand|blas, default hand)."""
     global _MLP_HAND
     _MLP_HAND = hand
 
@@ -197,7 +285,7 @@ def set_mlp_backend(hand: Optional[bool]) -> None:
 def mlp_on_hand_gemm() -> bool:
     if _MLP_HAND is not None:
         return _MLP_HAND
-    return os.environ.get("MI_DFT_MLP", "blas") == "hand"
+    return os.environ.get("MI_DFT_MLP", "hand") != "blas"
 
 
 def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
@@ -210,13 +298,13 @@ def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = 
     h, x = _ops().layer_norm(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, pending)
     # filter(LN1(x)) + LN1(x) [AFNO bias] + x [double skip], fused into the C2R store
     x = afno2d_amd(h, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, c.hard_thresholding_fraction,
-                   residual=x)
+                   residual=x, owner=f)
     yn, _ = layer_norm(x, blk.norm2)
     return x, yn
 
 
 def afno_block_mlp(blk, yn: torch.Tensor) -> torch.Tensor:
-    """MFMA-bound half of a block: fc1 (+bias, GELU epilogue) and fc2 (+bias) on hipBLASLt."""
+    """MFMA-bound half of a block (generic shapes): fc1 + GELU and fc2 + bias."""
     m = blk.mlp
     B, H, W, C = yn.shape
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)

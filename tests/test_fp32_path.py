@@ -1,0 +1,242 @@
+"""fp32 FourCastNet path (the reference precision, /root/reference/src/dft_plugins/dft_plugins.cpp:101-102):
+bf16x3 split GEMMs, fp32 LayerNorm / split kernels, fp32 W-transforms, the bf16x3 AFNO spectral
+kernel -- each against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_l2
+from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+from tensorrt_dft_plugins_amd.ops import spectral as S
+
+ops = torch.ops.amd_dft
+
+
+def _split_ref(x):
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    return hi, lo
+
+
+# ------------------------------------------------------------------ CPU semantics
+def test_split_bf16_cpu_roundtrip():
+    torch.manual_seed(0)
+    x = torch.randn(6, 64) * 3
+    s = ops.split_bf16(x, True)
+    assert s.shape == (6, 128) and s.dtype == torch.bfloat16
+    back = s[:, :64].float() + s[:, 64:].float()
+    assert rel_l2(back, x) < 2e-5  # 16 significant bits
+    p = ops.split_bf16(x, False)
+    assert p.shape == (2, 6, 64)
+    assert torch.equal(p[0], s[:, :64]) and torch.equal(p[1], s[:, 64:])
+
+
+def test_split_ops_meta_shapes():
+    x = torch.empty(4, 3, 256, device="meta")
+    assert ops.split_bf16(x, True).shape == (4, 3, 512)
+    assert ops.linear3(torch.empty(10, 512, device="meta", dtype=torch.bfloat16),
+                       torch.empty(256, 512, device="meta", dtype=torch.bfloat16), None, 0, None, True).shape == (10, 512)
+    assert ops.layer_norm_split(torch.empty(7, 768, device="meta"), torch.empty(768), torch.empty(768), 1e-6,
+                                None).shape == (7, 1536)
+
+
+def test_linear3_cpu_semantics():
+    torch.manual_seed(1)
+    x, w, b, r = torch.randn(9, 64), torch.randn(256, 64) * 0.1, torch.randn(256), torch.randn(9, 256)
+    xs, ws = ops.split_bf16(x, True), ops.split_bf16(w, True)
+    y = ops.linear3(xs, ws, b, 1, r, False)
+    assert rel_l2(y, F.gelu(F.linear(x, w, b)) + r) < 3e-5
+    ys = ops.linear3(xs, ws, b, 0, None, True)
+    assert ys.shape == (9, 512)
+    assert rel_l2(ys[:, :256].float() + ys[:, 256:].float(), F.linear(x, w, b)) < 3e-5
+
+
+def test_linear3_rejects_bad_bias():
+    xs = torch.zeros(4, 128, dtype=torch.bfloat16)
+    ws = torch.zeros(256, 128, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="bias"):
+        ops.linear3(xs, ws, torch.zeros(3), 0, None, False)
+
+
+def test_fp32_backends_agree_cpu():
+    """The fp32 amd backend on CPU (ATen op impls) matches the torch backend."""
+    torch.manual_seed(2)
+    cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
+    m = AFNONet(cfg, backend="torch").eval()
+    x = torch.randn(2, 4, 48, 96)
+    with torch.no_grad():
+        r = m(x)
+        o = m.set_backend("amd")(x)
+    assert rel_l2(o, r) < 1e-5
+
+
+def test_module_cache_follows_parameters():
+    """Packed weights are cached on the module and rebuilt when a parameter changes: two models
+    built in sequence never share an entry (id/pointer reuse across models)."""
+    lin = torch.nn.Linear(8, 256)
+    a = S.module_cached(lin, "w", (lin.weight,), lambda: lin.weight.detach() * 2)
+    assert S.module_cached(lin, "w", (lin.weight,), lambda: None) is a
+    with torch.no_grad():
+        lin.weight.add_(1.0)
+    b = S.module_cached(lin, "w", (lin.weight,), lambda: lin.weight.detach() * 2)
+    assert b is not a and torch.allclose(b, lin.weight * 2)
+    assert a in lin.__dict__["_amd_retired"]["w"]  # superseded entry kept alive for old graphs
+    lin2 = torch.nn.Linear(8, 256)
+    c = S.module_cached(lin2, "w", (lin2.weight,), lambda: lin2.weight.detach() * 2)
+    assert torch.allclose(c, lin2.weight * 2)
+
+
+# ------------------------------------------------------------------ GPU numerics
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,act,bias,res,split_out", [
+    (1000, 3072, 768, 1, True, False, True),   # fc1 (+erf GELU) -> split hidden
+    (777, 768, 3072, 0, False, True, False),   # fc2 + fp32 residual, ragged M
+    (300, 256, 64, 0, True, False, False),
+    (33, 512, 128, 1, True, True, False),
+])
+def test_linear3_gpu_vs_fp32(device, M, N, K, act, bias, res, split_out):
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K)
+    w = torch.randn(N, K) / K ** 0.5
+    b = torch.randn(N) * 0.1 if bias else None
+    r = torch.randn(M, N) if res else None
+    ref = F.linear(x, w, b)
+    if act:
+        ref = F.gelu(ref)
+    if r is not None:
+        ref = ref + r
+    xs = ops.split_bf16(x.to(device), True)
+    ws = ops.split_bf16(w.to(device), True)
+    y = ops.linear3(xs, ws, None if b is None else b.to(device), act, None if r is None else r.to(device), split_out)
+    if split_out:
+        assert y.shape == (M, 2 * N) and y.dtype == torch.bfloat16
+        y = y[:, :N].float() + y[:, N:].float()
+    else:
+        assert y.shape == (M, N) and y.dtype == torch.float32
+    assert rel_l2(y.cpu(), ref) < 2e-5  # bf16x3: ~5e-6 (bf16 alone: ~3e-3)
+
+
+@pytest.mark.gpu
+def test_linear3_asymmetric_exact(device):
+    """Integer operands split exactly (lo = 0): the 3 K-segments must reproduce x @ w^T exactly."""
+    M, N, K = 256, 256, 128
+    x = torch.randint(-3, 4, (M, K)).float()
+    w = torch.randint(-3, 4, (N, K)).float()
+    w[0] = 0
+    w[0, 7] = 1
+    y = ops.linear3(ops.split_bf16(x.to(device)), ops.split_bf16(w.to(device)), None, 0, None, False).cpu()
+    assert torch.equal(y, x @ w.t())
+    # lo halves exercised: x = integer + 2^-9 parts
+    x2 = x + torch.randint(0, 2, (M, K)).float() * 2.0 ** -9
+    y2 = ops.linear3(ops.split_bf16(x2.to(device)), ops.split_bf16(w.to(device)), None, 0, None, False).cpu()
+    assert torch.allclose(y2, x2.double().matmul(w.double().t()).float(), atol=1e-5, rtol=0)
+
+
+@pytest.mark.gpu
+def test_split_and_layernorm_fp32_gpu(device):
+    torch.manual_seed(3)
+    x = torch.randn(1000, 768) * 2 + 0.5
+    g = torch.randn(768) * 0.3 + 1
+    b = torch.randn(768) * 0.1
+    pre = torch.randn(768) * 0.2
+    s = ops.split_bf16(x.to(device), True).cpu()
+    hi, lo = _split_ref(x)
+    assert torch.equal(s[:, :768], hi) and torch.equal(s[:, 768:], lo)
+    ref = F.layer_norm(x + pre, (768,), g, b, 1e-6)
+    ys = ops.layer_norm_split(x.to(device), g.to(device), b.to(device), 1e-6, pre.to(device)).cpu()
+    assert rel_l2(ys[:, :768].float() + ys[:, 768:].float(), ref) < 2e-5
+    y, _ = ops.layer_norm(x.to(device), g.to(device), b.to(device), 1e-6, None)
+    assert y.dtype == torch.float32 and rel_l2(y.cpu(), F.layer_norm(x, (768,), g, b, 1e-6)) < 1e-6
+    st = ops.ln_stats(x.to(device), pre.to(device), 1e-6).cpu()
+    xp = x + pre
+    assert torch.allclose(st[:, 0], xp.mean(1), atol=1e-5)
+    assert torch.allclose(st[:, 1], torch.rsqrt(xp.var(1, unbiased=False) + 1e-6), rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_afno_spectral_fp32_kernel_vs_torch_fp32(device):
+    """bf16x3 AFNO H-filter vs the same op in plain fp32 (un-split fp32 weights): rel-L2 <= 1e-5."""
+    torch.manual_seed(4)
+    B, H, KM, C, nb = 2, 90, 46, 768, 8
+    bs = C // nb
+    xw = torch.randn(B, H, KM, C, 2)
+    w1, w2 = 0.05 * torch.randn(2, nb, bs, bs), 0.05 * torch.randn(2, nb, bs, bs)
+    b1, b2 = 0.05 * torch.randn(2, nb, bs), 0.05 * torch.randn(2, nb, bs)
+    w1t = S._real_block(w1).transpose(1, 2).contiguous()  # fp32 packed: the exact reference
+    w2t = S._real_block(w2).transpose(1, 2).contiguous()
+    b1p, b2p = torch.cat([b1[0], b1[1]], 1), torch.cat([b2[0], b2[1]], 1)
+    ref = ops.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)  # CPU: fp32 ATen math
+    w1s, w2s, b1s, b2s = S.pack_afno_weights(w1.to(device), b1.to(device), w2.to(device), b2.to(device), split=True)
+    assert w1s.shape == (nb, 2 * bs, 4 * bs)
+    out = ops.afno_spectral(xw.to(device), w1s, w2s, b1s, b2s, 0.01)
+    assert out.dtype == torch.float32
+    assert rel_l2(out.cpu(), ref) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_pre", [False, True])
+def test_afno_w_fp32_kernels(device, with_pre):
+    torch.manual_seed(5)
+    B, H, W, C = 2, 90, 180, 768
+    x = torch.randn(B, H, W, C)
+    g, b = torch.randn(C) * 0.3 + 1, torch.randn(C) * 0.1
+    pre = torch.randn(C) * 0.2 if with_pre else None
+    st = ops.ln_stats(x, pre, 1e-6)
+    scale = 1.0 / math.sqrt(H * W)
+    ref = ops.r2c_ln(x, 2, scale, 46, st, g, b, pre, torch.float32)
+    d = lambda t: None if t is None else t.to(device)  # noqa: E731
+    S.fallback_reset()
+    out = ops.r2c_ln(x.to(device), 2, scale, 46, st.to(device), g.to(device), b.to(device), d(pre), torch.float32)
+    assert out.dtype == torch.float32 and rel_l2(out.cpu(), ref) < 2e-6
+    X = torch.randn_like(ref)
+    ref2 = ops.c2r_ln_add(X, 2, W, scale, x, st, g, b, pre)
+    out2 = ops.c2r_ln_add(X.to(device), 2, W, scale, x.to(device), st.to(device), g.to(device), b.to(device), d(pre))
+    assert out2.dtype == torch.float32 and rel_l2(out2.cpu(), ref2) < 2e-6
+    assert S.fallback_counts() == {}
+
+
+@pytest.mark.gpu
+def test_fourcastnet_fp32_amd_vs_torch(device):
+    """The fp32 FourCastNet on the hand kernels vs the plain-PyTorch fp32 model (torch.fft,
+    hipBLASLt fp32 GEMMs) at depth 2: rel-L2 <= 1e-4, with zero fallbacks to ATen."""
+    torch.manual_seed(6)
+    m = AFNONet(AFNOConfig(depth=2), backend="torch").to(device).eval()
+    x = torch.randn(2, 20, 720, 1440, device=device)
+    with torch.no_grad():
+        ref = m(x)
+        S.fallback_reset()
+        out = m.set_backend("amd")(x)
+    assert out.dtype == torch.float32
+    assert S.fallback_counts() == {}
+    assert rel_l2(out, ref) < 1e-4
+
+
+@pytest.mark.gpu
+def test_fourcastnet_bf16_no_fallbacks(device):
+    torch.manual_seed(7)
+    m = AFNONet(AFNOConfig(depth=2), backend="amd").to(device).to(torch.bfloat16).eval()
+    x = torch.randn(2, 20, 720, 1440, device=device).to(torch.bfloat16)
+    with torch.no_grad():
+        S.fallback_reset()
+        m(x)
+    assert S.fallback_counts() == {}
+
+
+@pytest.mark.gpu
+def test_patch_linear3_and_unpatch3_gpu(device):
+    torch.manual_seed(8)
+    B, C, h, w, N = 2, 20, 6, 10, 768
+    x = torch.randn(B, C, h * 8, w * 8)
+    wt = torch.randn(N, C * 64) * 0.02
+    bias, pos = torch.randn(N) * 0.1, torch.randn(h * w, N) * 0.1
+    ref = F.conv2d(x, wt.reshape(N, C, 8, 8), bias, stride=8).flatten(2).transpose(1, 2) + pos
+    t = ops.patch_linear3(ops.split_bf16(x.to(device), False), ops.split_bf16(wt.to(device)), bias.to(device),
+                          pos.to(device), 8)
+    assert t.dtype == torch.float32 and rel_l2(t.cpu(), ref.reshape(-1, N)) < 2e-5
+    hw = torch.randn(C * 64, N) * 0.02
+    tt = torch.randn(B * h * w, N)
+    img = ops.linear_unpatch3(ops.split_bf16(tt.to(device)), ops.split_bf16(hw.to(device)), None, C, h, w, 8)
+    ref2 = ops.unpatchify(tt @ hw.t(), C, h, w, 8)
+    assert img.dtype == torch.float32 and rel_l2(img.cpu(), ref2) < 2e-5
