@@ -9,7 +9,10 @@ def short(n: str) -> str:
     m = re.search(r"fft_fixed_kernel<\(amd_dft::Kind\)(\d), (\w+), (\d+), (\d+), amd_dft::fixed_detail::FL<(.*?)>", n)
     if m:
         return f"fft_fixed K{m.group(1)} cols={m.group(2)} TP={m.group(3)} T={m.group(4)} R=<{m.group(5)}>"
-    for k in ("afno_spectral_kernel", "ln_bf16_kernel", "fft_pass_kernel", "fno_mix", "fno_pointwise_kernel", "patch_remap", "fno_c2r_pw_kernel", "dftw_r2c_kernel", "gemm_bf16_kernel", "ln_stats_kernel"):
+    m = re.search(r"gemm_bf16_kernel<(.*?)>", n)
+    if m:
+        return "gemm<" + m.group(1).replace("true", "T").replace("false", "F") + ">"
+    for k in ("afno_spectral_x3_kernel", "afno_spectral_kernel", "afno_w_r2c_ln_kernel", "afno_w_c2r_ln_kernel", "ln_f32_kernel", "split_bf16_kernel", "ln_bf16_kernel", "fft_pass_kernel", "fno_mix", "fno_pointwise_kernel", "patch_remap", "fno_c2r_pw_kernel", "dftw_r2c_kernel", "gemm_bf16_kernel", "ln_stats_kernel"):
         if k in n:
             return k + (n[n.index(k) + len(k):][:40])
     return n[:110]

@@ -29,7 +29,7 @@ def test_afno_spectral_kernel_vs_cpu(device):
     ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)  # CPU: fp32 math
     out = torch.ops.amd_dft.afno_spectral(xw.to(device), w1t.to(device), w2t.to(device), b1p.to(device),
                                           b2p.to(device), 0.01)
-    assert rel_l2(out, ref) < 1.5e-2  # bf16 MFMA operands, fp32 accumulation
+    assert rel_l2(out, ref) < 6e-3  # bf16 MFMA operands, fp32 accumulation (measured 3.3e-3)
 
 
 def test_afno_spectral_kernel_exact_weights(device):
