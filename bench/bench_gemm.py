@@ -21,6 +21,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32 * 16200)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--x3", action="store_true", help="bf16x3 split GEMMs (fp32 path) + the bf16 hand GEMMs")
     a = ap.parse_args(argv)
     tdp.load_plugins()
     M, C, Hd = a.rows, 768, 3072
@@ -41,6 +42,17 @@ def main(argv=None):
         "fc2 amd": lambda: ops.linear(h, w2, b2, 0, None),
         "fc2 hipblaslt": lambda: F.linear(h, w2, b2h),
     }
+    if a.x3:
+        xs = ops.split_bf16(x.float())
+        hs = ops.split_bf16(h.float())
+        w1s, w2s = ops.split_bf16(w1.float()), ops.split_bf16(w2.float())
+        r32 = torch.randn(M, C, device=dev)
+        v = {
+            "fc1_gelu x3 (split out)": lambda: ops.linear3(xs, w1s, b1, 1, None, True),
+            "fc2 x3 (+fp32 residual)": lambda: ops.linear3(hs, w2s, None, 0, r32, False),
+            "fc1_gelu amd": v["fc1_gelu amd"],
+            "fc2 amd": v["fc2 amd"],
+        }
     res = {k: [] for k in v}
     for _ in range(a.rounds):
         for k, f in v.items():
@@ -50,7 +62,8 @@ def main(argv=None):
     for k, t in res.items():
         med = statistics.median(t)
         out[k] = {"us": round(med, 1), "TFLOPs": round(flop / med / 1e6, 1)}
-        print(f"{k:22s} {med:9.1f} us  {flop / med / 1e6:7.1f} TFLOP/s", flush=True)
+        mult = 3 if "x3" in k else 1
+        print(f"{k:26s} {med:9.1f} us  {flop / med / 1e6:7.1f} TFLOP/s  ({mult * flop / med / 1e6:7.1f} bf16-MFMA TFLOP/s)", flush=True)
     y = ops.linear(x[:4096], w1, b1, 1, None).float()
     ref = F.gelu(F.linear(x[:4096].float(), w1.float(), b1))
     print("rel err", ((y - ref).norm() / ref.norm()).item())

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -409,8 +410,25 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   return M >= 1 && N % kBF == 0 && K % kBK == 0 && K >= kBK && M < (int64_t(1) << 31) && N * K < (int64_t(1) << 31);
 }
 
+// MI_DFT_GEMM=4w selects the four-wave 128x128-per-wave kernel (gemm4w.hip) where it applies;
+// default: the 8-wave ping-pong kernel below, measured faster on the FourCastNet shapes
+// (fc2 2127 vs 2466 us, fc1+GELU 3231 vs 3997 us, bf16x3 fc2 6360 vs 7639 us;
+// profiles/gemm_4w_vs_8w_r2.txt: hipcc keeps part of the 4-wave kernel's fragments in the
+// accumulator file and shuffles them back every few MFMAs)
+static int gemm_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MI_DFT_GEMM");
+    return (e && std::string(e) == "4w") ? 4 : 8;
+  }();
+  return v;
+}
+
 void launch_gemm(const GemmLaunch& p, void* stream) {
   if (!gemm_supported(p.M, p.N, p.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
+  if (gemm_variant() == 4 && gemm4w_applicable(p)) {
+    launch_gemm4w(p, stream);
+    return;
+  }
   if (p.ln_stats && !p.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
   if (p.out < 0 || p.out > 2 || (p.out != 0) != (p.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
