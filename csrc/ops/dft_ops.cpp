@@ -712,7 +712,8 @@ at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double 
   const c10::DeviceGuard guard(X_.device());
   check_ln_args(x_, dim, stats_, g_, b_, pre_, "c2r_ln_add");
   const int64_t axis = x_.dim() - 2;
-  TORCH_CHECK(X_.dim() == x_.dim() + 1 && X_.size(-1) == 2 && x_.size(axis) == n, "amd_dft.c2r_ln_add: shape mismatch");
+  TORCH_CHECK(X_.dim() == x_.dim() + 1 && X_.size(-1) == 2 && x_.size(axis) == n, "amd_dft.c2r_ln_add: shape mismatch "
+              "(X must be [..., km, C, 2] with the leading dims and C of x)");
   at::Tensor X = X_.contiguous(), x = x_.contiguous();
   const int64_t km = X.size(axis);
   const std::vector<int64_t> dv{axis}, nv{n}, kv{km, 0};
@@ -793,6 +794,9 @@ at::Tensor c2r_ln_add_cpu(const at::Tensor& X, int64_t dim, int64_t n, double sc
                           const std::optional<at::Tensor>& pre) {
   check_ln_args(x, dim, stats, g, b, pre, "c2r_ln_add");
   const int64_t axis = x.dim() - 2;
+  TORCH_CHECK(X.dim() == x.dim() + 1 && X.size(-1) == 2 && x.size(axis) == n && X.sizes().slice(0, axis) == x.sizes().slice(0, axis) &&
+                  X.size(axis + 1) == x.size(-1) && X.size(axis) <= n / 2 + 1,
+              "amd_dft.c2r_ln_add: X must be [..., km, C, 2] with the leading dims and C of x and km <= n/2+1");
   at::Tensor xp;
   at::Tensor h = ln_apply(x, stats, g, b, pre, &xp);
   const std::vector<int64_t> dv{axis}, nv{n}, kv{X.size(axis), 0};
@@ -963,6 +967,7 @@ std::string plugin_registry() {
 
 int64_t plan_cache_size() { return static_cast<int64_t>(plan_cache_entries()); }
 void plan_cache_clear() { plan_cache_reset(); }
+int64_t plan_cache_pinned_count() { return static_cast<int64_t>(plan_cache_pinned()); }
 
 }  // namespace
 }  // namespace amd_dft
@@ -986,6 +991,7 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("plugin_registry() -> str", &amd_dft::plugin_registry);
   m.def("plan_cache_size() -> int", &amd_dft::plan_cache_size);
   m.def("plan_cache_clear() -> ()", &amd_dft::plan_cache_clear);
+  m.def("plan_cache_pinned() -> int", &amd_dft::plan_cache_pinned_count);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {

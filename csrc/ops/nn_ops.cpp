@@ -90,6 +90,7 @@ at::Tensor linear_ref(const at::Tensor& x, const at::Tensor& w, const c10::optio
 at::Tensor linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
                       const c10::optional<at::Tensor>& residual) {
   TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear: act must be 0 (none) or 1 (gelu)");
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == w.size(0), "amd_dft.linear: bias must have N entries");
   return linear_ref(x, w, bias, act, residual);
 }
 
@@ -137,6 +138,7 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
 // permute path is the CPU implementation.
 at::Tensor patch_linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                             const c10::optional<at::Tensor>& pos, int64_t p) {
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == w.size(0), "patch_linear: bias must have N entries");
   at::Tensor t = patchify_cpu(x, p);
   at::Tensor y = linear_ref(t, w, bias, 0, c10::nullopt).to(at::kFloat);
   if (pos.has_value() && pos->defined()) {
@@ -192,6 +194,7 @@ at::Tensor patch_linear_meta(const at::Tensor& x, const at::Tensor& w, const c10
 
 at::Tensor linear_unpatch_cpu(const at::Tensor& t, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                               int64_t C, int64_t h, int64_t wd, int64_t p) {
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == w.size(0), "linear_unpatch: bias must have N entries");
   return unpatchify_cpu(linear_ref(t, w, bias, 0, c10::nullopt), C, h, wd, p);
 }
 

@@ -15,18 +15,24 @@ namespace amd_dft {
 namespace {
 
 // ------------------------------------------------------------------ plan cache
+// LRU over (device, length), capacity MI_DFT_PLAN_CACHE_SIZE (default 256).  A plan looked up
+// while the current stream is capturing a hipGraph is PINNED: the graph holds the raw
+// pointer of its twiddle table, so a pinned plan is never evicted and survives
+// plan_cache_clear() (eviction after capture would let the allocator hand the
+// twiddles' memory to another tensor under a live graph).
 class PlanCache {
  public:
   std::shared_ptr<DevPlan> get(int64_t L, const at::Device& dev) {
     const uint64_t key = (static_cast<uint64_t>(dev.index() + 1) << 40) | static_cast<uint64_t>(L);
+    const bool capturing = c10::hip::currentStreamCaptureStatusMayInitCtx() != c10::hip::CaptureStatus::None;
     std::lock_guard<std::mutex> g(mu_);
     auto it = map_.find(key);
     if (it != map_.end()) {
-      lru_.splice(lru_.begin(), lru_, it->second.second);
-      return it->second.first;
+      lru_.splice(lru_.begin(), lru_, it->second.pos);
+      if (capturing) it->second.pinned = true;
+      return it->second.plan;
     }
-    TORCH_CHECK(c10::hip::currentStreamCaptureStatusMayInitCtx() == c10::hip::CaptureStatus::None,
-                "amd_dft: FFT plan for length ", L,
+    TORCH_CHECK(!capturing, "amd_dft: FFT plan for length ", L,
                 " was not created before graph capture; run the model once (warm-up) before capturing");
     auto dp = std::make_shared<DevPlan>();
     dp->plan = make_plan_1d(static_cast<int32_t>(L));
@@ -34,24 +40,52 @@ class PlanCache {
                               at::TensorOptions().dtype(at::kFloat));
     dp->tw = host.to(dev);
     lru_.push_front(key);
-    map_[key] = {dp, lru_.begin()};
-    while (map_.size() > capacity()) {
-      map_.erase(lru_.back());
-      lru_.pop_back();
-    }
+    map_[key] = Entry{dp, lru_.begin(), false};
+    evict_locked();
     return dp;
   }
+  // drops every unpinned plan; refused while a graph is being captured
   void clear() {
+    TORCH_CHECK(c10::hip::currentStreamCaptureStatusMayInitCtx() == c10::hip::CaptureStatus::None,
+                "amd_dft.plan_cache_clear: not allowed during hipGraph capture");
     std::lock_guard<std::mutex> g(mu_);
-    map_.clear();
-    lru_.clear();
+    for (auto it = lru_.begin(); it != lru_.end();) {
+      auto e = map_.find(*it);
+      if (e->second.pinned) {
+        ++it;
+      } else {
+        map_.erase(e);
+        it = lru_.erase(it);
+      }
+    }
   }
   size_t size() {
     std::lock_guard<std::mutex> g(mu_);
     return map_.size();
   }
+  size_t pinned() {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t n = 0;
+    for (const auto& kv : map_) n += kv.second.pinned ? 1 : 0;
+    return n;
+  }
 
  private:
+  struct Entry {
+    std::shared_ptr<DevPlan> plan;
+    std::list<uint64_t>::iterator pos;
+    bool pinned;
+  };
+  void evict_locked() {
+    auto it = lru_.end();
+    while (map_.size() > capacity() && it != lru_.begin()) {
+      --it;
+      auto e = map_.find(*it);
+      if (e->second.pinned) continue;  // oldest unpinned first
+      map_.erase(e);
+      it = lru_.erase(it);
+    }
+  }
   static size_t capacity() {
     static size_t cap = [] {
       const char* e = std::getenv("MI_DFT_PLAN_CACHE_SIZE");
@@ -62,7 +96,7 @@ class PlanCache {
   }
   std::mutex mu_;
   std::list<uint64_t> lru_;
-  std::unordered_map<uint64_t, std::pair<std::shared_ptr<DevPlan>, std::list<uint64_t>::iterator>> map_;
+  std::unordered_map<uint64_t, Entry> map_;
 };
 
 PlanCache& plan_cache() {
@@ -95,6 +129,7 @@ std::pair<at::Tensor, at::Tensor> get_dft_gemm_tables(DftTable kind, int W, int 
   return cache[key] = {f, p};
 }
 size_t plan_cache_entries() { return plan_cache().size(); }
+size_t plan_cache_pinned() { return plan_cache().pinned(); }
 void plan_cache_reset() { plan_cache().clear(); }
 
 }  // namespace amd_dft

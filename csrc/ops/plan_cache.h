@@ -18,6 +18,7 @@ struct DevPlan {
 // while the current stream is capturing a hipGraph).
 std::shared_ptr<DevPlan> get_plan(int64_t L, const at::Device& dev);
 size_t plan_cache_entries();
+size_t plan_cache_pinned();  // plans looked up during a hipGraph capture (never evicted)
 
 // Fragment-ordered twiddle tables of the DFT-as-GEMM kernels, (fragments, phases) on `dev`.
 enum class DftTable { R2C = 0, C2R_F32 = 1, C2R_BF16 = 2 };

@@ -33,6 +33,11 @@ ENGINE_FORMAT_VERSION = 1
 PLUGIN_VERSION = "1"
 
 
+_BINDING_DTYPES = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16,
+                   "float64": torch.float64, "int64": torch.int64, "int32": torch.int32, "bool": torch.bool,
+                   "complex64": torch.complex64}
+
+
 @dataclass
 class Binding:
     name: str
@@ -41,7 +46,11 @@ class Binding:
     is_input: bool
 
     def torch_dtype(self) -> torch.dtype:
-        return getattr(torch, self.dtype)
+        # fixed name -> dtype map: the engine file is untrusted input (no getattr on torch)
+        try:
+            return _BINDING_DTYPES[self.dtype]
+        except KeyError:
+            raise ValueError(f"engine binding {self.name!r}: unsupported dtype {self.dtype!r}") from None
 
 
 @dataclass

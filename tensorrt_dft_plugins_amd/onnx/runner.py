@@ -462,14 +462,23 @@ def register_op(name: str, domain: str, fn: OpFn) -> None:
 AMD_DOMAIN = "com.amd.dft"
 
 
+_AMD_NODE_DENY = frozenset({"wrap_device_ptr", "wrap_host_ptr", "plan_cache_clear", "plan_cache_size", "plan_cache_pinned",
+                            "fallback_counts", "fallback_reset", "plugin_registry"})
+
+
 def _amd_node(opname: str):
     """Executor for a ``com.amd.dft::<op>`` node written by the exporter's generic symbolic:
     rebuilds the ``torch.ops.amd_dft.<op>`` call from the schema, the node inputs and attributes."""
     from .._loader import load_plugins
 
     load_plugins()
-    if not hasattr(torch.ops.amd_dft, opname):
-        raise NotImplementedError(f"com.amd.dft::{opname}: no such operator in the loaded library")
+    from .exporter import amd_op_names
+
+    # Only the tensor operators the exporter can emit are executable: an ONNX file or engine
+    # is untrusted input, and the library also holds runtime helpers (raw-pointer wrappers,
+    # cache controls) that must never be reachable from a graph (ADVICE r1).
+    if opname in _AMD_NODE_DENY or opname not in amd_op_names():
+        raise NotImplementedError(f"com.amd.dft::{opname}: not an exportable tensor operator of the loaded library")
     op = getattr(torch.ops.amd_dft, opname)
     sc = op.default._schema
 

@@ -1,0 +1,88 @@
+"""Hardening against untrusted engine / ONNX files and stale device pointers:
+allowlisted com.amd.dft nodes, a fixed binding-dtype map, shape checks on the public ops and
+plan-cache pinning under hipGraph capture."""
+import pytest
+import torch
+
+from tensorrt_dft_plugins_amd.engine.engine import Binding
+from tensorrt_dft_plugins_amd.onnx import proto as P
+from tensorrt_dft_plugins_amd.onnx.runner import OnnxGraph
+
+ops = torch.ops.amd_dft
+
+
+def _one_node_model(op_type, domain, attrs=()):
+    m = P.ModelProto()
+    m.ir_version = 8
+    op = m.opset_import.add()
+    op.domain, op.version = domain, 1
+    n = m.graph.node.add()
+    n.op_type, n.domain = op_type, domain
+    n.output.append("y")
+    for k, v in attrs:
+        a = n.attribute.add()
+        a.name, a.i, a.type = k, v, P.ATTR_INT
+    m.graph.output.add().name = "y"
+    return m.SerializeToString()
+
+
+@pytest.mark.parametrize("name", ["wrap_host_ptr", "wrap_device_ptr", "plan_cache_clear", "fallback_reset"])
+def test_onnx_runtime_helpers_not_dispatchable(name):
+    with pytest.raises(NotImplementedError, match="not an exportable tensor operator"):
+        OnnxGraph(_one_node_model(name, "com.amd.dft", (("ptr", 4096),)), device="cpu")
+
+
+def test_binding_dtype_fixed_map():
+    assert Binding("x", [1], "float32", True).torch_dtype() is torch.float32
+    with pytest.raises(ValueError, match="unsupported dtype"):
+        Binding("x", [1], "load", True).torch_dtype()
+
+
+def test_c2r_ln_add_rejects_mismatched_spectrum():
+    x = torch.randn(2, 4, 12, 16)
+    st = ops.ln_stats(x, None, 1e-6)
+    g, b = torch.ones(16), torch.zeros(16)
+    X_bad_batch = torch.randn(3, 4, 7, 16, 2)
+    with pytest.raises(RuntimeError, match="leading dims"):
+        ops.c2r_ln_add(X_bad_batch, 2, 12, 1.0, x, st, g, b, None)
+    X_bad_c = torch.randn(2, 4, 7, 8, 2)
+    with pytest.raises(RuntimeError, match="leading dims"):
+        ops.c2r_ln_add(X_bad_c, 2, 12, 1.0, x, st, g, b, None)
+
+
+@pytest.mark.parametrize("op", ["linear", "patch_linear", "linear_unpatch"])
+def test_gemm_ops_reject_bad_bias(op):
+    if op == "linear":
+        call = lambda: ops.linear(torch.randn(4, 64), torch.randn(256, 64), torch.randn(3), 0, None)  # noqa: E731
+    elif op == "patch_linear":
+        call = lambda: ops.patch_linear(torch.randn(1, 2, 16, 16), torch.randn(256, 128), torch.randn(3), None, 8)  # noqa: E731
+    else:
+        call = lambda: ops.linear_unpatch(torch.randn(4, 64), torch.randn(128, 64), torch.randn(3), 2, 2, 2, 8)  # noqa: E731
+    with pytest.raises(RuntimeError, match="bias"):
+        call()
+
+
+@pytest.mark.gpu
+def test_plan_cache_pinned_under_capture(device):
+    """Capture an rfft2 graph, clear the plan cache, churn the allocator, replay: the captured
+    twiddle pointers must still be valid (the plan was pinned at capture)."""
+    torch.manual_seed(0)
+    x = torch.randn(2, 90, 180, device=device)
+    ops.Rfft(x, 0, 1, 2)  # warm-up creates the plans
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.Rfft(x, 0, 1, 2)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        y = ops.Rfft(x, 0, 1, 2)
+    assert ops.plan_cache_pinned() >= 1
+    ops.plan_cache_clear()
+    assert ops.plan_cache_size() >= ops.plan_cache_pinned() >= 1
+    junk = [torch.full((1 << 16,), float("nan"), device=device) for _ in range(64)]  # reuse freed blocks
+    g.replay()
+    torch.cuda.synchronize()
+    ref = torch.view_as_real(torch.fft.rfft2(x.cpu().double()))
+    assert ((y.cpu().double() - ref).norm() / ref.norm()).item() < 1e-5
+    del junk
