@@ -26,6 +26,12 @@ CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build", "native")
 PKG = os.path.join(ROOT, "tensorrt_dft_plugins_amd")
 LIB = os.path.join(PKG, "_C.so")
+# host AddressSanitizer variant: the torch op layer / plan builder (host C++)
+# instrumented, device code unchanged; written to build/asan/_C.so, loaded via MI_DFT_LIB with
+# the ASan runtime preloaded (scripts/ci_cpu.sh)
+BUILD_ASAN = os.path.join(ROOT, "build", "asan")
+LIB_ASAN = os.path.join(BUILD_ASAN, "_C.so")
+ASAN_FLAGS = ["-fsanitize=address", "-fno-omit-frame-pointer", "-fno-gpu-sanitize"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 
@@ -58,9 +64,9 @@ def _headers_mtime() -> float:
     return max([os.path.getmtime(h) for h in hs] + [0.0])
 
 
-def _obj_path(src: str) -> str:
+def _obj_path(src: str, asan: bool = False) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-    return os.path.join(BUILD, rel + ".o")
+    return os.path.join(BUILD_ASAN if asan and not src.endswith(".hip") else BUILD, rel + ".o")
 
 
 def _file_flags(src: str) -> list:
@@ -73,8 +79,8 @@ def _file_flags(src: str) -> list:
     return []
 
 
-def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
-    obj = _obj_path(src)
+def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False) -> str:
+    obj = _obj_path(src, asan)
     cmd = [_hipcc(), "-c", "-fPIC", "-std=c++17", "-O3", "-Wall", "-Wno-unused-function",
            "-Wno-unused-variable", "-Wno-sign-compare", "-I" + CSRC,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-o", obj]
@@ -91,6 +97,8 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
         # host-only C++ that includes HIP runtime headers (torch's c10/hip)
         rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
         cmd += ["-x", "c++", "-I" + os.path.join(rocm, "include"), "-D__HIP_PLATFORM_AMD__=1"]
+        if asan:
+            cmd += ASAN_FLAGS
     if needs_torch:
         cmd += ["-O2", "-DUSE_ROCM=1", "-Wno-deprecated-declarations", "-Wno-unknown-pragmas"]
         cmd += ["-I" + p for p in tinc]
@@ -102,48 +110,56 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int) -> str:
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
-    """Compile every HIP/C++ source for gfx950 and link ``_C.so``; returns its path."""
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, asan: bool = False) -> str:
+    """Compile every HIP/C++ source for gfx950 and link ``_C.so``; returns its path.
+    ``asan``: host C++ with AddressSanitizer into build/asan/_C.so (device objects shared)."""
     os.makedirs(BUILD, exist_ok=True)
+    if asan:
+        os.makedirs(BUILD_ASAN, exist_ok=True)
+    lib = LIB_ASAN if asan else LIB
     tinc, tlib, abi = _torch_paths()
     hdr = _headers_mtime()
     srcs = sources()
     todo = []
     for src, nt in srcs:
-        obj = _obj_path(src)
+        obj = _obj_path(src, asan)
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
             todo.append((src, nt))
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     if todo:
         if verbose:
-            print(f"[amd_dft build] compiling {len(todo)} file(s) for {ARCH} with {jobs} jobs", flush=True)
+            print(f"[amd_dft build] compiling {len(todo)} file(s) for {ARCH} with {jobs} jobs"
+                  + (" (host ASan)" if asan else ""), flush=True)
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = {ex.submit(_compile, s, nt, tinc, abi): s for s, nt in todo}
+            futs = {ex.submit(_compile, s, nt, tinc, abi, asan): s for s, nt in todo}
             for f in cf.as_completed(futs):
                 f.result()
                 if verbose:
                     print("  built", os.path.relpath(futs[f], ROOT), flush=True)
-    objs = [_obj_path(s) for s, _ in srcs]
-    if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        tmp = LIB + ".tmp"
+    objs = [_obj_path(s, asan) for s, _ in srcs]
+    if todo or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        tmp = lib + ".tmp"
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
             "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             "-Wl,-rpath," + tlib]
+        if asan:
+            cmd += ["-fsanitize=address", "-shared-libasan", "-fno-gpu-sanitize"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib)
         if verbose:
-            print("[amd_dft build] linked", os.path.relpath(LIB, ROOT), flush=True)
-    return LIB
+            print("[amd_dft build] linked", os.path.relpath(lib, ROOT), flush=True)
+    return lib
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--asan", action="store_true", help="host AddressSanitizer build into build/asan/_C.so")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.j)
+    build(force=a.force, jobs=a.j, asan=a.asan)
 
 
 if __name__ == "__main__":
