@@ -141,14 +141,40 @@ def run_steps(runner, steps: int, warmup: int, world: int, dev, cuda: bool) -> f
     return elapsed
 
 
+class _EngineFn:
+    """A deserialized engine's graph as the per-step callable (captured by the DP runner)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+
+    def __call__(self, x):
+        return self.eng.graph.run(x)[0]
+
+
 def build_runner(cfg, dtype, B, dev, a, seed):
+    """Model -> (default) ONNX export with its com.amd.dft nodes -> serialized engine bytes ->
+    deserialized engine -> hipGraph-captured DP runner: the timed step is the engine a user
+    would load with ``dftexec --loadEngine`` (reference: export -> build -> serialize ->
+    deserialize -> execute_v2, /root/reference/tests/test_dft.py:89-115)."""
     torch.manual_seed(seed)
     model = AFNONet(cfg, backend="amd").to(dev).to(dtype).eval()
     x = torch.randn(B, cfg.in_chans, *cfg.img_size, device=dev).to(dtype)
+    info = {"engine": False}
+    fn = model
+    if a.engine and dev.type == "cuda":
+        from tensorrt_dft_plugins_amd.engine import Engine
+
+        t0 = time.perf_counter()
+        blob = Engine.build(model, (x,), device=dev, use_graph=False).serialize()
+        eng = Engine.deserialize(blob, device=dev, use_graph=False)
+        fn = _EngineFn(eng)
+        info = {"engine": True, "engine_bytes": len(blob), "engine_build_load_s": round(time.perf_counter() - t0, 1)}
+        log(f"{dtype}: engine exported, serialized ({len(blob) / 1e6:.0f} MB) and deserialized in "
+            f"{info['engine_build_load_s']}s")
     t0 = time.perf_counter()
-    runner = DataParallelInference(model, x, gather=not a.no_gather, use_graph=not a.no_graph)
+    runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph)
     log(f"{dtype}: captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t0:.1f}s")
-    return model, runner
+    return info, runner
 
 
 def main(argv=None) -> int:
@@ -161,6 +187,8 @@ def main(argv=None) -> int:
     ap.add_argument("--dtype", choices=sorted(DTYPES), default="fp32", help="headline precision")
     ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of the other-precision extra (0: skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-engine", dest="engine", action="store_false",
+                    help="capture the nn.Module directly instead of the serialized engine")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 / FNO block probes")
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
@@ -202,7 +230,7 @@ def main(argv=None) -> int:
         extra.update(time_fno_block_us())
         log(f"single-op probes: {extra}")
 
-    _, runner = build_runner(cfg, head_dt, B, dev, a, 1234 + rank)
+    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234 + rank)
     log(f"world={world} batch/GPU={B} dtype={head_dt}")
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
@@ -243,6 +271,9 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
                 "hipgraph": not a.no_graph and cuda,
+                "runtime": "serialized engine (ONNX com.amd.dft nodes, save/load, hipGraph replay)"
+                if eng_info.get("engine") else "captured nn.Module",
+                "engine_bytes": eng_info.get("engine_bytes"),
                 "output_allgather": gathered,
                 "gather_backend": ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()) if world > 1 else None,
                 "gemm": "hipblaslt" if gemm_table or (cuda and not mlp_on_hand_gemm()) else "hand-mfma",

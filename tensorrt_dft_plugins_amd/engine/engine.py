@@ -136,7 +136,11 @@ class Engine:
             if inputs is None:
                 raise ValueError("building from a module needs example inputs")
             ins = tuple(inputs) if isinstance(inputs, (list, tuple)) else (inputs,)
-            onnx_bytes = onnx_export.export(source, tuple(i.cpu() for i in ins), opset_version=opset_version)
+            # trace where the module lives: a GPU-resident model exports by running its forward on
+            # the MI355X kernels (a full-size FourCastNet traced on the CPU takes minutes)
+            prm = next(iter(source.parameters()), None)
+            tdev = prm.device if prm is not None else torch.device("cpu")
+            onnx_bytes = onnx_export.export(source, tuple(i.to(tdev) for i in ins), opset_version=opset_version)
             shapes = shapes or [list(i.shape) for i in ins]
             dtypes = dtypes or [i.dtype for i in ins]
         else:

@@ -105,11 +105,17 @@ def pack_afno_weights(w1, b1, w2, b2, split: bool = False) -> Tuple[torch.Tensor
     return w1t, w2t, b1p, b2p
 
 
+# (H, block size) instances of the fused AFNO kernel; mirrors afno_spectral_supported() in
+# csrc/spectral/afno_spectral.hip (checked equal in tests/test_models.py).  Kept in Python so
+# the check stays a constant under ONNX/TorchScript tracing (an op returning bool cannot be traced).
+AFNO_FUSED_SHAPES = frozenset({(90, 96)})
+
+
 def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:
     if not x.is_cuda:
         return False
-    B, H, W, C = x.shape
-    return bool(_ops().afno_spectral_supported(H, C // num_blocks))
+    B, H, W, C = (int(d) for d in x.shape)
+    return (H, C // int(num_blocks)) in AFNO_FUSED_SHAPES
 
 
 def afno_spectral_h(xw: torch.Tensor, w1, b1, w2, b2, num_blocks: int, lam: float, owner=None) -> torch.Tensor:
@@ -180,7 +186,7 @@ def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
     c = f.cfg
     if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.shape[-1] % 8 == 0):
         return False
-    B, H, W, C = x.shape
+    B, H, W, C = (int(d) for d in x.shape)
     r0, r1, km = kept_window(H, W, c.hard_thresholding_fraction)
     if x.dtype == torch.float32 and not (C % 256 == 0 and (4 * C) % 256 == 0):
         return False  # the bf16x3 MLP GEMMs tile 256 features
@@ -209,7 +215,7 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     f = blk.filter
     c = f.cfg
     n1 = blk.norm1
-    B, H, W, C = xs.shape
+    B, H, W, C = (int(d) for d in xs.shape)  # static ints (constants under tracing)
     _, _, km = kept_window(H, W, c.hard_thresholding_fraction)
     scale = 1.0 / math.sqrt(H * W)
     ops = _ops()
@@ -253,7 +259,7 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     f = blk.filter
     c = f.cfg
     n1, n2, m = blk.norm1, blk.norm2, blk.mlp
-    B, H, W, C = xs.shape
+    B, H, W, C = (int(d) for d in xs.shape)  # static ints (constants under tracing)
     _, _, km = kept_window(H, W, c.hard_thresholding_fraction)
     scale = 1.0 / math.sqrt(H * W)
     ops = _ops()

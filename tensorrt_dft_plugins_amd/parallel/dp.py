@@ -69,7 +69,7 @@ def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_
 class DataParallelInference:
     """Overlapped batch-DP inference of a static-shape module (per-rank shard = ``example``)."""
 
-    def __init__(self, module: torch.nn.Module, example: torch.Tensor, *, gather: bool = True,
+    def __init__(self, module, example: torch.Tensor, *, gather: bool = True,
                  use_graph: bool = True, warmup: int = 2):
         self.rank, self.world = world_info()
         self.gather = gather and self.world > 1

@@ -124,3 +124,62 @@ def test_engine_from_fast_models_gpu(device, tmp_path):
     Engine.build(afno.cpu(), (xa,), device=device).save(p)
     (ya,) = Engine.load(p, device=device).infer(xa.to(device))
     assert torch.allclose(ya, refa, atol=1e-3)
+
+
+class _Rfft2(nn.Module):
+    def forward(self, x):
+        return ex.OnnxRfft2.apply(x)
+
+
+class _Irfft2(nn.Module):
+    def forward(self, x):
+        return ex.OnnxIrfft2.apply(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["rfft2", "irfft2"])
+@pytest.mark.parametrize("dft_dim1", [1, 2])
+@pytest.mark.parametrize("dft_dim2", [4])
+@pytest.mark.parametrize("num_c", [1, 3])
+@pytest.mark.parametrize("batch_size", [1, 2])
+def test_reference_grid_through_engine_gpu(device, tmp_path, op, dft_dim1, dft_dim2, num_c, batch_size):
+    """The reference's 16 cases (/root/reference/tests/test_dft.py:124-184) on the GPU through
+    export -> Engine.build (hipGraph) -> save -> load -> execute_v2(device pointers)."""
+    torch.manual_seed(1)
+    x = torch.randn(batch_size, num_c, dft_dim1, dft_dim2)
+    if op == "rfft2":
+        model, inp = _Rfft2(), x
+        expected = torch.view_as_real(torch.fft.rfft2(x, dim=(-2, -1), norm="backward"))
+    else:
+        inp = torch.view_as_real(torch.fft.rfft2(x))
+        model = _Irfft2()
+        expected = torch.fft.irfft2(torch.view_as_complex(inp), dim=(-2, -1))
+    p = str(tmp_path / f"{op}.engine")
+    Engine.build(model, (inp,), device=device).save(p)
+    eng = Engine.load(p, device=device)
+    assert eng.use_graph and eng._cuda_graph is not None
+    xin = inp.to(device)
+    out = torch.empty(eng.bindings[-1].shape, device=device)
+    assert eng.execute_v2([xin.data_ptr(), out.data_ptr()])
+    assert torch.allclose(out.cpu(), expected, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fourcastnet_full_grid_engine_gpu(device, tmp_path, dtype):
+    """FourCastNet at the full 720x1440 grid (depth 2) exported with its com.amd.dft nodes,
+    saved, loaded and replayed from the engine file: matches the captured module."""
+    from tensorrt_dft_plugins_amd.engine.capture import CapturedModule
+    from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+    from helpers import rel_l2
+
+    torch.manual_seed(3)
+    m = AFNONet(AFNOConfig(depth=2), backend="amd").to(device).to(dtype).eval()
+    x = torch.randn(2, 20, 720, 1440, device=device).to(dtype)
+    (ref,) = CapturedModule(m, [x]).replay()
+    p = str(tmp_path / "fcn.engine")
+    Engine.build(m, (x,), device=device).save(p)
+    eng = Engine.load(p, device=device)
+    (y,) = eng.infer(x)
+    assert y.dtype == dtype and y.shape == ref.shape
+    assert rel_l2(y.float(), ref.float()) < (1e-5 if dtype == torch.float32 else 1e-2)

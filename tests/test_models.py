@@ -82,3 +82,11 @@ def test_layer_norm_op_cpu():
 def test_fourcastnet_flops():
     f = flops_per_sample(AFNOConfig())
     assert 1.8e12 < f < 2.1e12  # ~2.0 TFLOP/sample
+
+
+def test_afno_fused_shape_table_matches_native():
+    from tensorrt_dft_plugins_amd.ops.spectral import AFNO_FUSED_SHAPES
+
+    for H in (45, 90, 180):
+        for bs in (48, 64, 96, 128):
+            assert bool(torch.ops.amd_dft.afno_spectral_supported(H, bs)) == ((H, bs) in AFNO_FUSED_SHAPES)
