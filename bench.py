@@ -172,7 +172,8 @@ def build_runner(cfg, dtype, B, dev, a, seed):
         log(f"{dtype}: engine exported, serialized ({len(blob) / 1e6:.0f} MB) and deserialized in "
             f"{info['engine_build_load_s']}s")
     t0 = time.perf_counter()
-    runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph)
+    runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph,
+                                   gather_backend=a.gather)
     log(f"{dtype}: captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t0:.1f}s")
     return info, runner
 
@@ -190,6 +191,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-engine", dest="engine", action="store_false",
                     help="capture the nn.Module directly instead of the serialized engine")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather", choices=["rccl", "ipc"], default=os.environ.get("MI_DFT_GATHER", "rccl"),
+                    help="output all-gather: RCCL ring collective or direct IPC pushes over xGMI")
     ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 / FNO block probes")
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
     ap.add_argument("--json-out", default=None)
@@ -275,7 +278,8 @@ def main(argv=None) -> int:
                 if eng_info.get("engine") else "captured nn.Module",
                 "engine_bytes": eng_info.get("engine_bytes"),
                 "output_allgather": gathered,
-                "gather_backend": ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()) if world > 1 else None,
+                "gather_backend": (a.gather if a.gather == "ipc" else ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()))
+                if world > 1 and gathered else None,
                 "gemm": "hipblaslt" if gemm_table or (cuda and not mlp_on_hand_gemm()) else "hand-mfma",
                 "gemm_precision": "bf16x3 split, fp32 accumulate" if head_dt == torch.float32 else "bf16, fp32 accumulate",
                 "gemm_table": gemm_table,

@@ -24,20 +24,32 @@ from tensorrt_dft_plugins_amd.parallel import all_gather_batch, init_distributed
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=float, nargs="+", default=[1, 4, 16, 64, 166, 332, 1327])
-    ap.add_argument("--op", default="all_gather", choices=["all_gather", "all_to_all"])
+    ap.add_argument("--op", default="all_gather", choices=["all_gather", "all_to_all", "ipc_gather"],
+                    help="ipc_gather: direct pushes into every peer's buffer (parallel/ipc_gather.py)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args(argv)
     gpu = torch.cuda.is_available()
-    init_distributed("nccl" if gpu else "gloo")
+    # MI_DFT_DIST_BACKEND=gloo rehearses several ranks on one GPU (RCCL refuses that)
+    init_distributed(os.environ.get("MI_DFT_DIST_BACKEND") or ("nccl" if gpu else "gloo"))
     rank, world = world_info()
     local = int(os.environ.get("LOCAL_RANK", 0))
-    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    dev = torch.device("cuda", local % torch.cuda.device_count()) if gpu else torch.device("cpu")
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     es = torch.finfo(dt).bits // 8
     for mb in a.mb:
         n = max(1, int(mb * 1e6 / es))
-        if a.op == "all_to_all":  # n elements per peer block
+        if a.op == "ipc_gather":  # direct-mesh pushes + host handshake + IPC events
+            from tensorrt_dft_plugins_amd.parallel import IpcAllGather
+
+            x = torch.randn(n, device=dev).to(dt)
+            ig = IpcAllGather([n], dt, dev, nbuf=2)
+            it = {"k": 0}
+
+            def coll():
+                ig.gather(x, it["k"])
+                it["k"] += 1
+        elif a.op == "all_to_all":  # n elements per peer block
             x = torch.randn(world * n, device=dev).to(dt)
             out = torch.empty(world * n, device=dev, dtype=dt)
 
@@ -77,7 +89,7 @@ def main(argv=None):
             print(json.dumps({"op": a.op, "world": world, "dtype": a.dtype, "shard_MB": round(n * es / 1e6, 3), "ms": round(ms, 4),
                               "algbw_GBps": round(total / (ms * 1e-3) / 1e9, 2),
                               "busbw_GBps": round((world - 1) / world * total / (ms * 1e-3) / 1e9, 2),
-                              "backend": dist.get_backend()}), flush=True)
+                              "backend": "ipc" if a.op == "ipc_gather" else dist.get_backend()}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

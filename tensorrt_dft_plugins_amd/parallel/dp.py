@@ -67,12 +67,20 @@ def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_
 
 
 class DataParallelInference:
-    """Overlapped batch-DP inference of a static-shape module (per-rank shard = ``example``)."""
+    """Overlapped batch-DP inference of a static-shape module (per-rank shard = ``example``).
+
+    ``gather_backend``: ``"rccl"`` (``all_gather_into_tensor``; Gloo on CPU) or ``"ipc"`` (direct
+    pushes into every peer's buffer over xGMI, :mod:`.ipc_gather`); default from
+    ``MI_DFT_GATHER``, else rccl.
+    """
 
     def __init__(self, module, example: torch.Tensor, *, gather: bool = True,
-                 use_graph: bool = True, warmup: int = 2):
+                 use_graph: bool = True, warmup: int = 2, gather_backend: Optional[str] = None):
         self.rank, self.world = world_info()
         self.gather = gather and self.world > 1
+        self.gather_backend = (gather_backend or os.environ.get("MI_DFT_GATHER", "rccl")).lower()
+        if self.gather_backend not in ("rccl", "ipc"):
+            raise ValueError(f"gather_backend must be 'rccl' or 'ipc', got {self.gather_backend!r}")
         self.cap = CapturedModule(module, [example], warmup=warmup, n_graphs=2 if self.gather else 1,
                                   use_graph=use_graph)
         self.device = example.device
@@ -81,11 +89,20 @@ class DataParallelInference:
         self.full: List[Optional[torch.Tensor]] = [None, None]
         self.works: List[Optional[object]] = [None, None]
         self.events = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
+        self.done = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
+        self.done_pending = [False, False]
+        self.ipc = None
         if self.gather:
             o = self.cap.outputs[0][0]
-            for i in range(2):
-                self.full[i] = torch.empty((self.world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
-                                           device=o.device)
+            if self.gather_backend == "ipc":
+                from .ipc_gather import IpcAllGather
+
+                self.ipc = IpcAllGather(list(o.shape), o.dtype, o.device, nbuf=2)
+                self.full = list(self.ipc.full)
+            else:
+                for i in range(2):
+                    self.full[i] = torch.empty((self.world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
+                                               device=o.device)
         self.k = 0
 
     @property
@@ -99,9 +116,23 @@ class DataParallelInference:
         if self.gather and self.works[i] is not None:
             self.works[i].wait()  # stream-ordered: compute waits until the old gather read out[i]
             self.works[i] = None
+        if self.cuda and self.done_pending[i]:
+            torch.cuda.current_stream(self.device).wait_event(self.done[i])  # old push has read out[i]
+            self.done_pending[i] = False
         out = self.cap.replay(i)[0]
         if not self.gather:
             return out
+        if self.ipc is not None:
+            if self.cuda:
+                self.events[i].record()
+                with torch.cuda.stream(self.comm_stream):
+                    self.comm_stream.wait_event(self.events[i])
+                    self.ipc.gather(out, i)
+                    self.done[i].record(self.comm_stream)
+                self.done_pending[i] = True
+            else:
+                self.ipc.gather(out, i)
+            return self.full[i]
         if self.cuda:
             self.events[i].record()
             with torch.cuda.stream(self.comm_stream):

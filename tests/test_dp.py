@@ -18,15 +18,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, device="cpu"):
+def _worker(rank, world, port, q, device="cpu", backend="rccl"):
     try:
-        _worker_body(rank, world, port, q, device)
+        _worker_body(rank, world, port, q, device, backend)
     except BaseException as e:  # surface failures instead of a queue timeout
         q.put((rank, repr(e), None))
         raise
 
 
-def _worker_body(rank, world, port, q, device="cpu"):
+def _worker_body(rank, world, port, q, device="cpu", backend="rccl"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
@@ -40,26 +40,29 @@ def _worker_body(rank, world, port, q, device="cpu"):
     cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
     model = AFNONet(cfg, backend="amd").eval().to(device)
     g = torch.Generator().manual_seed(100 + rank)
-    x = torch.randn(2, cfg.in_chans, *cfg.img_size, generator=g).to(device)
-    dp = DataParallelInference(model, x, gather=True, use_graph=device != "cpu")
+    xs = [torch.randn(2, cfg.in_chans, *cfg.img_size, generator=g).to(device) for _ in range(3)]
+    dp = DataParallelInference(model, xs[0], gather=True, use_graph=device != "cpu", gather_backend=backend)
     outs = []
-    for _ in range(3):
+    for k in range(3):  # a different input per step and rank: slot / ordering mix-ups show
+        dp.inputs.copy_(xs[k])
         outs.append(dp.step())
     dp.drain()
-    full = outs[-1].clone().cpu()
+    if device != "cpu":
+        torch.cuda.synchronize()
+    full = [outs[1].clone().cpu(), outs[2].clone().cpu()]  # slots of steps 1 and 2
     with torch.no_grad():
-        local = model(x).cpu()
+        local = [model(xs[1]).cpu(), model(xs[2]).cpu()]
     q.put((rank, full, local))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_dp(device):
+def _run_dp(device, backend="rccl"):
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, device)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, device, backend)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -70,21 +73,27 @@ def _run_dp(device):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    expected = torch.cat([res[r][1] for r in range(world)], 0)
-    for r in range(world):
-        assert res[r][0].shape == expected.shape
-        assert torch.allclose(res[r][0], expected, atol=1e-5)
+    for step in (0, 1):
+        expected = torch.cat([res[r][1][step] for r in range(world)], 0)
+        for r in range(world):
+            assert res[r][0][step].shape == expected.shape
+            assert torch.allclose(res[r][0][step], expected, atol=1e-5), (r, step)
 
 
-def test_dp_allgather_gloo_world2():
-    _run_dp("cpu")
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_dp_allgather_gloo_world2(backend):
+    """CPU, Gloo, world 2: the RCCL-path collective (Gloo all_gather) and the direct-push IPC
+    protocol (/dev/shm transport: same slot / offset / handshake logic as the GPU transport)."""
+    _run_dp("cpu", backend)
 
 
 @pytest.mark.gpu
-def test_dp_allgather_gloo_world2_on_one_gpu():
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_dp_allgather_gloo_world2_on_one_gpu(backend):
     """Two ranks share the one GPU (Gloo; RCCL refuses duplicate devices): hipGraph replays on
-    two output buffers, the gather on the communication stream, event/stream ordering."""
-    _run_dp("cuda")
+    two output buffers, the gather on the communication stream, event/stream ordering.  ``ipc``:
+    real hipIpc memory + event handles across the two processes, direct pushes."""
+    _run_dp("cuda", backend)
 
 
 def test_bench_harness_torchrun_gloo():
