@@ -9,8 +9,8 @@
 //   _ipc_mem_handle / _ipc_open_mem / _ipc_close_mem      hipIpc{Get,Open,Close}MemHandle
 //   _ipc_event_*    inter-process events (hipEventInterprocess): record on the producer's
 //                   stream, hipStreamWaitEvent on the consumer's
-//   _ipc_push       hipMemcpyAsync of one source to N destination pointers on the current
-//                   stream (peer copies over xGMI; the copy engines run them concurrently)
+//   _ipc_push       one kernel copying a source to N destination pointers concurrently on
+//                   the current stream (peer stores over xGMI, one link per destination)
 // Names start with '_' so they are never exported into ONNX graphs (raw device pointers).
 // The reference has no multi-GPU path at all ("assuming single GPU",
 // /root/reference/src/dft_plugins/dft_plugins.cpp:341).
@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include "../parallel/ipc_push.h"
+
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -102,16 +105,29 @@ void ipc_stream_wait(int64_t ev, int64_t device) {
 
 void ipc_event_destroy(int64_t ev) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)); }
 
-// src -> every dst_ptrs[i] + offset (bytes), stream-ordered on the current stream
+// src -> every dst_ptrs[i] + offset (bytes), stream-ordered on the current stream: one kernel,
+// all destinations concurrently (csrc/parallel/ipc_push.hip); hipMemcpyAsync fallback for
+// unaligned sizes
 void ipc_push(const at::Tensor& src, at::IntArrayRef dst_ptrs, int64_t offset) {
   TORCH_CHECK(src.is_cuda() && src.is_contiguous(), "amd_dft._ipc_push: src must be a contiguous device tensor");
+  TORCH_CHECK(!dst_ptrs.empty() && dst_ptrs.size() <= static_cast<size_t>(kIpcMaxDst), "amd_dft._ipc_push: 1..16 destinations");
   auto st = c10::hip::getCurrentHIPStream(src.device().index()).stream();
-  const size_t n = static_cast<size_t>(src.numel()) * src.element_size();
-  for (int64_t p : dst_ptrs) {
-    TORCH_CHECK(p != 0, "amd_dft._ipc_push: null destination");
-    hip_ok(hipMemcpyAsync(reinterpret_cast<char*>(p) + offset, src.data_ptr(), n, hipMemcpyDeviceToDevice, st),
-           "_ipc_push");
+  const int64_t n = src.numel() * src.element_size();
+  IpcPushDsts d{};
+  for (size_t i = 0; i < dst_ptrs.size(); ++i) {
+    TORCH_CHECK(dst_ptrs[i] != 0, "amd_dft._ipc_push: null destination");
+    d.ptr[i] = reinterpret_cast<void*>(dst_ptrs[i]);
   }
+  const bool aligned = n % 16 == 0 && offset % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                       std::all_of(dst_ptrs.begin(), dst_ptrs.end(), [](int64_t p) { return p % 16 == 0; });
+  if (aligned) {
+    launch_ipc_push(src.data_ptr(), n, d, static_cast<int>(dst_ptrs.size()), offset, st);
+    return;
+  }
+  for (int64_t p : dst_ptrs)
+    hip_ok(hipMemcpyAsync(reinterpret_cast<char*>(p) + offset, src.data_ptr(), static_cast<size_t>(n),
+                          hipMemcpyDeviceToDevice, st),
+           "_ipc_push");
 }
 
 }  // namespace

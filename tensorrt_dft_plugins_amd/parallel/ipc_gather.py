@@ -7,8 +7,9 @@ concurrent copies, one per link, each moving one shard (ring: ~7 x shard / link 
 mesh: ~1 x shard / link bandwidth, derived in SURVEY §5.8).
 
 Protocol per step (buffer slot ``i`` of ``nbuf``, all on the caller's current stream):
-  1. push: ``hipMemcpyAsync`` of the local shard into slot ``i`` of every rank's buffer (peer
-     pointers from ``hipIpcOpenMemHandle``), at byte offset ``rank * shard_bytes``;
+  1. push: one kernel (csrc/parallel/ipc_push.hip) stores the local shard into slot ``i`` of every
+     rank's buffer at once (peer pointers from ``hipIpcOpenMemHandle``; one xGMI link per peer),
+     at byte offset ``rank * shard_bytes``;
   2. record this rank's inter-process event ``i`` after the pushes;
   3. host handshake: a barrier on a Gloo group -- afterwards every producer has ENQUEUED its
      pushes and its event record for this step (the host never waits for the GPU);
