@@ -26,12 +26,16 @@
 //
 // fp32 mode (SPLIT, "bf16x3"): fp32 operands are carried as bf16 pairs a = a_hi + a_lo
 // (a_hi = bf16(a), a_lo = bf16(a - a_hi); 16 significant bits) and the product is
-// A_hi.B_hi + A_lo.B_hi + A_hi.B_lo with fp32 accumulation -- 3 K-segments of the same
-// pipeline (the K loop runs over 3K; each K-tile's source half is remapped in the DMA
-// address).  Relative error ~5e-6 per GEMM (fp32 FMA: ~3e-7, bf16: ~3e-3) at 3x the bf16
-// MFMA work, vs 16x for the exact-f32 MFMA (v_mfma_f32_16x16x4_f32 runs at 1/16 of the bf16
-// rate on gfx950).  Operand rows are [hi(K) | lo(K)]; outputs are fp32 (OUT 1) or a split
-// pair row [hi(N) | lo(N)] ready to be the next GEMM's operand (OUT 2).
+// A_hi.B_hi + A_lo.B_hi + A_hi.B_lo with fp32 accumulation: relative error ~5e-6 per GEMM
+// (fp32 FMA: ~3e-7, bf16: ~3e-3) at 3x the bf16 MFMA work, vs 16x for the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32 runs at 1/16 of the bf16 rate on gfx950).  Operand rows use the
+// k32-interleaved split layout: every 32-deep k chunk is stored as [hi(32) | lo(32)]
+// (physical column (k / 32) * 64 + part * 32 + k % 32, row length 2K), so a 128-byte region
+// row of the pipeline below holds hi AND lo of one 32-deep K-tile: the same DMA, LDS images
+// and fragment reads as the bf16 kernel (its k-step 0 / 1 fragments become the hi / lo
+// fragments) feed 24 MFMAs per phase instead of 16 -- 2x the bf16 loads for 3x the MFMAs.
+// Outputs: fp32 (OUT 1) or a split pair row in the same layout (OUT 2), ready to be the
+// next GEMM's operand.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -101,17 +105,9 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
                                              int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
   char* dst = stage + REG * kRegion;
-  // SPLIT: K-tile kt of the 3K loop = segment seg (0: hi.hi, 1: lo.hi, 2: hi.lo) of logical
-  // K-tile kl; operand rows are [hi | lo] (row stride 2K), the gathered image has a lo plane
-  int64_t ld = K, wcol = 0, xcol = 0;
-  if constexpr (SPLIT) {
-    const int KT0 = static_cast<int>(K / kBK);
-    const int seg = kt >= 2 * KT0 ? 2 : (kt >= KT0 ? 1 : 0);
-    kt -= seg * KT0;
-    ld = 2 * K;
-    wcol = seg == 2 ? K : 0;
-    xcol = seg == 1 ? (MODE == 1 ? p.x_lo : K) : 0;
-  }
+  // SPLIT: K-tile kt = logical k [32 kt, 32 kt + 32); its hi and lo halves are adjacent in the
+  // k32-interleaved rows (row stride 2K), so the physical 64-element column block is kt * 64
+  const int64_t ld = SPLIT ? 2 * K : K;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int rb = (wave * 2 + i) * 8;
@@ -120,11 +116,16 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
     const int tr = region_row<REG>(row);
     const uint16_t* g;
     if constexpr (REG == 0 || REG == 3) {
-      g = W + static_cast<int64_t>(f0 + tr) * ld + wcol + kt * kBK + chunk * 8;
+      g = W + static_cast<int64_t>(f0 + tr) * ld + kt * kBK + chunk * 8;
     } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
-      g = X + xcol + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
+      if constexpr (SPLIT) {  // channel kt / 2, patch rows (kt & 1) * 4 + c % 4 of the hi / lo plane
+        const int py = (kt & 1) * 4 + (chunk & 3);
+        g = X + (chunk >= 4 ? p.x_lo : 0) + (gb[REG - 1][i] + ((kt >> 1) * (p.gh * 8) + py) * (p.gw * 8));
+      } else {
+        g = X + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
+      }
     } else {
-      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * ld + xcol + kt * kBK + chunk * 8;
+      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * ld + kt * kBK + chunk * 8;
     }
     __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
   }
@@ -151,17 +152,24 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
       b[s * 2 + j] = *reinterpret_cast<const bf16x8*>(base + swz(wc * 32 + j * 16 + r16, s * 4 + kq));
 }
 
-template <int MI, int NI>
+// bf16: k-steps 0 and 1.  SPLIT: fragments [0..3] / [4..7] of A and [0..1] / [2..3] of B are
+// the hi / lo halves of one 32-deep K-tile: hi.hi + lo.hi + hi.lo, products outermost so
+// consecutive MFMAs never chain on one accumulator
+template <int MI, int NI, bool SPLIT>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
   __builtin_amdgcn_s_setprio(1);
+  constexpr int NP = SPLIT ? 3 : 2;
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < NP; ++s)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[MI * 4 + i][NI * 2 + j] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s * 4 + i], b[s * 2 + j], acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        const int sa = SPLIT ? (s == 1 ? 1 : 0) : s;  // SPLIT products: (hi, hi), (lo, hi), (hi, lo)
+        const int sb = SPLIT ? (s == 2 ? 1 : 0) : s;
+        acc[MI * 4 + i][NI * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[sa * 4 + i], b[sb * 2 + j],
+                                                                                acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
+      }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -193,8 +201,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
   const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
   const int f0 = ft * kBF, t0 = tt * kBT;
-  const int KT = (SPLIT ? 3 : 1) * (K / kBK);
-  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && (K / kBK) * kBK == K && KT > 0, "gemm_bf16_kernel");
+  const int KT = SPLIT ? K / 32 : K / kBK;  // SPLIT: 32-deep logical K-tiles (hi | lo = 64 elements)
+  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && (SPLIT ? (K / 32) * 32 : (K / kBK) * kBK) == K && KT > 0,
+                    "gemm_bf16_kernel");
   const int r16 = lane & 15, kq = lane >> 4;
 
   f32x4 acc[8][4];
@@ -254,7 +263,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 0>(acc, a0, b0);
+    mfma_quadrant<0, 0, SPLIT>(acc, a0, b0);
     barrier();
     // ---- phase 1: (0, 1)
     wait_regions(issued(P - 1) + issued(P));
@@ -262,7 +271,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 1>(acc, a0, b1);
+    mfma_quadrant<0, 1, SPLIT>(acc, a0, b1);
     barrier();
     // ---- phase 2: (1, 1)
     wait_regions(issued(P) + issued(P + 1));
@@ -270,7 +279,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 1>(acc, a1, b1);
+    mfma_quadrant<1, 1, SPLIT>(acc, a1, b1);
     barrier();
     // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
     wait_regions(issued(P + 1) + issued(P + 2));
@@ -278,7 +287,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 0>(acc, a1, b0);
+    mfma_quadrant<1, 0, SPLIT>(acc, a1, b0);
     barrier();
   }
   if (wr == 0) barrier();  // re-align the two wave groups
@@ -347,13 +356,13 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       }
       if constexpr (OUT == 1) {
         *reinterpret_cast<float4*>(static_cast<float*>(p.y) + off) = make_float4(v[0], v[1], v[2], v[3]);
-      } else if constexpr (OUT == 2) {  // split pair row [hi(N) | lo(N)]
+      } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
         float lo[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
-        uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + f;
+        uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 + (f & 31);
         *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
-        *reinterpret_cast<uint2*>(yr + N) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
+        *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
       } else {
         *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
       }
@@ -409,6 +418,8 @@ void throw_last(const char* what) {
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   return M >= 1 && N % kBF == 0 && K % kBK == 0 && K >= kBK && M < (int64_t(1) << 31) && N * K < (int64_t(1) << 31);
 }
+// logical K of a split (bf16x3) GEMM: 32-deep K-tiles, at least 2 (the pipeline prologue)
+static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
 
 // MI_DFT_GEMM=4w selects the four-wave 128x128-per-wave kernel (gemm4w.hip) where it applies;
 // default: the 8-wave ping-pong kernel below, measured faster on the FourCastNet shapes
@@ -433,6 +444,7 @@ void launch_gemm(const GemmLaunch& p, void* stream) {
   if (p.out < 0 || p.out > 2 || (p.out != 0) != (p.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
   if (p.split && p.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
+  if (p.split && !split_k_ok(p.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);

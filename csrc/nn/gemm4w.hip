@@ -302,8 +302,9 @@ void dispatch_out(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 }  // namespace
 
 bool gemm4w_applicable(const GemmLaunch& p) {
-  return p.gC == 0 && p.sC == 0 && p.ln_stats == nullptr && p.N % kBF == 0 && p.K % kBK == 0 && p.K >= kBK &&
-         p.M >= 1 && !(p.out == 2 && p.residual);
+  // bf16 operands only (the split rows use gemm.hip's k32-interleaved layout)
+  return p.split == 0 && p.gC == 0 && p.sC == 0 && p.ln_stats == nullptr && p.N % kBF == 0 && p.K % kBK == 0 &&
+         p.K >= kBK && p.M >= 1;
 }
 
 void launch_gemm4w(const GemmLaunch& p, void* stream) {

@@ -246,20 +246,32 @@ at::Tensor linear_meta(const at::Tensor& x, const at::Tensor& w, const c10::opti
 
 // ------------------------------------------------------------------ bf16x3 (fp32-class) GEMMs
 // An fp32 operand is carried as a bf16 pair a = hi + lo (hi = bf16(a), lo = bf16(a - hi)):
-// split_bf16 packs rows as [..., 2K] = [hi(K) | lo(K)] (rows=true) or planes [2, ...] (rows=false).
+// split_bf16 packs rows as [..., 2K] k32-interleaved (every 32 columns [hi(32) | lo(32)],
+// rows=true) or planes [2, ...] (rows=false).
 // linear3 / patch_linear3 / linear_unpatch3 take split operands and run the 3-product GEMM
 // (csrc/nn/gemm.hip SPLIT mode) with fp32 accumulation and fp32 (or split-pair) outputs.
+// k32-interleaved split rows: every 32 columns c.. stored as [hi(32) | lo(32)]
 at::Tensor unsplit_rows(const at::Tensor& xs) {
   const int64_t K2 = xs.size(-1);
-  TORCH_CHECK(K2 % 2 == 0, "amd_dft: split rows must have an even last dim");
-  return xs.narrow(-1, 0, K2 / 2).to(at::kFloat) + xs.narrow(-1, K2 / 2, K2 / 2).to(at::kFloat);
+  TORCH_CHECK(K2 % 64 == 0, "amd_dft: split rows must have a last dim that is a multiple of 64");
+  std::vector<int64_t> s(xs.sizes().begin(), xs.sizes().end() - 1);
+  std::vector<int64_t> v = s;
+  v.insert(v.end(), {K2 / 64, 2, 32});
+  s.push_back(K2 / 2);
+  return xs.to(at::kFloat).reshape(v).sum(-2).reshape(s);
 }
 
 at::Tensor split_ref(const at::Tensor& x, bool rows) {
   at::Tensor xf = x.to(at::kFloat);
   at::Tensor hi = xf.to(at::kBFloat16);
   at::Tensor lo = (xf - hi.to(at::kFloat)).to(at::kBFloat16);
-  return rows ? at::cat({hi, lo}, -1).contiguous() : at::stack({hi, lo}, 0).contiguous();
+  if (!rows) return at::stack({hi, lo}, 0).contiguous();
+  const int64_t K = x.size(-1);
+  TORCH_CHECK(K % 32 == 0, "amd_dft.split_bf16: rows need a last dim that is a multiple of 32");
+  std::vector<int64_t> v(x.sizes().begin(), x.sizes().end() - 1), o = v;
+  v.insert(v.end(), {K / 32, 32});
+  o.push_back(2 * K);
+  return at::cat({hi.reshape(v), lo.reshape(v)}, -1).reshape(o).contiguous();
 }
 
 at::Tensor split_bf16_cpu(const at::Tensor& x, bool rows) { return split_ref(x, rows); }
@@ -270,7 +282,8 @@ at::Tensor split_bf16_cuda(const at::Tensor& x_, bool rows) {
   TORCH_CHECK(x_.dim() >= 1, "amd_dft.split_bf16: x must have at least one dim");
   at::Tensor x = x_.contiguous();
   const int64_t cols = x.size(-1);
-  TORCH_CHECK(x.numel() % 8 == 0 && (!rows || cols % 8 == 0), "amd_dft.split_bf16: needs multiples of 8 elements");
+  TORCH_CHECK(x.numel() % 8 == 0 && (!rows || cols % 32 == 0),
+              "amd_dft.split_bf16: needs multiples of 8 elements (rows: a last dim that is a multiple of 32)");
   std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
   if (rows) os.back() = 2 * cols;
   else os.insert(os.begin(), 2);

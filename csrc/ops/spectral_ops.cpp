@@ -41,10 +41,10 @@ at::Tensor afno_spectral_cpu(const at::Tensor& xw, const at::Tensor& w1t, const 
   at::Tensor X = at::fft_fft(at::view_as_complex(xw.to(at::kFloat).contiguous()), std::nullopt, 1, "backward");
   at::Tensor Xr = at::view_as_real(X).reshape({B, H, KM, NB, BS, 2});
   at::Tensor A = at::cat({Xr.select(-1, 0), Xr.select(-1, 1)}, -1);  // [..., NB, 2BS]
-  auto unsplit = [&](const at::Tensor& w) {
+  auto unsplit = [&](const at::Tensor& w) {  // k32-interleaved split rows -> fp32
     if (w.size(2) == w.size(1)) return w.to(at::kFloat);
     const int64_t k = w.size(1);
-    return w.narrow(2, 0, k).to(at::kFloat) + w.narrow(2, k, k).to(at::kFloat);
+    return w.to(at::kFloat).reshape({w.size(0), w.size(1), k / 32, 2, 32}).sum(3).reshape({w.size(0), w.size(1), k});
   };
   at::Tensor W1 = unsplit(w1t).transpose(1, 2);                      // [NB, k, n]
   at::Tensor W2 = unsplit(w2t).transpose(1, 2);
@@ -352,15 +352,21 @@ at::Tensor layer_norm_split_cpu(const at::Tensor& x, const at::Tensor& w, const 
   if (pre.has_value()) xf = xf + pre->to(at::kFloat);
   at::Tensor y = at::layer_norm(xf, {x.size(-1)}, w.to(at::kFloat), b.to(at::kFloat), eps);
   at::Tensor hi = y.to(at::kBFloat16);
-  return at::cat({hi, (y - hi.to(at::kFloat)).to(at::kBFloat16)}, -1).contiguous();
+  at::Tensor lo = (y - hi.to(at::kFloat)).to(at::kBFloat16);
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 32 == 0, "amd_dft.layer_norm_split: C must be a multiple of 32");
+  std::vector<int64_t> v(x.sizes().begin(), x.sizes().end() - 1), o = v;
+  v.insert(v.end(), {C / 32, 32});
+  o.push_back(2 * C);
+  return at::cat({hi.reshape(v), lo.reshape(v)}, -1).reshape(o).contiguous();  // k32-interleaved
 }
 
 at::Tensor layer_norm_split_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& b_, double eps,
                                  const std::optional<at::Tensor>& pre_) {
   const c10::DeviceGuard guard(x_.device());
   const int64_t C = x_.size(-1);
-  TORCH_CHECK(x_.scalar_type() == at::kFloat && C % 4 == 0 && C <= 2048,
-              "amd_dft.layer_norm_split: x must be float32 with C % 4 == 0 and C <= 2048");
+  TORCH_CHECK(x_.scalar_type() == at::kFloat && C % 32 == 0 && C <= 2048,
+              "amd_dft.layer_norm_split: x must be float32 with C % 32 == 0 and C <= 2048");
   TORCH_CHECK(w_.numel() == C && b_.numel() == C && (!pre_.has_value() || pre_->numel() == C),
               "amd_dft.layer_norm_split: weight/bias/pre must have C entries");
   at::Tensor x = x_.contiguous();

@@ -417,20 +417,21 @@ __device__ __forceinline__ void gemm_96x192_x3(const uint16_t* __restrict__ Ah, 
 #pragma unroll
     for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 bh[2][3], bl[2][3];
+  // split weight rows are k32-interleaved: k-step ks (32 deep) = [hi(32) | lo(32)] at ks * 64
 #pragma unroll
   for (int nj = 0; nj < 3; ++nj) {
     const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + kq * 8;
     bh[0][nj] = *reinterpret_cast<const bf16x8*>(row);
-    bl[0][nj] = *reinterpret_cast<const bf16x8*>(row + kK);
+    bl[0][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
   }
 #pragma unroll
   for (int ks = 0; ks < 6; ++ks) {
     if (ks + 1 < 6) {
 #pragma unroll
       for (int nj = 0; nj < 3; ++nj) {
-        const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + (ks + 1) * 32 + kq * 8;
+        const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + (ks + 1) * 64 + kq * 8;
         bh[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row);
-        bl[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row + kK);
+        bl[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
       }
     }
 #pragma unroll

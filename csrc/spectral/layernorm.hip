@@ -292,11 +292,12 @@ __global__ void __launch_bounds__(64 * kWaves) ln_f32_kernel(const float* __rest
     o[1] = (v[c][1] - mean) * rstd * g4.y + b4.y;
     o[2] = (v[c][2] - mean) * rstd * g4.z + b4.z;
     o[3] = (v[c][3] - mean) * rstd * g4.w + b4.w;
-    if constexpr (SPLIT) {
-      uint16_t* yr = static_cast<uint16_t*>(y) + row * (2 * cols);
+    if constexpr (SPLIT) {  // k32-interleaved pair row: column c -> (c / 32) * 64 + part * 32 + c % 32
+      const int c = ch * 4;
+      uint16_t* yr = static_cast<uint16_t*>(y) + row * (2 * cols) + (c >> 5) * 64 + (c & 31);
       const uint32_t h0 = bfpack(o[0], o[1]), h1 = bfpack(o[2], o[3]);
-      *reinterpret_cast<uint2*>(yr + ch * 4) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(yr + cols + ch * 4) = make_uint2(bfpack_lo(o[0], o[1], h0), bfpack_lo(o[2], o[3], h1));
+      *reinterpret_cast<uint2*>(yr) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(yr + 32) = make_uint2(bfpack_lo(o[0], o[1], h0), bfpack_lo(o[2], o[3], h1));
     } else {
       *reinterpret_cast<float4*>(static_cast<float*>(y) + row * cols + ch * 4) = make_float4(o[0], o[1], o[2], o[3]);
     }
@@ -320,7 +321,8 @@ void launch_f32(const float* x, const float* pre, const float* g, const float* b
 }
 
 // ---- fp32 -> bf16 split pairs (hi = bf16(x), lo = bf16(x - hi)), 8 elements per thread.
-// ROWS: row-major [rows, cols] -> [rows, 2 cols] rows [hi | lo]; else planes [2, n] (hi, lo).
+// ROWS: row-major [rows, cols] -> [rows, 2 cols] k32-interleaved pair rows (every 32 columns
+// stored as [hi(32) | lo(32)], the bf16x3 GEMM operand layout); else planes [2, n] (hi, lo).
 template <bool ROWS>
 __global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
                                                          int64_t n, int cols) {
@@ -332,10 +334,11 @@ __global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict
   const uint4 hi = make_uint4(h0, h1, h2, h3);
   const uint4 lo = make_uint4(bfpack_lo(a.x, a.y, h0), bfpack_lo(a.z, a.w, h1), bfpack_lo(c.x, c.y, h2),
                               bfpack_lo(c.z, c.w, h3));
-  if constexpr (ROWS) {
+  if constexpr (ROWS) {  // k32-interleaved pair rows (8 elements never straddle a 32-chunk)
     const int64_t r = i / cols, col = i - r * cols;
-    *reinterpret_cast<uint4*>(y + r * 2 * cols + col) = hi;
-    *reinterpret_cast<uint4*>(y + r * 2 * cols + cols + col) = lo;
+    uint16_t* yr = y + r * 2 * cols + (col >> 5) * 64 + (col & 31);
+    *reinterpret_cast<uint4*>(yr) = hi;
+    *reinterpret_cast<uint4*>(yr + 32) = lo;
   } else {
     *reinterpret_cast<uint4*>(y + i) = hi;
     *reinterpret_cast<uint4*>(y + n + i) = lo;
@@ -377,6 +380,7 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
   if (!p.bf16) {
     if (p.residual || p.cols % 4 != 0 || p.cols > 64 * 4 * 8)
       throw std::runtime_error("amd_dft: layernorm: fp32 rows need cols % 4 == 0, <= 2048, no residual");
+    if (p.split_out && p.cols % 32 != 0) throw std::runtime_error("amd_dft: layernorm: split output needs cols % 32 == 0");
     const auto* x = static_cast<const float*>(p.x);
     const auto* g = static_cast<const float*>(p.gamma);
     const auto* b = static_cast<const float*>(p.beta);
@@ -399,7 +403,8 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
 }
 
 void launch_split_bf16(const float* x, uint16_t* y, int64_t n, int cols, bool rows, void* stream) {
-  if (n % 8 != 0 || (rows && cols % 8 != 0)) throw std::runtime_error("amd_dft: split_bf16: needs 8-element multiples");
+  if (n % 8 != 0 || (rows && cols % 32 != 0))
+    throw std::runtime_error("amd_dft: split_bf16: needs 8-element multiples (rows: cols % 32 == 0)");
   if (n == 0) return;
   const dim3 grid(static_cast<uint32_t>((n / 8 + 255) / 256));
   if (rows) hipLaunchKernelGGL(split_bf16_kernel<true>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), x, y, n, cols);

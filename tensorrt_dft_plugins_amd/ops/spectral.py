@@ -33,7 +33,7 @@ from . import dft as D
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
            "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
            "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
-           "fallback_counts", "fallback_reset"]
+           "fallback_counts", "fallback_reset", "unsplit_bf16"]
 
 
 def _ops():
@@ -71,14 +71,16 @@ def fallback_reset() -> None:
 
 
 def split_bf16(t: torch.Tensor, rows: bool = True) -> torch.Tensor:
-    """fp32 -> bf16 pair (hi = bf16(t), lo = bf16(t - hi)): rows [..., 2K] = [hi | lo], or planes
-    [2, ...] (``rows=False``)."""
-    if t.is_cuda:
-        return _ops().split_bf16(t.float().contiguous(), rows)
-    t = t.float()
-    hi = t.to(torch.bfloat16)
-    lo = (t - hi.float()).to(torch.bfloat16)
-    return torch.cat([hi, lo], -1) if rows else torch.stack([hi, lo], 0)
+    """fp32 -> bf16 pair (hi = bf16(t), lo = bf16(t - hi)): rows [..., 2K] k32-interleaved (every
+    32 columns stored as [hi(32) | lo(32)], the bf16x3 GEMM operand layout), or planes [2, ...]
+    (``rows=False``)."""
+    return _ops().split_bf16(t.float().contiguous(), rows)
+
+
+def unsplit_bf16(ts: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``split_bf16(rows=True)``: [..., 2K] k32-interleaved pairs -> fp32 [..., K]."""
+    k2 = ts.shape[-1]
+    return ts.float().reshape(*ts.shape[:-1], k2 // 64, 2, 32).sum(-2).reshape(*ts.shape[:-1], k2 // 2)
 
 
 def _real_block(w: torch.Tensor) -> torch.Tensor:

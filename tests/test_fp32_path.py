@@ -10,6 +10,7 @@ import torch.nn.functional as F
 from helpers import rel_l2
 from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
 from tensorrt_dft_plugins_amd.ops import spectral as S
+from tensorrt_dft_plugins_amd.ops.spectral import unsplit_bf16
 
 ops = torch.ops.amd_dft
 
@@ -20,17 +21,26 @@ def _split_ref(x):
     return hi, lo
 
 
+def _halves(s):
+    """k32-interleaved pair rows [..., 2K] -> (hi [..., K], lo [..., K])"""
+    v = s.reshape(*s.shape[:-1], s.shape[-1] // 64, 2, 32)
+    return v[..., 0, :].reshape(*s.shape[:-1], -1), v[..., 1, :].reshape(*s.shape[:-1], -1)
+
+
 # ------------------------------------------------------------------ CPU semantics
 def test_split_bf16_cpu_roundtrip():
     torch.manual_seed(0)
     x = torch.randn(6, 64) * 3
     s = ops.split_bf16(x, True)
     assert s.shape == (6, 128) and s.dtype == torch.bfloat16
-    back = s[:, :64].float() + s[:, 64:].float()
+    back = unsplit_bf16(s)
     assert rel_l2(back, x) < 2e-5  # 16 significant bits
     p = ops.split_bf16(x, False)
     assert p.shape == (2, 6, 64)
-    assert torch.equal(p[0], s[:, :64]) and torch.equal(p[1], s[:, 64:])
+    hi, lo = _halves(s)
+    assert torch.equal(p[0], hi) and torch.equal(p[1], lo)
+    # layout: every 32 columns stored as [hi(32) | lo(32)]
+    assert torch.equal(s[:, 32:64], p[1][:, :32]) and torch.equal(s[:, 64:96], p[0][:, 32:])
 
 
 def test_split_ops_meta_shapes():
@@ -50,7 +60,7 @@ def test_linear3_cpu_semantics():
     assert rel_l2(y, F.gelu(F.linear(x, w, b)) + r) < 3e-5
     ys = ops.linear3(xs, ws, b, 0, None, True)
     assert ys.shape == (9, 512)
-    assert rel_l2(ys[:, :256].float() + ys[:, 256:].float(), F.linear(x, w, b)) < 3e-5
+    assert rel_l2(unsplit_bf16(ys), F.linear(x, w, b)) < 3e-5
 
 
 def test_linear3_rejects_bad_bias():
@@ -112,7 +122,7 @@ def test_linear3_gpu_vs_fp32(device, M, N, K, act, bias, res, split_out):
     y = ops.linear3(xs, ws, None if b is None else b.to(device), act, None if r is None else r.to(device), split_out)
     if split_out:
         assert y.shape == (M, 2 * N) and y.dtype == torch.bfloat16
-        y = y[:, :N].float() + y[:, N:].float()
+        y = unsplit_bf16(y)
     else:
         assert y.shape == (M, N) and y.dtype == torch.float32
     assert rel_l2(y.cpu(), ref) < 2e-5  # bf16x3: ~5e-6 (bf16 alone: ~3e-3)
@@ -143,10 +153,10 @@ def test_split_and_layernorm_fp32_gpu(device):
     pre = torch.randn(768) * 0.2
     s = ops.split_bf16(x.to(device), True).cpu()
     hi, lo = _split_ref(x)
-    assert torch.equal(s[:, :768], hi) and torch.equal(s[:, 768:], lo)
+    assert torch.equal(_halves(s)[0], hi) and torch.equal(_halves(s)[1], lo)
     ref = F.layer_norm(x + pre, (768,), g, b, 1e-6)
     ys = ops.layer_norm_split(x.to(device), g.to(device), b.to(device), 1e-6, pre.to(device)).cpu()
-    assert rel_l2(ys[:, :768].float() + ys[:, 768:].float(), ref) < 2e-5
+    assert rel_l2(unsplit_bf16(ys), ref) < 2e-5
     y, _ = ops.layer_norm(x.to(device), g.to(device), b.to(device), 1e-6, None)
     assert y.dtype == torch.float32 and rel_l2(y.cpu(), F.layer_norm(x, (768,), g, b, 1e-6)) < 1e-6
     st = ops.ln_stats(x.to(device), pre.to(device), 1e-6).cpu()
