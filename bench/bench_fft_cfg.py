@@ -1,4 +1,5 @@
-"""rfft2 / irfft2 720x1440 latency per column-pass tile config (MI_DFT_FIXED_CFG), one process."""
+"""rfft2 / irfft2 720x1440 latency per column-pass tile config (MI_DFT_FIXED_CFG) and XCD-aware
+tile order (MI_DFT_FFT_XCD), one process, interleaved."""
 import json
 import os
 import sys
@@ -12,13 +13,21 @@ from bench.bench_fft import time_graph  # noqa: E402
 tdp.load_plugins()
 x = torch.randn(1, 720, 1440, device="cuda")
 y = tdp.contrib_rfft(x, signal_ndim=2)
-for cfg in ["auto", "90,2", "90,4", "90,8", "45,4", "45,8", "45,16"]:
-    if cfg == "auto":
-        os.environ.pop("MI_DFT_FIXED_CFG", None)
-    else:
-        os.environ["MI_DFT_FIXED_CFG"] = cfg
-    f1 = lambda: tdp.contrib_rfft(x, signal_ndim=2)  # noqa: E731
-    f2 = lambda: tdp.contrib_irfft(y, signal_ndim=2)  # noqa: E731
-    f1(), f2()
-    r = {"rfft2": min(time_graph(f1, 50) for _ in range(5)), "irfft2": min(time_graph(f2, 50) for _ in range(5))}
-    print(cfg, json.dumps({k: round(v, 2) for k, v in r.items()}), flush=True)
+cfgs = sys.argv[1:] or ["auto", "90,2", "90,4", "90,8", "45,4", "45,8", "45,16"]
+res = {}
+for _ in range(3):
+    for cfg in cfgs:
+        for xcd in ("0", "1"):
+            os.environ["MI_DFT_FFT_XCD"] = xcd
+            if cfg == "auto":
+                os.environ.pop("MI_DFT_FIXED_CFG", None)
+            else:
+                os.environ["MI_DFT_FIXED_CFG"] = cfg
+            f1 = lambda: tdp.contrib_rfft(x, signal_ndim=2)  # noqa: E731
+            f2 = lambda: tdp.contrib_irfft(y, signal_ndim=2)  # noqa: E731
+            f1(), f2()
+            r = res.setdefault((cfg, xcd), {"rfft2": [], "irfft2": []})
+            r["rfft2"].append(time_graph(f1, 50))
+            r["irfft2"].append(time_graph(f2, 50))
+for (cfg, xcd), r in res.items():
+    print(f"cfg={cfg:6s} xcd={xcd}", json.dumps({k: round(min(v), 2) for k, v in r.items()}), flush=True)

@@ -2,6 +2,7 @@
 // selection (kernels: fft_fixed_impl.h, instantiated in fft_fixed_{c2c,r2c,c2r}.hip).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -66,11 +67,13 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     // C2R with fused addends prefers 32-channel tiles, the R2C 16 (wider R2C tiles lose).
     const int t_pref = (cols && d.kind == Kind::R2C) ? 16 : 1 << 30;
     const double tw = c.T <= t_pref ? c.T : -c.T;
-    // Small problems (rfft2 720x1440 column pass: 721 columns): wide column tiles win over
-    // occupancy as long as ~one wave per SIMD remains (bench/bench_fft_cfg.py: T=8 15.8 us,
-    // T=2 19.8 us, T=16 17.7 us with only 552 waves).
+    // Small problems (rfft2 720x1440 column pass: 721 columns): with the XCD-aware tile order
+    // (tiles sharing a 128-B line run on one XCD, see xcd_block) 4-column tiles win
+    // (bench/bench_fft_cfg.py, rfft2/irfft2 us: T=4 12.85/13.2, T=2 13.1/13.8, T=8 13.7/13.9;
+    // profiles/fft_xcd_r2.txt).
+    const double tmid = cols ? -std::abs(c.T - 4) : tw;
     const double score = waves >= 2048 ? 1e12 + tw * 1e6 + c.TP
-                         : waves >= 1000 ? 1e9 + tw * 1e3 + c.TP
+                         : waves >= 1000 ? 1e9 + tmid * 1e3 + c.TP
                                          : static_cast<double>(waves);
     if (score > best_score) {
       best_score = score;
@@ -123,6 +126,17 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
   const int64_t nblocks = d.O * a.tiles_per_outer;
   if (nblocks <= 0) return true;
   if (nblocks > 0x7fffffffLL) throw std::runtime_error("amd_dft: FFT grid too large");
+  {
+    // XCD-aware tile order for column layouts whose tile row is narrower than a 128-B line
+    // (MI_DFT_FFT_XCD=0/1 forces it off/on for A/B runs)
+    const int eb = a.bf16_in ? 2 : 4;
+    const int64_t row_bytes = static_cast<int64_t>(cfg.T) * 2 * eb;  // complex or paired-real elements
+    bool on = cfg.cols && row_bytes < 128 && nblocks >= 16;
+    if (const char* xe = std::getenv("MI_DFT_FFT_XCD")) on = std::atoi(xe) != 0;
+    a.xcd_nb = on ? static_cast<int32_t>(nblocks) : 0;
+    const char* ab = std::getenv("MI_DFT_FFT_ABLATE");
+    a.ablate = ab ? std::atoi(ab) : 0;
+  }
   LaunchFn fn = d.kind == Kind::C2C ? c2c_launcher(best) : (d.kind == Kind::R2C ? r2c_launcher(best) : c2r_launcher(best));
   fn(a, dim3(static_cast<uint32_t>(nblocks)), static_cast<hipStream_t>(stream));
   hipError_t err = hipGetLastError();

@@ -28,6 +28,8 @@ struct FixedArgs {
   int64_t So_in, So_out;              // outer offsets (64-bit, applied once per block)
   int32_t I, Si_in, Si_out, Sn_in, Sn_out;  // per-element offsets fit 32 bits (host-checked)
   int32_t in_lo, in_hi, out_lo, out_hi, tiles_per_outer;
+  int32_t xcd_nb;    // > 0: XCD-aware remap of the nb = xcd_nb blocks (see xcd_block)
+  int32_t ablate;    // timing ablations (MI_DFT_FFT_ABLATE, wrong results): 2 = no twiddles, 4 = no butterflies
   float scale;
   int32_t inverse, vec_in, vec_out, bf16_in, bf16_out;
   const void* add1;  // C2R epilogue: out = scale * irfft + add1 (+ add2); same layout/dtype as out
@@ -38,7 +40,18 @@ struct FixedArgs {
   const float* ln_gamma;
   const float* ln_beta;
   const float* ln_pre;
+#ifdef AMD_DFT_FFT_STAMPS
+  long long* stamps;  // diagnostic build only (bench/fft_stamps.hip): per-block phase clocks
+#endif
 };
+
+#ifdef AMD_DFT_FFT_STAMPS
+// slot 0: s_memrealtime at entry, 1..: s_memtime after each phase (vector store by thread 0)
+#define AMD_DFT_STAMP(a, slot, v) \
+  do { if (threadIdx.x == 0) (a).stamps[static_cast<int64_t>(blockIdx.x) * 16 + (slot)] = (v); } while (0)
+#else
+#define AMD_DFT_STAMP(a, slot, v) do { } while (0)
+#endif
 
 template <int... Rs>
 struct FL {
@@ -262,6 +275,7 @@ template <class F, int TP, int P>
 __device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, TP, P>::Q][PassGeom<F, TP, P>::TWR]) {
   using G = PassGeom<F, TP, P>;
   if constexpr (G::Ns > 1) {
+    if (x.a.ablate & 2) return;
 #pragma unroll
     for (int q = 0; q < G::Q; ++q) {
       const int j = x.tp + q * TP;
@@ -289,9 +303,11 @@ struct Step {
       float2 twn[GN::Q][GN::TWR];
       load_tw<F, TP, P + 1>(x, twn);
       body(x, tw);
+      AMD_DFT_STAMP(x.a, 3 + P, static_cast<long long>(__builtin_amdgcn_s_memtime()));
       Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR, NADD, PV>::run(x, twn);
     } else {
       body(x, tw);
+      AMD_DFT_STAMP(x.a, 3 + P, static_cast<long long>(__builtin_amdgcn_s_memtime()));
     }
   }
 
@@ -329,10 +345,12 @@ struct Step {
       const int j = x.tp + q * TP;
       if (G::EXACT || j < LR) {
         if constexpr (Ns > 1) {
+          if (!(x.a.ablate & 2)) {
 #pragma unroll
-          for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[q][r - 1]);
+            for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[q][r - 1]);
+          }
         }
-        Dft<R>::run(v[q]);
+        if (!(x.a.ablate & 4)) Dft<R>::run(v[q]);
       }
     }
     // ---- scatter
@@ -364,6 +382,15 @@ struct Step {
   }
 };
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its
+// own L2.  Column tiles narrower than a 128-B line share lines with their neighbours; the remap
+// gives every XCD one contiguous range of tiles so those neighbours meet in the same L2
+// instead of each XCD fetching the whole line.  Bijective for any nb.
+__device__ __forceinline__ int32_t xcd_block(int32_t b, int32_t nb) {
+  const int32_t per = nb >> 3, rem = nb & 7, xcd = b & 7, k = b >> 3;
+  return (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + k;
+}
+
 template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>
 __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   constexpr int L = F::L;
@@ -374,8 +401,10 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   const int tid = threadIdx.x;
   x.t = COLS ? tid % T : tid / TP;
   x.tp = COLS ? tid / T : tid % TP;
-  const int32_t o = blockIdx.x / a.tiles_per_outer;
-  const int32_t tile = blockIdx.x - o * a.tiles_per_outer;
+  const int32_t bid = a.xcd_nb > 0 ? xcd_block(static_cast<int32_t>(blockIdx.x), a.xcd_nb)
+                                   : static_cast<int32_t>(blockIdx.x);
+  const int32_t o = bid / a.tiles_per_outer;
+  const int32_t tile = bid - o * a.tiles_per_outer;
   x.c = tile * T + x.t;
   if constexpr (K == Kind::C2C) {
     x.ok0 = x.c < a.I;
@@ -403,6 +432,8 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
     x.pre = a.ln_pre ? *reinterpret_cast<const float2*>(a.ln_pre + ch) : make_float2(0.f, 0.f);
   }
   x.lds = lds;
+  AMD_DFT_STAMP(a, 0, static_cast<long long>(__builtin_amdgcn_s_memrealtime()));
+  AMD_DFT_STAMP(a, 1, static_cast<long long>(__builtin_amdgcn_s_memtime()));
   using G0 = PassGeom<F, TP, 0>;
   float2 tw0[G0::Q][G0::TWR];
   Step<K, COLS, TP, T, F, 0, BFI, BFO, PR, NADD, PV>::run(x, tw0);
@@ -432,11 +463,14 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
       }
     }
   }
+  AMD_DFT_STAMP(a, 2, static_cast<long long>(__builtin_amdgcn_s_memtime()));
+  AMD_DFT_STAMP(a, 8, static_cast<long long>(__builtin_amdgcn_s_memrealtime()));
 }
 
 // ------------------------------------------------------------------ config table
 #define AMD_DFT_FIXED_CONFIGS(X)          \
   X(1440, false, 144, 1, 10, 12, 12)      \
+  X(1440, false, 128, 1, 10, 12, 12)      \
   X(720, false, 90, 2, 8, 9, 10)          \
   X(1024, false, 128, 1, 8, 8, 16)        \
   X(2048, false, 256, 1, 8, 16, 16)       \
@@ -448,6 +482,7 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \
   X(720, true, 45, 16, 8, 9, 10)          \
+  X(720, true, 64, 4, 8, 9, 10)           \
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)            \
   X(180, true, 15, 32, 12, 15)
