@@ -65,7 +65,8 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   at::Tensor b1 = b1_.to(at::kFloat).contiguous(), b2 = b2_.to(at::kFloat).contiguous();
   const int64_t B = xw.size(0), H = xw.size(1), KM = xw.size(2), C = xw.size(3), NB = w1t.size(0);
   TORCH_CHECK(afno_spectral_supported(static_cast<int>(H), static_cast<int>(C / NB)),
-              "afno_spectral: fused kernel supports H == 90 and block size 96 (use the generic path)");
+              "afno_spectral: no fused instance for H = ", H, ", block size ", C / NB,
+              " (afno_spectral_shapes() lists them; use the generic path)");
   const bool x3 = w1t.size(2) == 2 * w1t.size(1);
   TORCH_CHECK(!x3 || xw.scalar_type() == at::kFloat, "afno_spectral: split (bf16x3) weights go with a float32 spectrum");
   at::Tensor y = at::empty_like(xw);
@@ -81,6 +82,9 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   p.b1 = b1.data_ptr<float>();
   p.b2 = b2.data_ptr<float>();
   p.tw = dp->tw.data_ptr();
+  TORCH_CHECK(dp->plan.radices.size() == 2, "afno_spectral: H = ", H, " is not a two-pass plan");
+  p.r0 = dp->plan.radices[0];
+  p.r1 = dp->plan.radices[1];
   p.B = static_cast<int>(B);
   p.H = static_cast<int>(H);
   p.KM = static_cast<int>(KM);
@@ -89,6 +93,15 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   p.lambda = static_cast<float>(lam);
   launch_afno_spectral(p, c10::hip::getCurrentHIPStream(xw.device().index()).stream());
   return checked(y, "afno_spectral");
+}
+
+std::vector<int64_t> afno_spectral_shape_list() {  // flattened (H, block size) pairs
+  std::vector<int64_t> v;
+  for (const auto& hb : afno_spectral_shapes()) {
+    v.push_back(hb.first);
+    v.push_back(hb.second);
+  }
+  return v;
 }
 
 bool afno_spectral_ok(int64_t H, int64_t block_size) {
@@ -452,6 +465,7 @@ at::Tensor afno_spectral_meta(const at::Tensor& xw, const at::Tensor&, const at:
 TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral(Tensor x, Tensor w1t, Tensor w2t, Tensor b1, Tensor b2, float lam) -> Tensor");
   m.def("afno_spectral_supported(int H, int block_size) -> bool", &amd_dft::afno_spectral_ok);
+  m.def("afno_spectral_shapes() -> int[]", &amd_dft::afno_spectral_shape_list);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
   m.def("layer_norm_split(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? pre=None) -> Tensor");

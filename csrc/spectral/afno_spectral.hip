@@ -11,23 +11,31 @@
 // barrier-separated; a standalone LDS-isolation test of co-resident workgroups is clean), so
 // the -O2 code generation is the suspect; the unit is kept at -O1 until that is isolated.
 //
-// One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H (=90),
-// c < 96, complex fp32, produced by the W-direction R2C pass.  In one launch it runs
-//   FFT_H (Stockham [9,10], register first pass)  ->
+// One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
+// c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
+//   FFT_H (two-pass Stockham [R0, R1] = the plan order of H, register first pass)  ->
 //   O1 = ReLU([Xr|Xi] . W1' + b1')  (bf16 MFMA 16x16x32, fp32 accumulate)  ->
 //   O2 = O1 . W2' + b2'  -> softshrink(lambda)  ->
 //   IFFT_H (register last pass, stored straight to global)
-// where W' = [[W0, W1], [-W1, W0]] is the real 192x192 form of the complex 96x96 block weight
-// (pre-packed transposed, [n][k], so a lane's B fragment is 16 contiguous bytes).
-// Everything between the global load and the global store stays in 38 KB of LDS (fp16 FFT
-// staging aliased with the bf16 GEMM tile) and in registers (3 workgroups / CU); the reference FourCastNet path is ~10 separate kernels with
-// 4 spectrum round trips through HBM.
+// where W' = [[W0, W1], [-W1, W0]] is the real 2BS x 2BS form of the complex BS x BS block
+// weight (pre-packed transposed, [n][k], so a lane's B fragment is 16 contiguous bytes).
+// Everything between the global load and the global store stays in LDS (fp16 FFT staging
+// aliased with the bf16 GEMM tile: 38 KB at H = 90, BS = 96, 3 workgroups / CU) and in
+// registers; the reference FourCastNet path is ~10 separate kernels with 4 spectrum round
+// trips through HBM.
+//
+// Instances (AFNO_SHAPES below): H in {45 = 9x5, 64 = 16x4, 90 = 9x10} (FourCastNet at patch
+// 16 / square 512-pixel grids / patch 8) x block size in {64, 96, 128}.  The GEMMs are
+// [16 MT x 2BS] = A . W' with MT = ceil(H / 16) row tiles (rows >= H are padding whose outputs
+// are discarded) and 2BS / 16 column tiles over the 4 waves.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../fft/dev_check.h"
 #include "../fft/radix.h"
@@ -39,16 +47,24 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNT = 256;      // threads
-constexpr int kBS = 96;       // channels per AFNO block
-constexpr int kK = 2 * kBS;   // real-block GEMM K = N = 192
-constexpr int kAPitch = kK + 8;
+constexpr int kNT = 256;  // threads
 #ifndef AFNO_BPF
 #define AFNO_BPF 2  // k-steps of B-fragment prefetch in the block-MLP GEMMs
 #endif
-#ifndef AFNO_OCC
-#define AFNO_OCC 3  // workgroups (waves) per SIMD the register budget is sized for
-#endif  // bf16 elements per A row (+16 B pad: ds_read_b128 spread)
+
+// Compile-time geometry of one instance: H = L = R0 x R1, block size BS.
+template <int L_, int R0_, int R1_, int BS_>
+struct AfnoShape {
+  static constexpr int L = L_, R0 = R0_, R1 = R1_, BS = BS_;
+  static constexpr int NP = BS / 2;       // channel pairs per row
+  static constexpr int K = 2 * BS;        // real-block GEMM K = N
+  static constexpr int APitch = K + 8;    // bf16 elements per A row (+16 B: ds_read_b128 spread)
+  static constexpr int MT = (L + 15) / 16;  // GEMM row tiles (rows >= L are padding)
+  static constexpr int NTW = BS / 32;     // 16-wide column tiles per wave (2BS / 16 over 4 waves)
+  static constexpr int KS = BS / 16;      // 32-deep k-steps
+  static constexpr int OCC = BS <= 96 ? 3 : 2;  // workgroups per SIMD the bf16 register budget targets
+  static_assert(R0 * R1 == L && BS % 32 == 0 && L <= 128, "AFNO instance geometry");
+};
 
 __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 
@@ -56,12 +72,6 @@ __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(
 // 2).  fp16 keeps 11 significant bits (the GEMM operands downstream are bf16, 8 bits); the
 // spectra of the AFNO filter stay orders of magnitude inside fp16 range.
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_h(h2_t* p, int i, float2 v) { p[i] = h2_t{static_cast<_Float16>(v.x), static_cast<_Float16>(v.y)}; }
-__device__ __forceinline__ float2 ld_h(const h2_t* p, int i) {
-  const h2_t h = p[i];
-  return make_float2(static_cast<float>(h[0]), static_cast<float>(h[1]));
-}
-
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 // two adjacent channels' complex values (fp16 LDS staging)
 __device__ __forceinline__ void st_hp(h2_t* p, int i, const cpair& v) {
@@ -96,46 +106,26 @@ __device__ __forceinline__ void stc2(void* p, int off, float2 a, float2 b) {
   }
 }
 
-template <bool BF>
-__device__ __forceinline__ float2 ldc(const void* p, int64_t off) {  // off in scalars
-  if constexpr (BF) {
-    const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(p) + off);
-    return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
-  } else {
-    return *reinterpret_cast<const float2*>(static_cast<const float*>(p) + off);
-  }
-}
-template <bool BF>
-__device__ __forceinline__ void stc(void* p, int64_t off, float2 v) {
-  if constexpr (BF) {
-    *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(p) + off) =
-        static_cast<uint32_t>(f2bf16(v.x)) | (static_cast<uint32_t>(f2bf16(v.y)) << 16);
-  } else {
-    *reinterpret_cast<float2*>(static_cast<float*>(p) + off) = v;
-  }
-}
-
-// Stockham pass over 96 interleaved signals in LDS (layout [n][96]) with register staging:
+// Stockham pass over BS interleaved signals in LDS (layout [n][BS]) with register staging:
 // gather -> barrier -> twiddle/DFT -> scatter.  A work item is one butterfly of a PAIR of
 // adjacent channels (8-byte global / LDS accesses, twiddles shared by the pair), held as a
 // cpair (radix.h) so every butterfly op is one packed fp32 instruction for both channels.
-constexpr int kNP = kBS / 2;  // channel pairs per row
-template <int R, int L>
+template <int R, int L, int NP>
 struct HPass {
   static constexpr int LR = L / R;
-  static constexpr int NB = LR * kNP;
+  static constexpr int NB = LR * NP;
   static constexpr int Q = (NB + kNT - 1) / kNT;
 };
 
-template <int R, int L, int Ns, int Q>
+template <int R, int L, int NP, int Ns, int Q>
 __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
-  using P = HPass<R, L>;
+  using P = HPass<R, L, NP>;
   static_assert(P::Q == Q, "pass geometry");
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int b = threadIdx.x + q * kNT;
     if (P::NB % kNT == 0 || b < P::NB) {
-      const int j = b / kNP;
+      const int j = b / NP;
       if constexpr (Ns > 1) {
         const int k = j % Ns;
 #pragma unroll
@@ -152,71 +142,72 @@ __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __
 struct AfnoArgs {
   const void* x;        // [B, H, KM, C, 2] fp32 or bf16
   void* y;              // [B, H, KM, C, 2] fp32 or bf16
-  const uint16_t* w1t;  // [NB][192][192] bf16, [n][k]
+  const uint16_t* w1t;  // [NB][2BS][2BS] bf16, [n][k]  (x3: [NB][2BS][2 * 2BS] split rows)
   const uint16_t* w2t;
-  const float* b1;      // [NB][192]
+  const float* b1;      // [NB][2BS]
   const float* b2;
-  const float2* tw;     // plan twiddles for length H ([9,10] order)
+  const float2* tw;     // plan twiddles for length H ([R0, R1] order)
   int KM, C, NB, H;
   float lambda;
 };
 
-// GEMM [96 x 192] = A (LDS bf16, pitch kAPitch) x Bt^T (global bf16 [n][k]); wave w owns
-// N-tiles 3w..3w+2 for all 6 M-tiles.
-__device__ __forceinline__ void gemm_96x192(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                                            f32x4 (&acc)[6][3]) {
+// GEMM [16 MT x 2BS] = A (LDS bf16, pitch APitch) x Bt^T (global bf16 [n][k]); wave w owns
+// column tiles NTW w .. NTW w + NTW - 1 for all MT row tiles.
+template <class S>
+__device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                                          f32x4 (&acc)[S::MT][S::NTW]) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
 #pragma unroll
-  for (int mi = 0; mi < 6; ++mi)
+  for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 72 VGPRs)
-  constexpr int D = AFNO_BPF, NQ = AFNO_BPF + 1;
-  bf16x8 bq[NQ][3];
+    for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 24 KS VGPRs)
+  constexpr int D = AFNO_BPF < S::KS ? AFNO_BPF : S::KS - 1, NQ = D + 1;
+  bf16x8 bq[NQ][S::NTW];
 #pragma unroll
   for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
-    for (int nj = 0; nj < 3; ++nj)
-      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + s2 * 32 + kq * 8);
+    for (int nj = 0; nj < S::NTW; ++nj)
+      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + ((S::NTW * w + nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
 #pragma unroll
-  for (int ks = 0; ks < 6; ++ks) {
-    if (ks + D < 6) {
+  for (int ks = 0; ks < S::KS; ++ks) {
+    if (ks + D < S::KS) {
 #pragma unroll
-      for (int nj = 0; nj < 3; ++nj)
+      for (int nj = 0; nj < S::NTW; ++nj)
         bq[(ks + D) % NQ][nj] =
-            *reinterpret_cast<const bf16x8*>(Bt + ((3 * w + nj) * 16 + r16) * kK + (ks + D) * 32 + kq * 8);
+            *reinterpret_cast<const bf16x8*>(Bt + ((S::NTW * w + nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
     }
-    bf16x8 afr[6];
+    bf16x8 afr[S::MT];
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
-      afr[mi] = *reinterpret_cast<const bf16x8*>(A + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
+    for (int mi = 0; mi < S::MT; ++mi)
+      afr[mi] = *reinterpret_cast<const bf16x8*>(A + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
+    for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
-      for (int nj = 0; nj < 3; ++nj)
+      for (int nj = 0; nj < S::NTW; ++nj)
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
   }
 }
 
-template <int L, int R0, int R1, bool BFI, bool BFO>
-__global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const AfnoArgs a) {
-  static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
-  extern __shared__ __attribute__((aligned(16))) h2_t lds[];  // [L][96] complex fp16 (34.5 KB at L=90)
-  uint16_t* A = reinterpret_cast<uint16_t*>(lds);             // aliases lds: [96][kAPitch] bf16 (38.4 KB)
+template <class S, bool BFI, bool BFO>
+__global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoArgs a) {
+  constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
+  extern __shared__ __attribute__((aligned(16))) h2_t lds[];  // [L][BS] complex fp16
+  uint16_t* A = reinterpret_cast<uint16_t*>(lds);             // aliases lds: [16 MT][APitch] bf16
   const int tid = threadIdx.x;
   const int blk = blockIdx.x % a.NB;
   const int bk = blockIdx.x / a.NB;  // b * KM + kw
   const int kw = bk % a.KM;
   const int b = bk / a.KM;
-  AMD_DFT_DEV_CHECK((blk + 1) * kBS <= a.C && kw < a.KM && L == a.H, "afno_spectral_kernel");
+  AMD_DFT_DEV_CHECK((blk + 1) * BS <= a.C && kw < a.KM && L == a.H, "afno_spectral_kernel");
   const int row_stride = a.KM * a.C * 2;  // scalars between consecutive h (host-checked: 32-bit offsets)
-  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
+  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * BS) * 2;
   const void* xin = static_cast<const char*>(a.x) + base * (BFI ? 2 : 4);
   void* yout = static_cast<char*>(a.y) + base * (BFO ? 2 : 4);
-  using P0 = HPass<R0, L>;
-  using P1 = HPass<R1, L>;
+  using P0 = HPass<R0, L, NP>;
+  using P1 = HPass<R1, L, NP>;
 
   // ---------------- forward FFT_H: pass 0 straight from global
   {
@@ -226,7 +217,7 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
       const int bb = tid + q * kNT;
       const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
       const int bc = ok ? bb : 0;
-      const int tp = bc % kNP, j = bc / kNP;
+      const int tp = bc % NP, j = bc / NP;
 #pragma unroll
       for (int r = 0; r < R0; ++r) {
         float2 c0, c1;
@@ -234,91 +225,92 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
         v[q][r] = make_cpair(c0, c1);
       }
     }
-    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
   __syncthreads();
-  // ---------------- pass 1: LDS -> registers -> A (bf16, [h][re 0..95 | im 96..191])
+  // ---------------- pass 1: LDS -> registers -> A (bf16, [h][re 0..BS-1 | im BS..2BS-1])
   {
     cpair v[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;  // last pass: outputs at n = j + r * R0
+        const int tp = bb % NP, j = bb / NP;  // last pass: outputs at n = j + r * R0
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          uint32_t* row = reinterpret_cast<uint32_t*>(A + n * kAPitch);
+          uint32_t* row = reinterpret_cast<uint32_t*>(A + n * AP);
           row[tp] = static_cast<uint32_t>(f2bf16(v[q][r].re[0])) | (static_cast<uint32_t>(f2bf16(v[q][r].re[1])) << 16);
-          row[kNP + tp] = static_cast<uint32_t>(f2bf16(v[q][r].im[0])) | (static_cast<uint32_t>(f2bf16(v[q][r].im[1])) << 16);
+          row[NP + tp] = static_cast<uint32_t>(f2bf16(v[q][r].im[0])) | (static_cast<uint32_t>(f2bf16(v[q][r].im[1])) << 16);
         }
       }
     }
   }
+  // rows L..16 MT - 1 of A (GEMM M padding) are never written: their outputs are discarded
   __syncthreads();
   // ---------------- GEMM1 + bias + ReLU -> H1 (bf16, in place of A)
   const int lane = tid & 63, w = tid >> 6;
-  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * kK * kK;
-  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * kK * kK;
-  const float* b1 = a.b1 + blk * kK;
-  const float* b2 = a.b2 + blk * kK;
-  f32x4 acc[6][3];
-  gemm_96x192(A, w1t, acc);
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * K;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * K;
+  const float* b1 = a.b1 + blk * K;
+  const float* b2 = a.b2 + blk * K;
+  f32x4 acc[S::MT][S::NTW];
+  gemm_tile<S>(A, w1t, acc);
   __syncthreads();
 #pragma unroll
-  for (int nj = 0; nj < 3; ++nj) {
-    const int n = (3 * w + nj) * 16 + (lane & 15);
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b1[n];
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
+    for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mi * 16 + 4 * (lane >> 4) + i;
-        A[m * kAPitch + n] = f2bf16(fmaxf(acc[mi][nj][i] + bias, 0.f));
+        A[m * AP + n] = f2bf16(fmaxf(acc[mi][nj][i] + bias, 0.f));
       }
   }
   __syncthreads();
-  // ---------------- GEMM2 + bias + softshrink -> X (fp32 complex, conjugated for the inverse)
-  gemm_96x192(A, w2t, acc);
+  // ---------------- GEMM2 + bias + softshrink -> X (fp16 complex, conjugated for the inverse)
+  gemm_tile<S>(A, w2t, acc);
   __syncthreads();
   _Float16* X = reinterpret_cast<_Float16*>(lds);
   const float lam = a.lambda;
 #pragma unroll
-  for (int nj = 0; nj < 3; ++nj) {
-    const int n = (3 * w + nj) * 16 + (lane & 15);
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b2[n];
-    const int c = n < kBS ? n : n - kBS;
-    const int part = n < kBS ? 0 : 1;
+    const int c = n < BS ? n : n - BS;
+    const int part = n < BS ? 0 : 1;
     const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
+    for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mi * 16 + 4 * (lane >> 4) + i;
         if (m < L) {
           const float v = acc[mi][nj][i] + bias;
           const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
-          X[(m * kBS + c) * 2 + part] = static_cast<_Float16>(sgn * s);
+          X[(m * BS + c) * 2 + part] = static_cast<_Float16>(sgn * s);
         }
       }
   }
@@ -330,20 +322,20 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_hp(lds, (j + r * P0::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_hp(lds, (j + r * P0::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_hp(lds, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
@@ -355,17 +347,17 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
@@ -382,10 +374,9 @@ __global__ void __launch_bounds__(kNT, AFNO_OCC) afno_spectral_kernel(const Afno
 // H-FFT, and the two block-MLP GEMMs as 3-product split GEMMs -- an fp32 operand is the bf16
 // pair hi + lo and A.B = Ah.Bh + Al.Bh + Ah.Bl with fp32 accumulation (relative error ~5e-6,
 // the exact-f32 MFMA would cost 16x the bf16 rate, this 3x).  The A operand is split into two
-// bf16 planes [96][kAPitch] (hi, lo) when it is written to LDS; the weights arrive pre-split as
-// [NB][192 n][hi 192 k | lo 192 k].  76.8 KB of LDS: 2 workgroups per CU.
-constexpr int kK2 = 2 * kK;  // split weight row: [hi | lo]
-
+// bf16 planes [16 MT][APitch] (hi, lo) when it is written to LDS; the weights arrive pre-split
+// as k32-interleaved rows [NB][2BS n][2 * 2BS k].  76.8 KB of LDS at H = 90, BS = 96: 2
+// workgroups per CU.
 __device__ __forceinline__ void st_fp(float2* p, int i, const cpair& v) {
   *reinterpret_cast<float4*>(p + i) = make_float4(v.re[0], v.im[0], v.re[1], v.im[1]);
 }
@@ -406,40 +397,41 @@ __device__ __forceinline__ void put_split2(uint16_t* Ahi, uint16_t* Alo, int idx
       (static_cast<uint32_t>(f2bf16(b - __uint_as_float(static_cast<uint32_t>(hb) << 16))) << 16);
 }
 
-// [96 x 192] = (Ah + Al) x (Bh + Bl)^T without Al.Bl; wave w owns N-tiles 3w..3w+2
-__device__ __forceinline__ void gemm_96x192_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
-                                               const uint16_t* __restrict__ Bt, f32x4 (&acc)[6][3]) {
+// [16 MT x 2BS] = (Ah + Al) x (Bh + Bl)^T without Al.Bl; wave w owns column tiles NTW w ..
+template <class S>
+__device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
+                                             const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
+  constexpr int K2 = 2 * S::K;  // split weight row: k32-interleaved [hi(32) | lo(32)] chunks
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
 #pragma unroll
-  for (int mi = 0; mi < 6; ++mi)
+  for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
-    for (int nj = 0; nj < 3; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 bh[2][3], bl[2][3];
-  // split weight rows are k32-interleaved: k-step ks (32 deep) = [hi(32) | lo(32)] at ks * 64
+    for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bh[2][S::NTW], bl[2][S::NTW];
 #pragma unroll
-  for (int nj = 0; nj < 3; ++nj) {
-    const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + kq * 8;
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + kq * 8;
     bh[0][nj] = *reinterpret_cast<const bf16x8*>(row);
     bl[0][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
   }
 #pragma unroll
-  for (int ks = 0; ks < 6; ++ks) {
-    if (ks + 1 < 6) {
+  for (int ks = 0; ks < S::KS; ++ks) {
+    if (ks + 1 < S::KS) {
 #pragma unroll
-      for (int nj = 0; nj < 3; ++nj) {
-        const uint16_t* row = Bt + ((3 * w + nj) * 16 + r16) * kK2 + (ks + 1) * 64 + kq * 8;
+      for (int nj = 0; nj < S::NTW; ++nj) {
+        const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + (ks + 1) * 64 + kq * 8;
         bh[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row);
         bl[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
       }
     }
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi) {
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ah + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Al + (mi * 16 + r16) * kAPitch + ks * 32 + kq * 8);
+    for (int mi = 0; mi < S::MT; ++mi) {
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ah + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Al + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
 #pragma unroll
-      for (int nj = 0; nj < 3; ++nj) {
+      for (int nj = 0; nj < S::NTW; ++nj) {
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks & 1][nj], acc[mi][nj], 0, 0, 0);
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
@@ -448,26 +440,25 @@ __device__ __forceinline__ void gemm_96x192_x3(const uint16_t* __restrict__ Ah, 
   }
 }
 
-constexpr int kX3Plane = kBS * kAPitch;  // bf16 elements per A plane
-
-template <int L, int R0, int R1>
+template <class S>
 __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs a) {
-  static_assert(R0 * R1 == L && L <= 96, "two-pass H FFT with H <= 96");
-  extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][96] complex fp32 (69 KB at L=90)
-  uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [96][kAPitch] bf16 hi
-  uint16_t* Al = Ah + kX3Plane;                                  //          [96][kAPitch] bf16 lo
+  constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
+  constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
+  extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][BS] complex fp32
+  uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [16 MT][APitch] bf16 hi
+  uint16_t* Al = Ah + plane;                                     //          [16 MT][APitch] bf16 lo
   const int tid = threadIdx.x;
   const int blk = blockIdx.x % a.NB;
   const int bk = blockIdx.x / a.NB;
   const int kw = bk % a.KM;
   const int b = bk / a.KM;
-  AMD_DFT_DEV_CHECK((blk + 1) * kBS <= a.C && kw < a.KM && L == a.H, "afno_spectral_x3_kernel");
+  AMD_DFT_DEV_CHECK((blk + 1) * BS <= a.C && kw < a.KM && L == a.H, "afno_spectral_x3_kernel");
   const int row_stride = a.KM * a.C * 2;
-  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * kBS) * 2;
+  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * BS) * 2;
   const float* xin = static_cast<const float*>(a.x) + base;
   float* yout = static_cast<float*>(a.y) + base;
-  using P0 = HPass<R0, L>;
-  using P1 = HPass<R1, L>;
+  using P0 = HPass<R0, L, NP>;
+  using P1 = HPass<R1, L, NP>;
   // ---------------- forward FFT_H: pass 0 straight from global
   {
     cpair v[P0::Q][R0];
@@ -476,7 +467,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       const int bb = tid + q * kNT;
       const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
       const int bc = ok ? bb : 0;
-      const int tp = bc % kNP, j = bc / kNP;
+      const int tp = bc % NP, j = bc / NP;
 #pragma unroll
       for (int r = 0; r < R0; ++r) {
         float2 c0, c1;
@@ -484,89 +475,89 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         v[q][r] = make_cpair(c0, c1);
       }
     }
-    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
   __syncthreads();
-  // ---------------- pass 1: LDS -> registers -> A planes ([h][re 0..95 | im 96..191], hi / lo)
+  // ---------------- pass 1: LDS -> registers -> A planes ([h][re 0..BS-1 | im BS..2BS-1], hi / lo)
   {
     cpair v[P1::Q][R1];
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
-          put_split2(Ah, Al, (n * kAPitch) / 2 + tp, v[q][r].re[0], v[q][r].re[1]);
-          put_split2(Ah, Al, (n * kAPitch) / 2 + kNP + tp, v[q][r].im[0], v[q][r].im[1]);
+          put_split2(Ah, Al, (n * AP) / 2 + tp, v[q][r].re[0], v[q][r].re[1]);
+          put_split2(Ah, Al, (n * AP) / 2 + NP + tp, v[q][r].im[0], v[q][r].im[1]);
         }
       }
     }
   }
-  // rows L..95 of A (GEMM M padding) are never written: their outputs are discarded
+  // rows L..16 MT - 1 of A (GEMM M padding) are never written: their outputs are discarded
   __syncthreads();
   const int lane = tid & 63, w = tid >> 6;
-  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * kK * kK2;
-  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * kK * kK2;
-  const float* b1 = a.b1 + blk * kK;
-  const float* b2 = a.b2 + blk * kK;
-  f32x4 acc[6][3];
-  gemm_96x192_x3(Ah, Al, w1t, acc);
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * 2 * K;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * 2 * K;
+  const float* b1 = a.b1 + blk * K;
+  const float* b2 = a.b2 + blk * K;
+  f32x4 acc[S::MT][S::NTW];
+  gemm_tile_x3<S>(Ah, Al, w1t, acc);
   __syncthreads();
 #pragma unroll
-  for (int nj = 0; nj < 3; ++nj) {
-    const int n = (3 * w + nj) * 16 + (lane & 15);
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b1[n];
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
+    for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mi * 16 + 4 * (lane >> 4) + i;
-        put_split(Ah, Al, m * kAPitch + n, fmaxf(acc[mi][nj][i] + bias, 0.f));
+        put_split(Ah, Al, m * AP + n, fmaxf(acc[mi][nj][i] + bias, 0.f));
       }
   }
   __syncthreads();
-  gemm_96x192_x3(Ah, Al, w2t, acc);
+  gemm_tile_x3<S>(Ah, Al, w2t, acc);
   __syncthreads();
   float* X = reinterpret_cast<float*>(ldsf);
   const float lam = a.lambda;
 #pragma unroll
-  for (int nj = 0; nj < 3; ++nj) {
-    const int n = (3 * w + nj) * 16 + (lane & 15);
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b2[n];
-    const int c = n < kBS ? n : n - kBS;
-    const int part = n < kBS ? 0 : 1;
+    const int c = n < BS ? n : n - BS;
+    const int part = n < BS ? 0 : 1;
     const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
 #pragma unroll
-    for (int mi = 0; mi < 6; ++mi)
+    for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mi * 16 + 4 * (lane >> 4) + i;
         if (m < L) {
           const float v = acc[mi][nj][i] + bias;
           const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
-          X[(m * kBS + c) * 2 + part] = sgn * s;
+          X[(m * BS + c) * 2 + part] = sgn * s;
         }
       }
   }
@@ -578,20 +569,20 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp(ldsf, (j + r * P0::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp(ldsf, (j + r * P0::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
-    h_twiddle_dft<R0, L, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P0::NB % kNT == 0 || bb < P0::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * kBS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
@@ -603,17 +594,17 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * kBS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
       if (P1::NB % kNT == 0 || bb < P1::NB) {
-        const int tp = bb % kNP, j = bb / kNP;
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
@@ -625,18 +616,82 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   }
 }
 
+// ------------------------------------------------------------------ instance table
+// (H, R0, R1, block size): (R0, R1) must be the FFT plan's radix order for H (plan_info),
+// because the kernel reads the plan's twiddle table; launch_afno_spectral checks it.
+#define AFNO_SHAPES(X) \
+  X(90, 9, 10, 96)     \
+  X(90, 9, 10, 64)     \
+  X(90, 9, 10, 128)    \
+  X(45, 9, 5, 96)      \
+  X(45, 9, 5, 64)      \
+  X(45, 9, 5, 128)     \
+  X(64, 16, 4, 64)     \
+  X(64, 16, 4, 96)     \
+  X(64, 16, 4, 128)
+
+using KernFn = void (*)(AfnoArgs);
+struct AfnoInstance {
+  int H, R0, R1, BS;
+  int64_t lds_bf16, lds_x3;  // dynamic LDS bytes of the bf16 and bf16x3 kernels
+  KernFn bf16[2][2];         // [bf16_in][bf16_out]
+  KernFn x3;
+};
+
+template <class S>
+AfnoInstance make_instance() {
+  constexpr int64_t plane = 16LL * S::MT * S::APitch * 2;  // bytes of one bf16 A tile
+  constexpr int64_t st16 = static_cast<int64_t>(S::L) * S::BS * 4, st32 = 2 * st16;
+  AfnoInstance r{S::L, S::R0, S::R1, S::BS, st16 > plane ? st16 : plane, st32 > 2 * plane ? st32 : 2 * plane,
+                 {{afno_spectral_kernel<S, false, false>, afno_spectral_kernel<S, false, true>},
+                  {afno_spectral_kernel<S, true, false>, afno_spectral_kernel<S, true, true>}},
+                 afno_spectral_x3_kernel<S>};
+  return r;
+}
+
+#define AFNO_INSTANCE(H, R0, R1, BS) make_instance<AfnoShape<H, R0, R1, BS>>(),
+const std::vector<AfnoInstance>& instances() {
+  static const std::vector<AfnoInstance> v = {AFNO_SHAPES(AFNO_INSTANCE)};
+  return v;
+}
+
+const AfnoInstance* find_instance(int H, int bs) {
+  for (const auto& i : instances())
+    if (i.H == H && i.BS == bs) return &i;
+  return nullptr;
+}
+
+void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a, void* stream) {
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     static_cast<int>(lds));
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
+  hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), static_cast<size_t>(lds),
+                     static_cast<hipStream_t>(stream), a);
+  e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral launch: ") + hipGetErrorString(e));
+}
+
 }  // namespace
 
-bool afno_spectral_supported(int H, int block_size) { return H == 90 && block_size == kBS; }
+bool afno_spectral_supported(int H, int block_size) { return find_instance(H, block_size) != nullptr; }
 
-int64_t afno_spectral_lds_bytes(int H) {
-  const int64_t staging = static_cast<int64_t>(H) * kBS * 4;  // fp16 complex
-  const int64_t a_tile = static_cast<int64_t>(kBS) * kAPitch * 2;  // bf16 GEMM operand (aliased)
-  return staging > a_tile ? staging : a_tile;
+std::vector<std::pair<int, int>> afno_spectral_shapes() {
+  std::vector<std::pair<int, int>> v;
+  for (const auto& i : instances()) v.emplace_back(i.H, i.BS);
+  return v;
+}
+
+int64_t afno_spectral_lds_bytes(int H, int block_size, bool x3) {
+  const AfnoInstance* in = find_instance(H, block_size);
+  return in ? (x3 ? in->lds_x3 : in->lds_bf16) : 0;
 }
 
 void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
-  if (!afno_spectral_supported(p.H, p.C / p.NB)) throw std::runtime_error("amd_dft: afno_spectral: unsupported shape");
+  if (p.NB <= 0 || p.C % p.NB) throw std::runtime_error("amd_dft: afno_spectral: C must be a multiple of NB");
+  const AfnoInstance* in = find_instance(p.H, p.C / p.NB);
+  if (!in) throw std::runtime_error("amd_dft: afno_spectral: unsupported shape");
+  if (p.r0 != in->R0 || p.r1 != in->R1)
+    throw std::runtime_error("amd_dft: afno_spectral: twiddle table radix order does not match the kernel");
   if (static_cast<int64_t>(p.H) * p.KM * p.C * 2 >= (int64_t(1) << 31))
     throw std::runtime_error("amd_dft: afno_spectral: per-batch spectrum exceeds 32-bit offsets");
   AfnoArgs a;
@@ -656,26 +711,10 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   if (nblocks <= 0) return;
   if (p.x3) {
     if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
-    const int64_t staging = static_cast<int64_t>(p.H) * kBS * 8, planes = 2LL * kX3Plane * 2;
-    size_t lds = static_cast<size_t>(staging > planes ? staging : planes);
-    auto kern = afno_spectral_x3_kernel<90, 9, 10>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(lds));
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
-    hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), lds, static_cast<hipStream_t>(stream), a);
-    e = hipGetLastError();
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral launch: ") + hipGetErrorString(e));
+    launch_kernel(in->x3, in->lds_x3, nblocks, a, stream);
     return;
   }
-  size_t lds = static_cast<size_t>(afno_spectral_lds_bytes(p.H));
-  auto kern = p.bf16_in ? (p.bf16_out ? afno_spectral_kernel<90, 9, 10, true, true> : afno_spectral_kernel<90, 9, 10, true, false>)
-                        : (p.bf16_out ? afno_spectral_kernel<90, 9, 10, false, true> : afno_spectral_kernel<90, 9, 10, false, false>);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     static_cast<int>(lds));
-  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
-  hipLaunchKernelGGL(kern, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), lds, static_cast<hipStream_t>(stream), a);
-  e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral launch: ") + hipGetErrorString(e));
+  launch_kernel(in->bf16[p.bf16_in ? 1 : 0][p.bf16_out ? 1 : 0], in->lds_bf16, nblocks, a, stream);
 }
 
 }  // namespace amd_dft

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <cstdint>
+#include <utility>
+#include <vector>
 
 namespace amd_dft {
 
@@ -16,11 +18,13 @@ struct AfnoLaunch {
   const float* b1;      // [NB][2*BS] = [b_re | b_im]
   const float* b2;
   const void* tw;       // FFT plan twiddles for length H
+  int r0 = 0, r1 = 0;   // the plan's radix order (must match the instance's two passes)
   int B, H, KM, C, NB;
   float lambda;
 };
 bool afno_spectral_supported(int H, int block_size);
-int64_t afno_spectral_lds_bytes(int H);
+std::vector<std::pair<int, int>> afno_spectral_shapes();  // instantiated (H, block size) pairs
+int64_t afno_spectral_lds_bytes(int H, int block_size, bool x3);
 void launch_afno_spectral(const AfnoLaunch& p, void* stream);
 
 // ---- FNO: per-mode complex channel mixing out[b,o,m] = sum_i x[b,i,m] * w[i,o,m]

@@ -110,7 +110,7 @@ def pack_afno_weights(w1, b1, w2, b2, split: bool = False) -> Tuple[torch.Tensor
 # (H, block size) instances of the fused AFNO kernel; mirrors afno_spectral_supported() in
 # csrc/spectral/afno_spectral.hip (checked equal in tests/test_models.py).  Kept in Python so
 # the check stays a constant under ONNX/TorchScript tracing (an op returning bool cannot be traced).
-AFNO_FUSED_SHAPES = frozenset({(90, 96)})
+AFNO_FUSED_SHAPES = frozenset({(H, bs) for H in (45, 64, 90) for bs in (64, 96, 128)})
 
 
 def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:

@@ -87,6 +87,8 @@ def test_fourcastnet_flops():
 def test_afno_fused_shape_table_matches_native():
     from tensorrt_dft_plugins_amd.ops.spectral import AFNO_FUSED_SHAPES
 
-    for H in (45, 90, 180):
+    for H in (32, 45, 64, 90, 180):
         for bs in (48, 64, 96, 128):
             assert bool(torch.ops.amd_dft.afno_spectral_supported(H, bs)) == ((H, bs) in AFNO_FUSED_SHAPES)
+    listed = list(torch.ops.amd_dft.afno_spectral_shapes())
+    assert set(zip(listed[0::2], listed[1::2])) == set(AFNO_FUSED_SHAPES)

@@ -69,6 +69,66 @@ def test_afno2d_amd_fused_vs_reference(device):
     assert rel_l2(outb.float(), ref) < 2e-2
 
 
+# every (H, block size) instance of the fused kernel beyond FourCastNet's (90, 96): the bf16 kernel
+# (bf16 and fp32 spectra) against the CPU op (fp32 ATen math, pinned to a torch composition in
+# tests/test_models.py), and the bf16x3 kernel against the same op with un-split fp32 weights
+_NEW_SHAPES = sorted(S.AFNO_FUSED_SHAPES - {(90, 96)})
+
+
+@pytest.mark.parametrize("H,bs", _NEW_SHAPES)
+def test_afno_spectral_shapes_bf16(device, H, bs):
+    torch.manual_seed(H * 1000 + bs)
+    B, KM, nb = 1, 3, 2
+    C = nb * bs
+    xw = torch.randn(B, H, KM, C, 2)
+    w1, b1, w2, b2 = _afno_params(nb, bs, scale=0.05, seed=bs)
+    w1t, w2t, b1p, b2p = S.pack_afno_weights(w1, b1, w2, b2)
+    ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)
+    args = [t.to(device) for t in (w1t, w2t, b1p, b2p)]
+    out = torch.ops.amd_dft.afno_spectral(xw.to(device), *args, 0.01)
+    assert out.dtype == torch.float32
+    assert rel_l2(out, ref) < 6e-3  # bf16 MFMA operands, fp16 staging
+    outb = torch.ops.amd_dft.afno_spectral(xw.to(device, torch.bfloat16), *args, 0.01)
+    assert outb.dtype == torch.bfloat16
+    assert rel_l2(outb.float(), ref) < 1.2e-2
+
+
+@pytest.mark.parametrize("H,bs", _NEW_SHAPES)
+def test_afno_spectral_shapes_x3(device, H, bs):
+    torch.manual_seed(H * 7 + bs)
+    B, KM, nb = 1, 3, 2
+    C = nb * bs
+    xw = torch.randn(B, H, KM, C, 2)
+    w1, w2 = 0.05 * torch.randn(2, nb, bs, bs), 0.05 * torch.randn(2, nb, bs, bs)
+    b1, b2 = 0.05 * torch.randn(2, nb, bs), 0.05 * torch.randn(2, nb, bs)
+    w1t = S._real_block(w1).transpose(1, 2).contiguous()
+    w2t = S._real_block(w2).transpose(1, 2).contiguous()
+    b1p, b2p = torch.cat([b1[0], b1[1]], 1), torch.cat([b2[0], b2[1]], 1)
+    ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)
+    w1s, w2s, b1s, b2s = S.pack_afno_weights(w1.to(device), b1.to(device), w2.to(device), b2.to(device), split=True)
+    out = torch.ops.amd_dft.afno_spectral(xw.to(device), w1s, w2s, b1s, b2s, 0.01)
+    assert rel_l2(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("H,W,bs", [(45, 90, 64), (64, 128, 128)])
+def test_afno2d_amd_fused_new_shapes(device, H, W, bs):
+    """End to end through afno2d_amd (fused H filter at the new instances) vs the FourCastNet
+    AFNO2D forward, fp32 activations and bf16 activations."""
+    torch.manual_seed(H + W)
+    B, nb = 1, 2
+    C = nb * bs
+    x = torch.randn(B, H, W, C)
+    w1, b1, w2, b2 = _afno_params(nb, bs, scale=0.05, seed=H)
+    ref = afno2d_reference(x, w1, b1, w2, b2, nb, 0.01, 1.0)
+    xd = x.to(device)
+    assert S.afno_fused_available(xd, nb)
+    p = [t.to(device) for t in (w1, b1, w2, b2)]
+    out = afno2d_amd(xd, p[0], p[1], p[2], p[3], nb, 0.01, 1.0)
+    assert rel_l2(out, ref) < 1e-2
+    outb = afno2d_amd(xd.to(torch.bfloat16), p[0], p[1], p[2], p[3], nb, 0.01, 1.0)
+    assert rel_l2(outb.float(), ref) < 2e-2
+
+
 def test_layernorm_kernel(device):
     torch.manual_seed(2)
     x = torch.randn(1000, 768, device=device).to(torch.bfloat16)
