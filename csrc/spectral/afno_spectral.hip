@@ -51,6 +51,9 @@ constexpr int kNT = 256;  // threads
 #ifndef AFNO_BPF
 #define AFNO_BPF 2  // k-steps of B-fragment prefetch in the block-MLP GEMMs
 #endif
+#ifndef AFNO_ABLATE
+#define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs
+#endif
 
 // Compile-time geometry of one instance: H = L = R0 x R1, block size BS.
 template <int L_, int R0_, int R1_, int BS_>
@@ -121,6 +124,7 @@ template <int R, int L, int NP, int Ns, int Q>
 __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
   using P = HPass<R, L, NP>;
   static_assert(P::Q == Q, "pass geometry");
+  if constexpr (AFNO_ABLATE & 1) return;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int b = threadIdx.x + q * kNT;
@@ -186,8 +190,10 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
 #pragma unroll
     for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
-      for (int nj = 0; nj < S::NTW; ++nj)
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+      for (int nj = 0; nj < S::NTW; ++nj) {
+        if constexpr (AFNO_ABLATE & 2) acc[mi][nj] += __builtin_bit_cast(f32x4, afr[mi]) + __builtin_bit_cast(f32x4, bq[ks % NQ][nj]);
+        else acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+      }
   }
 }
 
@@ -432,6 +438,11 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(Al + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
+        if constexpr (AFNO_ABLATE & 2) {
+          acc[mi][nj] += __builtin_bit_cast(f32x4, al) + __builtin_bit_cast(f32x4, bh[ks & 1][nj]) +
+                         __builtin_bit_cast(f32x4, ah) + __builtin_bit_cast(f32x4, bl[ks & 1][nj]);
+          continue;
+        }
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks & 1][nj], acc[mi][nj], 0, 0, 0);
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
