@@ -549,6 +549,7 @@ class OnnxGraph:
                     else v.to(self.device)
                 continue
             self.nodes.append((_OPS[key], attrs, list(n.input), list(n.output), n.op_type))
+        self.folded = self._fold_constants()
         # plugin-style validation of contrib nodes at build time (creator checks)
         for _, attrs, _, _, opt in self.nodes:
             if opt in ("Rfft", "Irfft"):
@@ -556,6 +557,32 @@ class OnnxGraph:
                         not 1 <= attrs.get("signal_ndim", 1) <= 3:
                     raise ValueError(f"invalid {opt} attributes {attrs} (normalized=0, onesided=1, "
                                      "1<=signal_ndim<=3 required)")
+
+    def _fold_constants(self) -> int:
+        """Evaluate once, at load, every node whose inputs are all constants (initializers or
+        folded outputs): e.g. the bf16x3 weight splits and LayerNorm-fold weight sums of an
+        exported FourCastNet, which would otherwise re-run on every replay.  TensorRT folds the
+        same way at engine build.  Constants no remaining node reads are dropped."""
+        kept, folded = [], 0
+        with torch.no_grad():
+            for node in self.nodes:
+                fn, attrs, ins, outs, _ = node
+                real = [i for i in ins if i]
+                if not real or not all(i in self.consts for i in real):
+                    kept.append(node)
+                    continue
+                args = [self.consts[i] if i else None for i in ins]
+                while args and args[-1] is None:
+                    args.pop()
+                res = fn(attrs, *args)
+                res = list(res) if isinstance(res, (list, tuple)) else [res]
+                for o, r in zip(outs, res):
+                    self.consts[o] = r
+                folded += 1
+        self.nodes = kept
+        used = {i for _, _, ins, _, _ in kept for i in ins if i} | set(self.output_names)
+        self.consts = {k: v for k, v in self.consts.items() if k in used}
+        return folded
 
     def run(self, *inputs: torch.Tensor) -> List[torch.Tensor]:
         if len(inputs) != len(self.input_names):

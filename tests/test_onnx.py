@@ -204,3 +204,29 @@ def test_export_fast_afno_model_amd_nodes():
     data = ex.export(m, x)
     (y,) = OnnxGraph(data, device="cpu").run(x)
     assert torch.allclose(y, ref, atol=1e-4)
+
+
+def test_constant_subgraphs_folded_at_load():
+    """Nodes whose inputs are all constants run once when the graph is loaded (TensorRT-style
+    constant folding): the weight-only subgraph disappears from the per-run node list."""
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = nn.Parameter(torch.randn(8, 8))
+
+        def forward(self, x):
+            w2 = torch.tanh(self.w * 2.0).t()  # constant-only: folded
+            return x @ w2 + 1.0
+
+    torch.manual_seed(0)
+    m = M().eval()
+    x = torch.randn(4, 8)
+    with torch.no_grad():
+        ref = m(x)
+    data = ex.export(m, x)
+    g = OnnxGraph(data, device="cpu")
+    assert g.folded >= 2
+    assert all(op not in ("Tanh", "Transpose", "Mul") for *_, op in g.nodes)
+    (y,) = g.run(x)
+    assert torch.allclose(y, ref, atol=1e-6)
