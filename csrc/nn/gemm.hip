@@ -421,14 +421,14 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
 // logical K of a split (bf16x3) GEMM: 32-deep K-tiles, at least 2 (the pipeline prologue)
 static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
 
-// MI_DFT_GEMM=4w selects the four-wave 128x128-per-wave kernel (gemm4w.hip) where it applies;
+// MI_DFT_GEMM_KERNEL=4w selects the four-wave 128x128-per-wave kernel (gemm4w.hip) where it applies;
 // default: the 8-wave ping-pong kernel below, measured faster on the FourCastNet shapes
 // (fc2 2127 vs 2466 us, fc1+GELU 3231 vs 3997 us, bf16x3 fc2 6360 vs 7639 us;
 // profiles/gemm_4w_vs_8w_r2.txt: hipcc keeps part of the 4-wave kernel's fragments in the
 // accumulator file and shuffles them back every few MFMAs)
 static int gemm_variant() {
   static const int v = [] {
-    const char* e = std::getenv("MI_DFT_GEMM");
+    const char* e = std::getenv("MI_DFT_GEMM_KERNEL");  // "4w": the experimental 4-wave kernel
     return (e && std::string(e) == "4w") ? 4 : 8;
   }();
   return v;
