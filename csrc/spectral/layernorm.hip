@@ -304,6 +304,73 @@ __global__ void __launch_bounds__(64 * kWaves) ln_f32_kernel(const float* __rest
   }
 }
 
+// LayerNorm with the split-pair output, for rows of cols % 256 == 0: the k32-interleaved pair
+// row (4 cols bytes) is written as NK full 1-KB wave stores (lane l of store k writes bytes
+// [1024 k + 16 l, +16): chunk 8k + l / 8, part (l / 4) & 1, 8 columns (l & 3) * 8) instead of
+// 8-byte half-line pieces; lanes l and l ^ 4 normalise the same 8 columns (their loads hit the
+// same L1 lines) and store the hi resp. lo half.
+template <int NK, bool PRE>
+__global__ void __launch_bounds__(64 * kWaves) ln_split_kernel(const float* __restrict__ x, const float* __restrict__ pre,
+                                                               const float* __restrict__ g, const float* __restrict__ b,
+                                                               uint16_t* __restrict__ y, int64_t rows, float eps) {
+  constexpr int cols = NK * 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * cols;
+  const int cbase = (lane >> 3) * 32 + (lane & 3) * 8;
+  float v[NK][8];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = k * 256 + cbase;
+    const float4 a = *reinterpret_cast<const float4*>(xr + c0);
+    const float4 c = *reinterpret_cast<const float4*>(xr + c0 + 4);
+    v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+    v[k][4] = c.x; v[k][5] = c.y; v[k][6] = c.z; v[k][7] = c.w;
+    if constexpr (PRE) {
+      const float4 pa = *reinterpret_cast<const float4*>(pre + c0);
+      const float4 pc = *reinterpret_cast<const float4*>(pre + c0 + 4);
+      v[k][0] += pa.x; v[k][1] += pa.y; v[k][2] += pa.z; v[k][3] += pa.w;
+      v[k][4] += pc.x; v[k][5] += pc.y; v[k][6] += pc.z; v[k][7] += pc.w;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[k][i];
+  const float mean = wave_sum(s) * (0.5f / cols);  // every column is held by two lanes
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[k][i] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(q) * (0.5f / cols) + eps);
+  const bool lo_half = (lane >> 2) & 1;
+  uint16_t* yr = y + row * (2 * cols) + lane * 8;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = k * 256 + cbase;
+    const float4 ga = *reinterpret_cast<const float4*>(g + c0), gc = *reinterpret_cast<const float4*>(g + c0 + 4);
+    const float4 ba = *reinterpret_cast<const float4*>(b + c0), bc = *reinterpret_cast<const float4*>(b + c0 + 4);
+    const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gc.x, gc.y, gc.z, gc.w};
+    const float bb[8] = {ba.x, ba.y, ba.z, ba.w, bc.x, bc.y, bc.z, bc.w};
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mean) * rstd * gg[i] + bb[i];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t h = bfpack(o[2 * i], o[2 * i + 1]);
+      w[i] = lo_half ? bfpack_lo(o[2 * i], o[2 * i + 1], h) : h;
+    }
+    *reinterpret_cast<uint4*>(yr + k * 512) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <bool STATS, bool SPLIT>
 void launch_f32(const float* x, const float* pre, const float* g, const float* b, void* y, float2* st, int64_t rows,
                 int cols, float eps, hipStream_t s) {
@@ -384,7 +451,15 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
     const auto* x = static_cast<const float*>(p.x);
     const auto* g = static_cast<const float*>(p.gamma);
     const auto* b = static_cast<const float*>(p.beta);
-    if (p.split_out) launch_f32<false, true>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
+    if (p.split_out && p.cols == 768 && p.rows <= static_cast<int64_t>(0x7fffffff) * kWaves) {
+      const dim3 grid(static_cast<uint32_t>((p.rows + kWaves - 1) / kWaves)), blk(64 * kWaves);
+      auto* y = static_cast<uint16_t*>(p.y);
+      hipStream_t s = static_cast<hipStream_t>(stream);
+      if (p.pre) hipLaunchKernelGGL((ln_split_kernel<3, true>), grid, blk, 0, s, x, p.pre, g, b, y, p.rows, p.eps);
+      else hipLaunchKernelGGL((ln_split_kernel<3, false>), grid, blk, 0, s, x, nullptr, g, b, y, p.rows, p.eps);
+    } else if (p.split_out) {
+      launch_f32<false, true>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
+    }
     else launch_f32<false, false>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: layernorm launch: ") + hipGetErrorString(e));

@@ -157,6 +157,13 @@ def test_split_and_layernorm_fp32_gpu(device):
     ref = F.layer_norm(x + pre, (768,), g, b, 1e-6)
     ys = ops.layer_norm_split(x.to(device), g.to(device), b.to(device), 1e-6, pre.to(device)).cpu()
     assert rel_l2(unsplit_bf16(ys), ref) < 2e-5
+    x1 = x[:999]  # partial last workgroup, no pre
+    ys1 = ops.layer_norm_split(x1.to(device), g.to(device), b.to(device), 1e-6, None).cpu()
+    ref1 = F.layer_norm(x1, (768,), g, b, 1e-6)
+    assert rel_l2(unsplit_bf16(ys1), ref1) < 2e-5
+    hi1, lo1 = (h.float() for h in _halves(ys1))  # a valid split: |lo| <= ulp(hi) / 2
+    assert rel_l2(hi1, ref1) < 4e-3
+    assert bool((lo1.abs() <= hi1.abs() * 2.0 ** -8).all())
     y, _ = ops.layer_norm(x.to(device), g.to(device), b.to(device), 1e-6, None)
     assert y.dtype == torch.float32 and rel_l2(y.cpu(), F.layer_norm(x, (768,), g, b, 1e-6)) < 1e-6
     st = ops.ln_stats(x.to(device), pre.to(device), 1e-6).cpu()
