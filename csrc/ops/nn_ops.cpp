@@ -130,6 +130,80 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
   return y;
 }
 
+// ------------------------------------------------------------------ LayerNorm folded into a GEMM
+// linear_ln: y = act(LN(x) W^T + b) computed from the RAW rows x (no normalised copy):
+//   w = W * gamma (per k, as used by the GEMM), c1[n] = sum_k w[n, k], bias = W beta + b,
+//   stats[m] = (mean_m, rstd_m) of x  ->  y = act(rstd_m * (x w^T - mean_m c1) + bias).
+// c1 must be summed from the same (bf16-rounded) w the GEMM reads: x w^T - mean c1 is then
+// (x - mean) w exactly, with no cancellation beyond fp32 accumulation.
+void check_linear_ln(const at::Tensor& x, const at::Tensor& w, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
+                     const at::Tensor& stats, int64_t act) {
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear_ln: act must be 0 (none) or 1 (gelu)");
+  TORCH_CHECK(w.dim() == 2 && x.size(-1) == w.size(1), "amd_dft.linear_ln: x [..., K], w [N, K]");
+  const int64_t K = w.size(1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(c1.numel() == N, "amd_dft.linear_ln: c1 must have N entries");
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "amd_dft.linear_ln: bias must have N entries");
+  TORCH_CHECK(stats.numel() == 2 * M && stats.size(-1) == 2, "amd_dft.linear_ln: stats must be [M, 2] (mean, rstd)");
+}
+
+at::Tensor linear_ln_ref(const at::Tensor& x, const at::Tensor& w, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
+                         const at::Tensor& stats, int64_t act) {
+  const int64_t K = w.size(1);
+  at::Tensor xf = x.to(at::kFloat).reshape({-1, K});
+  at::Tensor st = stats.to(at::kFloat).reshape({-1, 2});
+  at::Tensor t = at::matmul(xf, w.to(at::kFloat).t());
+  at::Tensor y = st.select(1, 1).unsqueeze(1) * (t - st.select(1, 0).unsqueeze(1) * c1.to(at::kFloat).reshape({1, -1}));
+  if (bias.has_value() && bias->defined()) y = y + bias->to(at::kFloat).reshape({1, -1});
+  if (act == 1) y = at::gelu(y);
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = w.size(0);
+  return y.reshape(os).to(x.scalar_type());
+}
+
+at::Tensor linear_ln_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
+                         const at::Tensor& stats, int64_t act) {
+  check_linear_ln(x, w, c1, bias, stats, act);
+  return linear_ln_ref(x, w, c1, bias, stats, act);
+}
+
+at::Tensor linear_ln_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& c1_,
+                          const c10::optional<at::Tensor>& bias, const at::Tensor& stats_, int64_t act) {
+  const c10::DeviceGuard guard(x_.device());
+  check_linear_ln(x_, w_, c1_, bias, stats_, act);
+  const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
+  if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K)) {
+    fallback_note("linear_ln", "needs bf16 operands, N % 256 == 0, K % 64 == 0");
+    return linear_ln_ref(x_, w_, c1_, bias, stats_, act);
+  }
+  at::Tensor x = x_.contiguous(), w = w_.contiguous();
+  at::Tensor c1 = c1_.to(at::kFloat).contiguous(), stats = stats_.to(at::kFloat).contiguous();
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = N;
+  at::Tensor y = at::empty(os, x.options());
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  p.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  p.y = y.data_ptr();
+  p.ln_stats = stats.data_ptr<float>();
+  p.ln_c1 = c1.data_ptr<float>();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.act = static_cast<int>(act);
+  launch_gemm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear_ln_meta(const at::Tensor& x, const at::Tensor& w, const at::Tensor&, const c10::optional<at::Tensor>&,
+                          const at::Tensor&, int64_t) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = w.size(0);
+  return at::empty(os, x.options());
+}
+
 // ------------------------------------------------------------------ patch embedding / head
 // patch_linear: tokens = patchify(x) @ w^T + bias + pos[token % (h*w)]  ([B*h*w, N] bf16)
 // linear_unpatch: image = unpatchify(t @ w^T + bias)                     ([B, C, h*p, w*p])
@@ -476,6 +550,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("patchify(Tensor x, int p) -> Tensor");
   m.def("unpatchify(Tensor t, int C, int h, int w, int p) -> Tensor");
   m.def("linear(Tensor x, Tensor w, Tensor? bias=None, int act=0, Tensor? residual=None) -> Tensor");
+  m.def("linear_ln(Tensor x, Tensor w, Tensor c1, Tensor? bias, Tensor stats, int act=0) -> Tensor");
   m.def("patch_linear(Tensor x, Tensor w, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
   m.def("linear_unpatch(Tensor t, Tensor w, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
   m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
@@ -487,6 +562,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cuda));
   m.impl("unpatchify", AMD_DFT_TRACED("amd_dft::unpatchify", amd_dft::unpatchify_cuda));
   m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cuda));
+  m.impl("linear_ln", AMD_DFT_TRACED("amd_dft::linear_ln", amd_dft::linear_ln_cuda));
   m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cuda));
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cuda));
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
@@ -498,6 +574,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("patchify", AMD_DFT_TRACED("amd_dft::patchify", amd_dft::patchify_cpu));
   m.impl("unpatchify", AMD_DFT_TRACED("amd_dft::unpatchify", amd_dft::unpatchify_cpu));
   m.impl("linear", AMD_DFT_TRACED("amd_dft::linear", amd_dft::linear_cpu));
+  m.impl("linear_ln", AMD_DFT_TRACED("amd_dft::linear_ln", amd_dft::linear_ln_cpu));
   m.impl("patch_linear", AMD_DFT_TRACED("amd_dft::patch_linear", amd_dft::patch_linear_cpu));
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cpu));
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
@@ -509,6 +586,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("patchify", &amd_dft::patchify_meta);
   m.impl("unpatchify", &amd_dft::unpatchify_meta);
   m.impl("linear", &amd_dft::linear_meta);
+  m.impl("linear_ln", &amd_dft::linear_ln_meta);
   m.impl("patch_linear", &amd_dft::patch_linear_meta);
   m.impl("linear_unpatch", &amd_dft::linear_unpatch_meta);
   m.impl("split_bf16", &amd_dft::split_bf16_meta);

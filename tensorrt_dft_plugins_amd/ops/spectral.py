@@ -206,7 +206,8 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
       X_w   = R2C_W(LN1(x))                      LN applied on load (no normalised copy in HBM)
       Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral (MFMA)
       x1    = C2R_W(Y_w) + LN1(x) + x            both skips from one read of xs
-      yn    = LN2(x1); h = GELU(fc1(yn))         hand MFMA GEMM, erf GELU in the epilogue
+      h     = GELU(fc1(LN2(x1)))                 ln_stats + hand MFMA GEMM with LN2 folded in
+                                                 (linear_ln) and the erf GELU in the epilogue
       x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue
 
     Returns (x1, fc2.bias): the bias is folded into the next block's statistics and loads
@@ -228,20 +229,37 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.bfloat16)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
     x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-    yn, _ = layer_norm(x1, blk.norm2)
     if mlp_on_hand_gemm():
         # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
         # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL
-        # collective blocks), which stall hipBLASLt's persistent stream-K grid
-        hid = ops.linear(yn.reshape(-1, C), m.fc1.weight, m.fc1.bias, 1, None)
+        # collective blocks), which stall hipBLASLt's persistent stream-K grid.  LN2 is folded
+        # into fc1 (linear_ln): only the per-token statistics are computed, no normalised copy.
+        st2 = ops.ln_stats(x1, None, blk.norm2.eps)
+        w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
+        hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 1)
         x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
         return x1, m.fc2.bias
+    yn, _ = layer_norm(x1, blk.norm2)
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
     if torch.jit.is_tracing():
         x1 = torch.addmm(x1.reshape(-1, C), hid, m.fc2.weight.t()).reshape(B, H, W, C)
     else:
         x1.view(-1, C).addmm_(hid, m.fc2.weight.t())
     return x1, m.fc2.bias
+
+
+def _ln_folded_fc(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
+    """(W * gamma as bf16, c1 = row sums of that bf16 matrix, c2 = W beta + b): the operands of
+    ``linear_ln`` for fc(LN(x)), cached on the Linear module."""
+    def build():
+        w = fc.weight.float()
+        wg = (w * ln.weight.float()[None, :]).to(torch.bfloat16).contiguous()
+        c1 = wg.float().sum(1).contiguous()
+        c2 = (w @ ln.bias.float() + (fc.bias.float() if fc.bias is not None else 0.0)).contiguous()
+        return wg, c1, c2
+
+    return module_cached(fc, "ln_folded", (fc.weight, ln.weight, ln.bias) + ((fc.bias,) if fc.bias is not None else ()),
+                         build)
 
 
 def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):

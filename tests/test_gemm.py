@@ -58,3 +58,52 @@ def test_linear_gemm_asymmetric_exact(device):
     ref = x.float() @ w.float().t()
     assert torch.equal(y, ref)
     assert torch.equal(y[:, 0], x[:, 5].float())
+
+
+def _ln_fold_operands(fc_w, fc_b, gamma, beta):
+    wg = (fc_w.float() * gamma.float()[None, :]).to(torch.bfloat16)
+    c1 = wg.float().sum(1)
+    c2 = fc_w.float() @ beta.float() + fc_b.float()
+    return wg, c1, c2
+
+
+def _ln_stats(x, eps):
+    xf = x.float()
+    return torch.stack([xf.mean(-1), torch.rsqrt(xf.var(-1, unbiased=False) + eps)], -1)
+
+
+def test_linear_ln_cpu_semantics():
+    """linear_ln(x) == fc(LN(x)) with the fold operands (pinned to the torch composition)."""
+    torch.manual_seed(1)
+    M, K, N = 7, 64, 256
+    x = torch.randn(M, K) * 2 + 0.7
+    w, b = torch.randn(N, K) / 8, torch.randn(N)
+    g, be = torch.randn(K) * 0.2 + 1, torch.randn(K) * 0.1
+    wg, c1, c2 = _ln_fold_operands(w, b, g, be)
+    y = torch.ops.amd_dft.linear_ln(x, wg, c1, c2, _ln_stats(x, 1e-6), 1)
+    ref = F.gelu(F.linear(F.layer_norm(x, (K,), eps=1e-6), wg.float(), c2))  # same rounded W * gamma
+    ref2 = F.gelu(F.linear(F.layer_norm(x, (K,), g, be, 1e-6), w, b))
+    assert rel_l2(y, ref2) < 5e-3  # bf16-rounded W * gamma
+    assert rel_l2(y, ref) < 1e-5
+    with pytest.raises(RuntimeError):
+        torch.ops.amd_dft.linear_ln(x, wg, c1[:-1], c2, _ln_stats(x, 1e-6), 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,act", [(1000, 1), (777, 0)])
+def test_linear_ln_gpu(device, M, act):
+    """LN2 folded into fc1 on the hand GEMM vs LayerNorm -> linear in fp32 (FourCastNet fc1
+    shape; the residual stream carries a large mean to exercise the mean * c1 correction)."""
+    torch.manual_seed(M)
+    K, N = 768, 3072
+    x = (torch.randn(M, K) * 1.5 + 3.0).to(torch.bfloat16)
+    w, b = torch.randn(N, K) / K ** 0.5, torch.randn(N) * 0.1
+    g, be = torch.randn(K) * 0.2 + 1, torch.randn(K) * 0.1
+    wg, c1, c2 = _ln_fold_operands(w, b, g, be)
+    st = torch.ops.amd_dft.ln_stats(x.to(device), None, 1e-6)
+    y = torch.ops.amd_dft.linear_ln(x.to(device), wg.to(device), c1.to(device), c2.to(device), st, act)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    ref = F.linear(F.layer_norm(x.float(), (K,), g, be, 1e-6), w, b)
+    if act:
+        ref = F.gelu(ref)
+    assert rel_l2(y.float().cpu(), ref) < 8e-3
