@@ -26,6 +26,9 @@ struct GemmLaunch {
   int res_rows = 0;          // > 0: residual row = token % res_rows (broadcast over the batch)
   // Un-patchify scatter (y is an image [B, sC, sh*8, sw*8]; feature order (c, py, px)).
   int sC = 0, sh = 0, sw = 0;
+#ifdef AMD_DFT_GEMM_STAMPS
+  long long* stamps = nullptr;  // diagnostic build only (bench/gemm_stamps.hip): per-block phase clocks
+#endif
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 void launch_gemm(const GemmLaunch& p, void* stream);

@@ -42,6 +42,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include "../fft/dev_check.h"
 #include "gemm.h"
@@ -180,6 +181,15 @@ __device__ __forceinline__ void wait_regions(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#ifdef AMD_DFT_GEMM_STAMPS
+// slot 0 / 5: s_memrealtime at entry / exit; 1..4: s_memtime at entry, after the prologue,
+// after the main loop, after the epilogue (thread 0 only, vector store)
+#define GEMM_STAMP(slot, v) \
+  do { if (threadIdx.x == 0) p.stamps[static_cast<int64_t>(blockIdx.x) * 8 + (slot)] = static_cast<long long>(v); } while (0)
+#else
+#define GEMM_STAMP(slot, v) do { } while (0)
+#endif
+
 __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -194,6 +204,8 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   const int M = p.M, N = p.N, K = p.K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 2, wc = wave & 3;  // 2 (features) x 4 (tokens)
+  GEMM_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  GEMM_STAMP(1, __builtin_amdgcn_s_memtime());
   // ---- XCD-aware tile order (bijective for any grid size)
   const int tiles_f = N / kBF;
   const int nwg = gridDim.x, b = blockIdx.x;
@@ -206,6 +218,35 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                     "gemm_bf16_kernel");
   const int r16 = lane & 15, kq = lane >> 4;
 
+  // ---- output geometry: lane holds features f..f+3 of token t for each (i, j) accumulator tile
+  // (recomputed where used instead of held in registers across the main loop)
+  auto tok = [&](int j) { return t0 + wc * 64 + j * 16 + r16; };
+  auto tokc = [&](int j) { return min(tok(j), M - 1); };  // loads use clamped (valid) rows; stores check t < M
+  auto out_off = [&](int i, int j) -> int64_t {
+    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+    const int t = tokc(j);
+    if constexpr (MODE == 2) {  // un-patchify: feature f = (c, py, px), 4 consecutive px
+      const int hw = p.sh * p.sw;
+      const int bb = t / hw, rem = t - bb * hw;
+      const int ii = rem / p.sw, jj = rem - ii * p.sw;
+      return (static_cast<int64_t>(bb * p.sC + (f >> 6)) * (p.sh * 8) + ii * 8 + ((f >> 3) & 7)) * (p.sw * 8) + jj * 8 +
+             (f & 7);
+    } else {
+      return static_cast<int64_t>(t) * N + f;
+    }
+  };
+  auto res_off = [&](int i, int j) -> int64_t {
+    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+    if constexpr (MODE == 1) {
+      if (p.res_rows > 0) return static_cast<int64_t>(tokc(j) % p.res_rows) * N + f;
+    }
+    return out_off(i, j);
+  };
+  typedef typename std::conditional<OUT == 1, float4, uint2>::type ResT;
+  auto load_res = [&](int i, int j) -> ResT {
+    if constexpr (OUT == 1) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + res_off(i, j));
+    else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + res_off(i, j));
+  };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -249,6 +290,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   bf16x8 a0[8], a1[8], b0[4], b1[4];
   read_a<0>(a0, smem, wr, r16, kq);
   if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
+  GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
 
 #ifndef GEMM_ABLATE
 #define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads
@@ -291,83 +333,92 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
   }
   if (wr == 0) barrier();  // re-align the two wave groups
+  GEMM_STAMP(3, __builtin_amdgcn_s_memtime());
 
-  // ---- epilogue: lane holds features f..f+3 of token t for each (i, j) tile
+  // ---- epilogue: lane holds features f..f+3 of token t for each (i, j) tile.
+  // No load sits behind a per-element branch (hipcc would then wait for each one in turn:
+  // 32 serialised round trips per wave, ~20 us per tile): bias / c1 / LN statistics are loaded
+  // up front, residual rows from clamped (always valid) addresses two i-tiles at a time with
+  // the next pair in flight, and only the stores are predicated on t < M.
+  float4 bias4[8], c14[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    float cv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BIAS) {
-      const float4 b4 = *reinterpret_cast<const float4*>(p.bias + f);
-      bv[0] = b4.x;
-      bv[1] = b4.y;
-      bv[2] = b4.z;
-      bv[3] = b4.w;
-    }
-    if constexpr (LN) {
-      const float4 c4 = *reinterpret_cast<const float4*>(p.ln_c1 + f);
-      cv[0] = c4.x;
-      cv[1] = c4.y;
-      cv[2] = c4.z;
-      cv[3] = c4.w;
+    bias4[i] = BIAS ? *reinterpret_cast<const float4*>(p.bias + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    c14[i] = LN ? *reinterpret_cast<const float4*>(p.ln_c1 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float2 lst[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
+  constexpr bool ERES = RES;
+  ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
+  if constexpr (ERES) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rq[0][ii][j] = load_res(ii, j);
+  }
+#pragma unroll
+  for (int ip = 0; ip < 4; ++ip) {  // i-tile pairs (2 ip, 2 ip + 1)
+    if constexpr (ERES) {
+      if (ip + 1 < 4) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rq[(ip + 1) & 1][ii][j] = load_res(2 * (ip + 1) + ii, j);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = t0 + wc * 64 + j * 16 + r16;
-      if (t >= M) continue;
-      float v[4];
-      float mean = 0.f, rstd = 1.f;
-      if constexpr (LN) {
-        const float2 st = *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(t));
-        mean = st.x;
-        rstd = st.y;
-      }
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = 2 * ip + ii;
+      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+      const float bv[4] = {bias4[i].x, bias4[i].y, bias4[i].z, bias4[i].w};
+      const float cv[4] = {c14[i].x, c14[i].y, c14[i].z, c14[i].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = acc[i][j][e];
-        if constexpr (LN) a = rstd * fmaf(-mean, cv[e], a);
-        v[e] = a + bv[e];
-        if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
-      }
-      int64_t off = static_cast<int64_t>(t) * N + f;
-      if constexpr (MODE == 2) {  // un-patchify: feature f = (c, py, px), 4 consecutive px
-        const int hw = p.sh * p.sw;
-        const int b = t / hw, rem = t - b * hw;
-        const int ii = rem / p.sw, jj = rem - ii * p.sw;
-        off = (static_cast<int64_t>(b * p.sC + (f >> 6)) * (p.sh * 8) + ii * 8 + ((f >> 3) & 7)) * (p.sw * 8) +
-              jj * 8 + (f & 7);
-      }
-      if constexpr (RES) {
-        const int64_t roff = (MODE == 1 && p.res_rows > 0) ? static_cast<int64_t>(t % p.res_rows) * N + f : off;
-        if constexpr (OUT == 1) {  // fp32 residual (in place allowed: same lane reads, then writes)
-          const float4 rr = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + roff);
-          v[0] += rr.x;
-          v[1] += rr.y;
-          v[2] += rr.z;
-          v[3] += rr.w;
-        } else {
-          const uint2 rr = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + roff);
-          v[0] += __uint_as_float(rr.x << 16);
-          v[1] += __uint_as_float(rr.x & 0xffff0000u);
-          v[2] += __uint_as_float(rr.y << 16);
-          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = acc[i][j][e];
+          if constexpr (LN) a = lst[j].y * fmaf(-lst[j].x, cv[e], a);
+          v[e] = a + bv[e];
+          if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
         }
-      }
-      if constexpr (OUT == 1) {
-        *reinterpret_cast<float4*>(static_cast<float*>(p.y) + off) = make_float4(v[0], v[1], v[2], v[3]);
-      } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
-        float lo[4];
+        if constexpr (ERES) {
+          const ResT rr = rq[ip & 1][ii][j];
+          if constexpr (OUT == 1) {  // fp32 residual (in place allowed: same lane reads, then writes)
+            v[0] += rr.x;
+            v[1] += rr.y;
+            v[2] += rr.z;
+            v[3] += rr.w;
+          } else {
+            v[0] += __uint_as_float(rr.x << 16);
+            v[1] += __uint_as_float(rr.x & 0xffff0000u);
+            v[2] += __uint_as_float(rr.y << 16);
+            v[3] += __uint_as_float(rr.y & 0xffff0000u);
+          }
+        }
+        if (tok(j) < M) {
+          if constexpr (OUT == 1) {
+            *reinterpret_cast<float4*>(static_cast<float*>(p.y) + out_off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
+          } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
+            float lo[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
-        uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 + (f & 31);
-        *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
-        *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
-      } else {
-        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + off) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
+            uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(tok(j)) * (2 * N) + (f >> 5) * 64 + (f & 31);
+            *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
+          } else {
+            *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + out_off(i, j)) =
+                make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+          }
+        }
       }
     }
   }
+  GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
+  GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
 }
 
 template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
@@ -434,17 +485,18 @@ static int gemm_variant() {
   return v;
 }
 
-void launch_gemm(const GemmLaunch& p, void* stream) {
-  if (!gemm_supported(p.M, p.N, p.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
-  if (gemm_variant() == 4 && gemm4w_applicable(p)) {
-    launch_gemm4w(p, stream);
+void launch_gemm(const GemmLaunch& p_, void* stream) {
+  if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
+  if (gemm_variant() == 4 && gemm4w_applicable(p_)) {
+    launch_gemm4w(p_, stream);
     return;
   }
-  if (p.ln_stats && !p.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
-  if (p.out < 0 || p.out > 2 || (p.out != 0) != (p.split != 0))
+  if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
+  if (p_.out < 0 || p_.out > 2 || (p_.out != 0) != (p_.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
-  if (p.split && p.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
-  if (p.split && !split_k_ok(p.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
+  if (p_.split && p_.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
+  if (p_.split && !split_k_ok(p_.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
+  const GemmLaunch& p = p_;
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);

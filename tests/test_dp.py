@@ -52,7 +52,9 @@ def _worker_body(rank, world, port, q, device="cpu", backend="rccl"):
     full = [outs[1].clone().cpu(), outs[2].clone().cpu()]  # slots of steps 1 and 2
     with torch.no_grad():
         local = [model(xs[1]).cpu(), model(xs[2]).cpu()]
-    q.put((rank, full, local))
+    # numpy arrays pickle by value: a torch tensor would travel as a shared-memory handle that the
+    # parent can only open while this process is still alive (ConnectionResetError races)
+    q.put((rank, [t.numpy() for t in full], [t.numpy() for t in local]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -74,10 +76,11 @@ def _run_dp(device, backend="rccl"):
         p.join(timeout=60)
         assert p.exitcode == 0
     for step in (0, 1):
-        expected = torch.cat([res[r][1][step] for r in range(world)], 0)
+        expected = torch.cat([torch.from_numpy(res[r][1][step]) for r in range(world)], 0)
         for r in range(world):
-            assert res[r][0][step].shape == expected.shape
-            assert torch.allclose(res[r][0][step], expected, atol=1e-5), (r, step)
+            got = torch.from_numpy(res[r][0][step])
+            assert got.shape == expected.shape
+            assert torch.allclose(got, expected, atol=1e-5), (r, step)
 
 
 @pytest.mark.parametrize("backend", ["rccl", "ipc"])
