@@ -151,13 +151,14 @@ class _EngineFn:
         return self.eng.graph.run(x)[0]
 
 
-def build_runner(cfg, dtype, B, dev, a, seed):
+def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0):
     """Model -> (default) ONNX export with its com.amd.dft nodes -> serialized engine bytes ->
     deserialized engine -> hipGraph-captured DP runner: the timed step is the engine a user
     would load with ``dftexec --loadEngine`` (reference: export -> build -> serialize ->
     deserialize -> execute_v2, /root/reference/tests/test_dft.py:89-115)."""
-    torch.manual_seed(seed)
+    torch.manual_seed(seed)  # the same weights on every rank (data parallel = one model)
     model = AFNONet(cfg, backend="amd").to(dev).to(dtype).eval()
+    torch.manual_seed(seed + 1 + input_seed)  # each rank's own batch
     x = torch.randn(B, cfg.in_chans, *cfg.img_size, device=dev).to(dtype)
     info = {"engine": False}
     fn = model
@@ -233,7 +234,7 @@ def main(argv=None) -> int:
         extra.update(time_fno_block_us())
         log(f"single-op probes: {extra}")
 
-    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234 + rank)
+    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234, rank)
     log(f"world={world} batch/GPU={B} dtype={head_dt}")
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
@@ -246,7 +247,7 @@ def main(argv=None) -> int:
 
     if cuda and a.extra_steps > 0 and not a.tiny:
         other = "bf16" if a.dtype == "fp32" else "fp32"
-        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 4321 + rank)
+        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 4321, rank)
         e2 = run_steps(r2, a.extra_steps, 2, world, dev, cuda)
         extra[f"{other}_samples_per_s"] = round(world * B / (e2 / a.extra_steps), 3)
         extra[f"{other}_ms_per_step"] = round(e2 * 1000.0 / a.extra_steps, 3)
