@@ -59,8 +59,7 @@ def _worker_body(rank, world, port, q, device="cpu", backend="rccl"):
     dist.destroy_process_group()
 
 
-def _run_dp(device, backend="rccl"):
-    world = 2
+def _run_dp(device, backend="rccl", world=2):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -88,6 +87,13 @@ def test_dp_allgather_gloo_world2(backend):
     """CPU, Gloo, world 2: the RCCL-path collective (Gloo all_gather) and the direct-push IPC
     protocol (/dev/shm transport: same slot / offset / handshake logic as the GPU transport)."""
     _run_dp("cpu", backend)
+
+
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_dp_allgather_gloo_world3(backend):
+    """An odd world size: every rank's slot offset and every peer push list differ from world 2
+    (rehearses the 8-GPU node's rank arithmetic on the CPU)."""
+    _run_dp("cpu", backend, world=3)
 
 
 @pytest.mark.gpu
