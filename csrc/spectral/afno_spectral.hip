@@ -51,8 +51,12 @@ constexpr int kNT = 256;  // threads
 #ifndef AFNO_BPF
 #define AFNO_BPF 2  // k-steps of B-fragment prefetch in the block-MLP GEMMs
 #endif
+#ifndef AFNO_BPF3
+#define AFNO_BPF3 2  // k-steps of B-fragment prefetch in the bf16x3 block-MLP GEMMs
+#endif
 #ifndef AFNO_ABLATE
-#define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs
+#define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs,
+                       // 4 = x3 GEMM B fragments of k-step 0 reused (no weight loads after the first)
 #endif
 
 // Compile-time geometry of one instance: H = L = R0 x R1, block size BS.
@@ -183,6 +187,7 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
         bq[(ks + D) % NQ][nj] =
             *reinterpret_cast<const bf16x8*>(Bt + ((S::NTW * w + nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of its use (see gemm_tile_x3)
     bf16x8 afr[S::MT];
 #pragma unroll
     for (int mi = 0; mi < S::MT; ++mi)
@@ -415,23 +420,32 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
   for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 bh[2][S::NTW], bl[2][S::NTW];
+  // B (weight) fragments stream from L2 AFNO_BPF3 k-steps ahead: with one k-step of lookahead
+  // the L2 latency is exposed every k-step (bench/afno_ablate.hip, AFNO_ABLATE=4: -164 us)
+  constexpr int D0 = S::NTW >= 4 ? 1 : AFNO_BPF3;  // 4 column tiles per wave: no registers for 2
+  constexpr int D = D0 < S::KS ? D0 : S::KS - 1, NQ = D + 1;
+  bf16x8 bh[NQ][S::NTW], bl[NQ][S::NTW];
 #pragma unroll
-  for (int nj = 0; nj < S::NTW; ++nj) {
-    const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + kq * 8;
-    bh[0][nj] = *reinterpret_cast<const bf16x8*>(row);
-    bl[0][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
-  }
+  for (int s2 = 0; s2 < D; ++s2)
+#pragma unroll
+    for (int nj = 0; nj < S::NTW; ++nj) {
+      const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
+      bh[s2][nj] = *reinterpret_cast<const bf16x8*>(row);
+      bl[s2][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
+    }
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
-    if (ks + 1 < S::KS) {
+    if (ks + D < S::KS && !(AFNO_ABLATE & 4)) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
-        const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + (ks + 1) * 64 + kq * 8;
-        bh[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row);
-        bl[(ks + 1) & 1][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
+        const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
+        bh[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row);
+        bl[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
       }
     }
+    // keep the prefetch where it is written: the scheduler otherwise sinks these loads next to
+    // their MFMAs (lower register pressure) and every k-step waits for an L2 round trip
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mi = 0; mi < S::MT; ++mi) {
       const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ah + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
@@ -439,13 +453,13 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
         if constexpr (AFNO_ABLATE & 2) {
-          acc[mi][nj] += __builtin_bit_cast(f32x4, al) + __builtin_bit_cast(f32x4, bh[ks & 1][nj]) +
-                         __builtin_bit_cast(f32x4, ah) + __builtin_bit_cast(f32x4, bl[ks & 1][nj]);
+          acc[mi][nj] += __builtin_bit_cast(f32x4, al) + __builtin_bit_cast(f32x4, bh[ks % NQ][nj]) +
+                         __builtin_bit_cast(f32x4, ah) + __builtin_bit_cast(f32x4, bl[ks % NQ][nj]);
           continue;
         }
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks & 1][nj], acc[mi][nj], 0, 0, 0);
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks & 1][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
       }
     }
   }
