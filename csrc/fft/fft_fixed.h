@@ -31,4 +31,5 @@ std::vector<int32_t> fixed_radices(int32_t L);
 // Launch the best fixed configuration for d; returns false when none applies.
 bool launch_fft_fixed(const PassDesc& d, void* stream);
 
+
 }  // namespace amd_dft

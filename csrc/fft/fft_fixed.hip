@@ -34,7 +34,10 @@ std::vector<int32_t> fixed_radices(int32_t L) {
   return {};
 }
 
-bool launch_fft_fixed(const PassDesc& d, void* stream) {
+namespace {
+
+// Picks the configuration for d and fills its kernel arguments; false if none applies.
+bool prepare_fixed(const PassDesc& d, int& best_out, FixedArgs& a, int64_t& nblocks_out) {
   // MI_DFT_FIXED=0 disables the specialised kernels (A/B tests); MI_DFT_FIXED_CFG="TP,T"
   // forces one configuration.
   const char* fe = std::getenv("MI_DFT_FIXED");
@@ -82,7 +85,7 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
   }
   if (best < 0) return false;
   const FixedCfg& cfg = cfgs[best];
-  FixedArgs a;
+  a = FixedArgs{};
   a.in = d.in;
   a.out = d.out;
   a.tw = static_cast<const float2*>(d.tw);
@@ -124,7 +127,6 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     if (!ok) return false;
   }
   const int64_t nblocks = d.O * a.tiles_per_outer;
-  if (nblocks <= 0) return true;
   if (nblocks > 0x7fffffffLL) throw std::runtime_error("amd_dft: FFT grid too large");
   {
     // XCD-aware tile order for column layouts whose tile row is narrower than a 128-B line
@@ -137,6 +139,19 @@ bool launch_fft_fixed(const PassDesc& d, void* stream) {
     const char* ab = std::getenv("MI_DFT_FFT_ABLATE");
     a.ablate = ab ? std::atoi(ab) : 0;
   }
+  best_out = best;
+  nblocks_out = nblocks;
+  return true;
+}
+
+}  // namespace
+
+bool launch_fft_fixed(const PassDesc& d, void* stream) {
+  int best = -1;
+  FixedArgs a;
+  int64_t nblocks = 0;
+  if (!prepare_fixed(d, best, a, nblocks)) return false;
+  if (nblocks <= 0) return true;
   LaunchFn fn = d.kind == Kind::C2C ? c2c_launcher(best) : (d.kind == Kind::R2C ? r2c_launcher(best) : c2r_launcher(best));
   fn(a, dim3(static_cast<uint32_t>(nblocks)), static_cast<hipStream_t>(stream));
   hipError_t err = hipGetLastError();

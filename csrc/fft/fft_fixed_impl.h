@@ -392,17 +392,12 @@ __device__ __forceinline__ int32_t xcd_block(int32_t b, int32_t nb) {
 }
 
 template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>
-__global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
+__device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int tid, bool active, float2* lds) {
   constexpr int L = F::L;
-  constexpr int LDSN = COLS ? lds_pad(L * T) + 2 : T * (lds_pad(L) + 1);
-  __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
   Ctx x;
   x.a = a;
-  const int tid = threadIdx.x;
   x.t = COLS ? tid % T : tid / TP;
   x.tp = COLS ? tid / T : tid % TP;
-  const int32_t bid = a.xcd_nb > 0 ? xcd_block(static_cast<int32_t>(blockIdx.x), a.xcd_nb)
-                                   : static_cast<int32_t>(blockIdx.x);
   const int32_t o = bid / a.tiles_per_outer;
   const int32_t tile = bid - o * a.tiles_per_outer;
   x.c = tile * T + x.t;
@@ -419,6 +414,10 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
       x.i0c = x.ok0 ? 2 * x.c : a.I - 1;
       x.i1c = x.ok1 ? 2 * x.c + 1 : a.I - 1;
     }
+  }
+  if (!active) {  // spare threads of a larger fused workgroup: run the same passes on a private
+    x.ok0 = false;  // LDS slot (barriers stay uniform), store nothing
+    x.ok1 = false;
   }
   x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
   x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
@@ -467,10 +466,23 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   AMD_DFT_STAMP(a, 8, static_cast<long long>(__builtin_amdgcn_s_memrealtime()));
 }
 
+// LDS image of one tile (float2 entries) for T signal slots
+template <bool COLS, int T, int L>
+constexpr int tile_lds(int slots = T) {
+  return COLS ? lds_pad(L * T) + 2 : slots * (lds_pad(L) + 1);
+}
+
+template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>
+__global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
+  __shared__ __attribute__((aligned(16))) float2 lds[tile_lds<COLS, T, F::L>()];
+  const int32_t bid = a.xcd_nb > 0 ? xcd_block(static_cast<int32_t>(blockIdx.x), a.xcd_nb)
+                                   : static_cast<int32_t>(blockIdx.x);
+  fixed_tile<K, COLS, TP, T, F, BFI, BFO, PR, NADD, PV>(a, bid, static_cast<int>(threadIdx.x), true, lds);
+}
+
 // ------------------------------------------------------------------ config table
 #define AMD_DFT_FIXED_CONFIGS(X)          \
   X(1440, false, 144, 1, 10, 12, 12)      \
-  X(1440, false, 128, 1, 10, 12, 12)      \
   X(720, false, 90, 2, 8, 9, 10)          \
   X(1024, false, 128, 1, 8, 8, 16)        \
   X(2048, false, 256, 1, 8, 16, 16)       \
@@ -482,7 +494,6 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \
   X(720, true, 45, 16, 8, 9, 10)          \
-  X(720, true, 64, 4, 8, 9, 10)           \
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)            \
   X(180, true, 15, 32, 12, 15)

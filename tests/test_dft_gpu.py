@@ -239,3 +239,31 @@ def test_long_length_2d_and_pruned(device):
     full = torch.fft.rfft2(x.double().cpu())
     ref = torch.cat([full[:, :3, :40], full[:, -2:, :40]], 1)
     assert rel_l2(yp, ref) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(720, 1440), (1, 720, 1440)])
+def test_rfft2_irfft2_720x1440_graph_replays(device, shape):
+    """The headline transform (XCD-ordered 4-column tiles) eagerly and under hipGraph replay
+    against torch.fft in fp64."""
+    torch.manual_seed(11)
+    x = torch.randn(*shape)
+    ref = torch.view_as_real(torch.fft.rfft2(x.double()))
+    xd = x.to(device)
+    y = tdp.contrib_rfft(xd, signal_ndim=2)
+    assert (y.cpu().double() - ref).norm() / ref.norm() < 2e-6
+    z = tdp.contrib_irfft(y, signal_ndim=2)
+    assert (z.cpu().double() - x.double()).norm() / x.double().norm() < 2e-6
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        tdp.contrib_irfft(tdp.contrib_rfft(xd, signal_ndim=2), signal_ndim=2)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        yg = tdp.contrib_rfft(xd, signal_ndim=2)
+        zg = tdp.contrib_irfft(yg, signal_ndim=2)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert (yg.cpu().double() - ref).norm() / ref.norm() < 2e-6
+    assert (zg.cpu().double() - x.double()).norm() / x.double().norm() < 2e-6
