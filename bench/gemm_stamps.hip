@@ -130,5 +130,27 @@ int main() {
   f2.out = 1;
   f2.stamps = stamps;
   run("fc2 x3 (+fp32 residual)", f2, stamps);
+  // bf16 operands (the bf16 model's MLP): x rows [M, K], hidden [M, 4C] bf16, bf16 residual
+  GemmLaunch g1;
+  g1.x = x;
+  g1.w = w1;
+  g1.bias = b1;
+  g1.y = h;
+  g1.M = M;
+  g1.N = Hd;
+  g1.K = C;
+  g1.act = 1;
+  g1.stamps = stamps;
+  run("fc1 bf16 + GELU", g1, stamps);
+  GemmLaunch g2;
+  g2.x = h;
+  g2.w = w2;
+  g2.residual = x;
+  g2.y = x;
+  g2.M = M;
+  g2.N = C;
+  g2.K = Hd;
+  g2.stamps = stamps;
+  run("fc2 bf16 (+bf16 residual)", g2, stamps);
   return 0;
 }
