@@ -1,0 +1,79 @@
+"""A/B of the hand GEMM kernel variants (MI_DFT_GEMM_KERNEL=8w | 2wg) on the FourCastNet MLP
+launches: bit-exactness of the outputs (both variants run the same MFMA sequence per output, so
+they must agree exactly) and timing (bench/bench_gemm.py --x3 in a child per variant, since the
+variant is read once per process).
+
+Usage: python bench/gemm_variant_ab.py [--rows 518400] [--rounds 3] [--variants 8w,2wg,2wg:60000]  (variant[:stagger cycles])
+"""
+import argparse
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys, torch
+sys.path.insert(0, %(root)r)
+import tensorrt_dft_plugins_amd as tdp
+tdp.load_plugins()
+ops = torch.ops.amd_dft
+torch.manual_seed(0)
+M = 20000 + 77  # ragged last token tile
+C, H = 768, 3072
+x = torch.randn(M, C, device="cuda")
+w1 = torch.randn(H, C, device="cuda") * 0.02
+w2 = torch.randn(C, H, device="cuda") * 0.02
+b1 = torch.randn(H, device="cuda") * 0.02
+r = torch.randn(M, C, device="cuda")
+xs, w1s, w2s = ops.split_bf16(x), ops.split_bf16(w1), ops.split_bf16(w2)
+h = ops.linear3(xs, w1s, b1, 1, None, True)
+y = ops.linear3(h, w2s, None, 0, r.clone(), False)
+y1 = ops.linear3(xs, w1s, b1, 0, None, False)
+xb, w1b, w2b = x.bfloat16(), w1.bfloat16(), w2.bfloat16()
+hb = ops.linear(xb, w1b, b1, 1, None)
+yb = ops.linear(hb, w2b, None, 0, r.bfloat16())
+torch.cuda.synchronize()
+torch.save({"h": h.cpu(), "y": y.cpu(), "y1": y1.cpu(), "hb": hb.cpu(), "yb": yb.cpu()}, sys.argv[1])
+print("saved", sys.argv[1], flush=True)
+"""
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=32 * 16200)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="8w,2wg")
+    ap.add_argument("--no-time", action="store_true")
+    a = ap.parse_args(argv)
+    outdir = os.environ.get("TMPDIR", "/tmp")
+    os.makedirs(outdir, exist_ok=True)
+    files = {}
+    for v in a.variants.split(","):
+        env = dict(os.environ, MI_DFT_GEMM_KERNEL=v.split(":")[0], MI_DFT_GEMM_STAGGER=(v.split(":") + ["0"])[1])
+        f = os.path.join(outdir, f"gemm_ab_{v.replace(':', '_')}.pt")
+        subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT}, f], env=env, check=True, timeout=300)
+        files[v] = f
+    import torch
+
+    vs = list(files)
+    base = torch.load(files[vs[0]], weights_only=True)
+    ok = True
+    for v in vs[1:]:
+        other = torch.load(files[v], weights_only=True)
+        for k in base:
+            same = torch.equal(base[k], other[k])
+            diff = (base[k].float() - other[k].float()).abs().max().item()
+            print(f"{vs[0]} vs {v} {k:3s}: bit-identical={same} max|diff|={diff:.3e}", flush=True)
+            ok &= same
+    if not a.no_time:
+        for v in vs:
+            print(f"== MI_DFT_GEMM_KERNEL={v}", flush=True)
+            env = dict(os.environ, MI_DFT_GEMM_KERNEL=v.split(":")[0], MI_DFT_GEMM_STAGGER=(v.split(":") + ["0"])[1])
+            subprocess.run([sys.executable, os.path.join(ROOT, "bench", "bench_gemm.py"), "--x3", "--rows", str(a.rows),
+                            "--rounds", str(a.rounds)], env=env, check=True, timeout=600)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

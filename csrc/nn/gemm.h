@@ -26,6 +26,7 @@ struct GemmLaunch {
   int res_rows = 0;          // > 0: residual row = token % res_rows (broadcast over the batch)
   // Un-patchify scatter (y is an image [B, sC, sh*8, sw*8]; feature order (c, py, px)).
   int sC = 0, sh = 0, sw = 0;
+  int stagger = 0;           // gemm2wg only: start delay (shader cycles) of second-resident workgroups
 #ifdef AMD_DFT_GEMM_STAMPS
   long long* stamps = nullptr;  // diagnostic build only (bench/gemm_stamps.hip): per-block phase clocks
 #endif
@@ -35,5 +36,8 @@ void launch_gemm(const GemmLaunch& p, void* stream);
 // four-wave 128x128-per-wave variant (gemm4w.hip) for plain token-major operands
 bool gemm4w_applicable(const GemmLaunch& p);
 void launch_gemm4w(const GemmLaunch& p, void* stream);
+// two-workgroups-per-CU 128x256 variant (gemm2wg.hip) for plain token-major operands
+bool gemm2wg_applicable(const GemmLaunch& p);
+void launch_gemm2wg(const GemmLaunch& p, void* stream);
 
 }  // namespace amd_dft

@@ -479,8 +479,10 @@ static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
 // accumulator file and shuffles them back every few MFMAs)
 static int gemm_variant() {
   static const int v = [] {
-    const char* e = std::getenv("MI_DFT_GEMM_KERNEL");  // "4w": the experimental 4-wave kernel
-    return (e && std::string(e) == "4w") ? 4 : 8;
+    const char* e = std::getenv("MI_DFT_GEMM_KERNEL");  // "4w" / "2wg" / "8w"
+    if (e && std::string(e) == "4w") return 4;
+    if (e && std::string(e) == "2wg") return 2;
+    return 8;
   }();
   return v;
 }
@@ -489,6 +491,17 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
   if (gemm_variant() == 4 && gemm4w_applicable(p_)) {
     launch_gemm4w(p_, stream);
+    return;
+  }
+  if (gemm_variant() == 2 && gemm2wg_applicable(p_) && !(p_.split && p_.ln_stats) &&
+      (p_.out != 0) == (p_.split != 0) && !(p_.ln_stats && !p_.ln_c1)) {
+    static const int stagger = [] {
+      const char* e = std::getenv("MI_DFT_GEMM_STAGGER");  // experiment: cycles
+      return e ? std::atoi(e) : 0;
+    }();
+    GemmLaunch q = p_;
+    q.stagger = stagger;
+    launch_gemm2wg(q, stream);
     return;
   }
   if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");

@@ -1,0 +1,382 @@
+// Two-workgroups-per-CU variant of the fused-epilogue GEMM (csrc/nn/gemm.hip) for plain
+// token-major operands (the FourCastNet MLP: fc1 + GELU, fc2 + residual, bf16 or bf16x3 split).
+//
+// Why: gemm.hip runs ONE 512-thread workgroup per CU (128 KB of LDS) whose two wave groups
+// ping-pong MFMA against LDS reads.  Its epilogue (bias, erf-GELU, split, 256 KB of stores) is
+// 25 % of a bf16x3 fc1 tile (profiles/gemm_stamps_r2.txt: 28k of 114k cycles) and nothing else
+// runs on the CU meanwhile.  Here a workgroup is 4 waves computing a 128-feature x 256-token
+// tile with the same 128 x 64 per-wave tile, fragment reads, MFMA quadrants and epilogue, but
+// its operand staging needs only 72 KB of LDS, so TWO workgroups share a CU (one wave of each
+// per SIMD): while one runs its epilogue (VALU + stores) the other keeps the matrix cores busy,
+// and their MFMA / LDS-read bursts interleave without an explicit ping-pong.
+//
+// LDS: two rings instead of two full K-tile stages.
+//   A ring: 3 slots x 8 KB  (64 feature rows x 128 B: RA0 = rows 0..63, RA1 = rows 64..127)
+//   B ring: 3 slots x 16 KB (128 token rows: RB0 = tokens {64c + 0..31}, RB1 = {64c + 32..63})
+// Phase schedule per 64-deep K-tile t (one region DMA'd per phase, read 4 phases later):
+//   q0: read RB0(t) -> b0, MFMA (a0, b0); DMA RB0(t+1)
+//   q1: read RB1(t) -> b1, MFMA (a0, b1); DMA RB1(t+1)
+//   q2: read RA1(t) -> a1, MFMA (a1, b1); DMA RA1(t+1)
+//   q3: read RA0(t+1) -> a0, MFMA (a1, b0); DMA RA0(t+2)
+// A region's slot is reused 3 loads later; its previous occupant was read at least one phase
+// earlier, and every phase starts with a barrier that follows each wave's lgkmcnt(0), so the
+// DMA never overwrites bytes a wave still reads.  vmcnt is counted per region (B: 4, A: 2
+// instructions per wave), so three regions stay in flight across the barriers.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+#include "../fft/dev_check.h"
+#include "gemm.h"
+
+namespace amd_dft {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kBF = 128;  // features per workgroup
+constexpr int kBT = 256;  // tokens per workgroup
+constexpr int kBK = 64;   // physical K columns per K-tile (bf16: 64-deep; split: 32-deep hi | lo)
+constexpr int kThreads = 256;
+constexpr int kA = 64 * 128;   // A region bytes
+constexpr int kB = 128 * 128;  // B region bytes
+constexpr int kLds = 3 * kA + 3 * kB;  // 72 KB
+
+__device__ __forceinline__ float gelu_erf(float v) {
+  const float z = fabsf(v) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = fmaf(-p, __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z), 1.f);
+  return 0.5f * v * (1.f + copysignf(e, v));
+}
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 v;
+  v[0] = static_cast<__bf16>(a);
+  v[1] = static_cast<__bf16>(b);
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
+
+// Phase R reads (R mod 4): 0 RB0, 1 RB1, 2 RA1 of tile R/4; 3 RA0 of tile (R+1)/4.
+__device__ __forceinline__ int tile_of(int R) { return (R >> 2) + ((R & 3) == 3 ? 1 : 0); }
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+struct Ctx {
+  const uint16_t* W;
+  const uint16_t* X;
+  int64_t ld;  // row stride of both operands (bf16 elements)
+  int f0, t0, M, KT, wave, lane;
+  char* smem;
+};
+
+// DMA the region read at phase R (lane-linear LDS writes; the 16-byte chunk swizzle is applied
+// to the source address, the inverse of swz()).
+__device__ __forceinline__ void stage(const Ctx& c, int R) {
+  const int q = R & 3, t = tile_of(R);
+  const int pos = c.lane & 7;
+  if (q >= 2) {  // A: 64 feature rows, 2 instructions per wave
+    const int h = q == 2 ? 1 : 0;
+    char* dst = c.smem + ((2 * t + h) % 3) * kA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rb = (c.wave * 2 + i) * 8, row = rb + (c.lane >> 3);
+      const uint16_t* g = c.W + static_cast<int64_t>(c.f0 + h * 64 + row) * c.ld + t * kBK + (pos ^ (row & 7)) * 8;
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
+    }
+  } else {  // B: 128 token rows, 4 instructions per wave
+    const int h = q;
+    char* dst = c.smem + 3 * kA + ((2 * t + h) % 3) * kB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rb = (c.wave * 4 + i) * 8, row = rb + (c.lane >> 3);
+      const int tok = min(c.t0 + (row >> 5) * 64 + h * 32 + (row & 31), c.M - 1);
+      const uint16_t* g = c.X + static_cast<int64_t>(tok) * c.ld + t * kBK + (pos ^ (row & 7)) * 8;
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
+    }
+  }
+}
+
+// vector-memory instructions per wave of the DMA issued at phase P (0 if that region is past K)
+__device__ __forceinline__ int dma_cnt(int P, int KT) {
+  if (tile_of(P + 4) >= KT) return 0;
+  return (P & 3) < 2 ? 4 : 2;
+}
+
+__device__ __forceinline__ void read_a(bf16x8 (&a)[8], const char* slot, int r16, int kq) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[s * 4 + i] = *reinterpret_cast<const bf16x8*>(slot + swz(i * 16 + r16, s * 4 + kq));
+}
+__device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* slot, int wc, int r16, int kq) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      b[s * 2 + j] = *reinterpret_cast<const bf16x8*>(slot + swz(wc * 32 + j * 16 + r16, s * 4 + kq));
+}
+
+template <int MI, int NI, bool SPLIT>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
+  constexpr int NP = SPLIT ? 3 : 2;
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < NP; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int sa = SPLIT ? (s == 1 ? 1 : 0) : s;  // SPLIT products: (hi, hi), (lo, hi), (hi, lo)
+        const int sb = SPLIT ? (s == 2 ? 1 : 0) : s;
+        acc[MI * 4 + i][NI * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[sa * 4 + i], b[sb * 2 + j],
+                                                                                acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
+      }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int ACT, bool BIAS, bool RES, bool LN, bool SPLIT, int OUT>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm2wg_kernel(GemmLaunch p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M = p.M, N = p.N, K = p.K;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;  // wave = token column wc
+  // XCD-aware tile order (bijective): consecutive tiles of one XCD share the token panel
+  const int tiles_f = N / kBF;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  const int tt = lid / tiles_f, ft = lid - tt * tiles_f;
+  const int f0 = ft * kBF, t0 = tt * kBT;
+  const int KT = SPLIT ? K / 32 : K / kBK;
+  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && KT > 0, "gemm2wg_kernel");
+  const int r16 = lane & 15, kq = lane >> 4;
+  const Ctx c{p.w, p.x, SPLIT ? 2 * static_cast<int64_t>(K) : static_cast<int64_t>(K), f0, t0, M, KT, wave, lane, smem};
+
+  // optional start stagger (p.stagger cycles) for the second resident workgroup of each CU in the
+  // first dispatch round, so the two workgroups of a CU run out of phase
+  if (p.stagger > 0 && b < 8 * 64 && (b >> 3) >= 32) {
+    const long long s0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - s0 < p.stagger) __builtin_amdgcn_s_sleep(8);
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: the regions read at phases -1 (RA0(0)), 0, 1, 2, 3
+  for (int R = -1; R <= 3; ++R)
+    if (tile_of(R) < KT) stage(c, R);
+  bf16x8 a0[8], a1[8], b0[4], b1[4];
+  wait_vm(dma_cnt(-4, KT) + dma_cnt(-3, KT) + dma_cnt(-2, KT) + dma_cnt(-1, KT));
+  barrier();
+  read_a(a0, smem + 0 * kA, r16, kq);  // RA0(0): A slot 0
+
+  const char* aring = smem;
+  const char* bring = smem + 3 * kA;
+  for (int t = 0; t < KT; ++t) {
+    const int R = 4 * t;
+    // ---- q0: (mi 0, ni 0) from RB0(t)
+    wait_vm(dma_cnt(R - 3, KT) + dma_cnt(R - 2, KT) + dma_cnt(R - 1, KT));
+    barrier();
+    if (tile_of(R + 4) < KT) stage(c, R + 4);
+    read_b(b0, bring + ((2 * t) % 3) * kB, wave, r16, kq);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<0, 0, SPLIT>(acc, a0, b0);
+    // ---- q1: (0, 1) from RB1(t)
+    wait_vm(dma_cnt(R - 2, KT) + dma_cnt(R - 1, KT) + dma_cnt(R, KT));
+    barrier();
+    if (tile_of(R + 5) < KT) stage(c, R + 5);
+    read_b(b1, bring + ((2 * t + 1) % 3) * kB, wave, r16, kq);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<0, 1, SPLIT>(acc, a0, b1);
+    // ---- q2: (1, 1) from RA1(t)
+    wait_vm(dma_cnt(R - 1, KT) + dma_cnt(R, KT) + dma_cnt(R + 1, KT));
+    barrier();
+    if (tile_of(R + 6) < KT) stage(c, R + 6);
+    read_a(a1, aring + ((2 * t + 1) % 3) * kA, r16, kq);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma_quadrant<1, 1, SPLIT>(acc, a1, b1);
+    // ---- q3: (1, 0); A0 fragments of K-tile t+1 are read here
+    wait_vm(dma_cnt(R, KT) + dma_cnt(R + 1, KT) + dma_cnt(R + 2, KT));
+    barrier();
+    if (tile_of(R + 7) < KT) stage(c, R + 7);
+    if (t + 1 < KT) read_a(a0, aring + ((2 * t + 2) % 3) * kA, r16, kq);
+    mfma_quadrant<1, 0, SPLIT>(acc, a1, b0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // ---- epilogue (as gemm.hip): lane holds features f..f+3 of token t for each (i, j) tile;
+  // all loads up front / from clamped rows, only the stores are predicated on t < M
+  auto tok = [&](int j) { return t0 + wave * 64 + j * 16 + r16; };
+  auto tokc = [&](int j) { return min(tok(j), M - 1); };
+  auto off = [&](int i, int j) -> int64_t { return static_cast<int64_t>(tokc(j)) * N + f0 + i * 16 + 4 * kq; };
+  typedef typename std::conditional<OUT == 1, float4, uint2>::type ResT;
+  auto load_res = [&](int i, int j) -> ResT {
+    if constexpr (OUT == 1) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + off(i, j));
+    else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + off(i, j));
+  };
+  float4 bias4[8], c14[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int f = f0 + i * 16 + 4 * kq;
+    bias4[i] = BIAS ? *reinterpret_cast<const float4*>(p.bias + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    c14[i] = LN ? *reinterpret_cast<const float4*>(p.ln_c1 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float2 lst[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
+  ResT rq[RES ? 2 : 1][2][4];
+  if constexpr (RES) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rq[0][ii][j] = load_res(ii, j);
+  }
+#pragma unroll
+  for (int ip = 0; ip < 4; ++ip) {
+    if constexpr (RES) {
+      if (ip + 1 < 4) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rq[(ip + 1) & 1][ii][j] = load_res(2 * (ip + 1) + ii, j);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = 2 * ip + ii;
+      const int f = f0 + i * 16 + 4 * kq;
+      const float bv[4] = {bias4[i].x, bias4[i].y, bias4[i].z, bias4[i].w};
+      const float cv[4] = {c14[i].x, c14[i].y, c14[i].z, c14[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = acc[i][j][e];
+          if constexpr (LN) a = lst[j].y * fmaf(-lst[j].x, cv[e], a);
+          v[e] = a + bv[e];
+          if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
+        }
+        if constexpr (RES) {
+          const ResT rr = rq[ip & 1][ii][j];
+          if constexpr (OUT == 1) {
+            v[0] += rr.x;
+            v[1] += rr.y;
+            v[2] += rr.z;
+            v[3] += rr.w;
+          } else {
+            v[0] += __uint_as_float(rr.x << 16);
+            v[1] += __uint_as_float(rr.x & 0xffff0000u);
+            v[2] += __uint_as_float(rr.y << 16);
+            v[3] += __uint_as_float(rr.y & 0xffff0000u);
+          }
+        }
+        if (tok(j) < M) {
+          if constexpr (OUT == 1) {
+            *reinterpret_cast<float4*>(static_cast<float*>(p.y) + off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
+          } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved
+            float lo[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
+            uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(tok(j)) * (2 * N) + (f >> 5) * 64 + (f & 31);
+            *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
+          } else {
+            *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + off(i, j)) =
+                make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int ACT, bool BIAS, bool RES, bool LN, bool SPLIT, int OUT>
+void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  auto kern = gemm2wg_kernel<ACT, BIAS, RES, LN, SPLIT, OUT>;
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm2wg attr: ") + hipGetErrorString(e));
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
+}
+
+template <int ACT, bool BIAS>
+void launch_act_bias(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if (p.split) {
+    if (p.out == 2) launch_one<ACT, BIAS, false, false, true, 2>(p, st, grid);
+    else if (p.residual) launch_one<ACT, BIAS, true, false, true, 1>(p, st, grid);
+    else launch_one<ACT, BIAS, false, false, true, 1>(p, st, grid);
+  } else if (p.ln_stats) {
+    if (p.residual) launch_one<ACT, BIAS, true, true, false, 0>(p, st, grid);
+    else launch_one<ACT, BIAS, false, true, false, 0>(p, st, grid);
+  } else {
+    if (p.residual) launch_one<ACT, BIAS, true, false, false, 0>(p, st, grid);
+    else launch_one<ACT, BIAS, false, false, false, 0>(p, st, grid);
+  }
+}
+
+}  // namespace
+
+// plain token-major operands (no patch gather / scatter), N a multiple of 128; the other
+// preconditions (K, split / out / LN combinations) are checked by launch_gemm before dispatch
+bool gemm2wg_applicable(const GemmLaunch& p) {
+  return p.gC == 0 && p.sC == 0 && p.res_rows == 0 && p.N % kBF == 0 && p.M >= 1 &&
+         (p.split ? (p.K % 32 == 0 && p.K >= 64) : (p.K % kBK == 0 && p.K >= kBK)) &&
+         !(p.out == 2 && p.residual);
+}
+
+void launch_gemm2wg(const GemmLaunch& p, void* stream) {
+  if (!gemm2wg_applicable(p)) throw std::runtime_error("amd_dft: gemm2wg: unsupported launch");
+  const int64_t nwg = ((static_cast<int64_t>(p.M) + kBT - 1) / kBT) * (p.N / kBF);
+  if (nwg >= (int64_t(1) << 31)) throw std::runtime_error("amd_dft: gemm2wg: grid too large");
+  const dim3 grid(static_cast<uint32_t>(nwg));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool bias = p.bias != nullptr;
+  if (p.act == 1) {
+    if (bias) launch_act_bias<1, true>(p, st, grid);
+    else launch_act_bias<1, false>(p, st, grid);
+  } else {
+    if (bias) launch_act_bias<0, true>(p, st, grid);
+    else launch_act_bias<0, false>(p, st, grid);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm2wg launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace amd_dft
