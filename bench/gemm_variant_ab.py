@@ -1,9 +1,9 @@
-"""A/B of the hand GEMM kernel variants (MI_DFT_GEMM_KERNEL=8w | 2wg) on the FourCastNet MLP
+"""A/B of the hand GEMM kernel variants (MI_DFT_GEMM_KERNEL=8w | 2wg, MI_DFT_GEMM_EPI) on the FourCastNet MLP
 launches: bit-exactness of the outputs (both variants run the same MFMA sequence per output, so
 they must agree exactly) and timing (bench/bench_gemm.py --x3 in a child per variant, since the
 variant is read once per process).
 
-Usage: python bench/gemm_variant_ab.py [--rows 518400] [--rounds 3] [--variants 8w,2wg,2wg:60000]  (variant[:stagger cycles])
+Usage: python bench/gemm_variant_ab.py [--rows 518400] [--rounds 3] [--variants 8w+direct,8w,2wg]  (kernel[:stagger cycles][+direct])
 """
 import argparse
 import os
@@ -39,6 +39,15 @@ print("saved", sys.argv[1], flush=True)
 """
 
 
+def variant_env(v: str) -> dict:
+    """"8w", "8w+direct" (epilogue stored straight from the MFMA layout), "8w:50" (odd CUs start
+    50 % of a tile late), "2wg", "2wg:60000" (second-resident workgroups start 60000 cycles late)."""
+    kern, _, epi = v.partition("+")
+    kern, _, stagger = kern.partition(":")
+    key = "MI_DFT_GEMM2WG_STAGGER" if kern == "2wg" else "MI_DFT_GEMM_STAGGER"
+    return {"MI_DFT_GEMM_KERNEL": kern, key: stagger or "0", "MI_DFT_GEMM_EPI": epi or "staged"}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=32 * 16200)
@@ -50,8 +59,8 @@ def main(argv=None):
     os.makedirs(outdir, exist_ok=True)
     files = {}
     for v in a.variants.split(","):
-        env = dict(os.environ, MI_DFT_GEMM_KERNEL=v.split(":")[0], MI_DFT_GEMM_STAGGER=(v.split(":") + ["0"])[1])
-        f = os.path.join(outdir, f"gemm_ab_{v.replace(':', '_')}.pt")
+        env = dict(os.environ, **variant_env(v))
+        f = os.path.join(outdir, f"gemm_ab_{v.replace(':', '_').replace('+', '_')}.pt")
         subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT}, f], env=env, check=True, timeout=300)
         files[v] = f
     import torch
@@ -69,7 +78,7 @@ def main(argv=None):
     if not a.no_time:
         for v in vs:
             print(f"== MI_DFT_GEMM_KERNEL={v}", flush=True)
-            env = dict(os.environ, MI_DFT_GEMM_KERNEL=v.split(":")[0], MI_DFT_GEMM_STAGGER=(v.split(":") + ["0"])[1])
+            env = dict(os.environ, **variant_env(v))
             subprocess.run([sys.executable, os.path.join(ROOT, "bench", "bench_gemm.py"), "--x3", "--rows", str(a.rows),
                             "--rounds", str(a.rounds)], env=env, check=True, timeout=600)
     return 0 if ok else 1

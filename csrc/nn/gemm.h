@@ -26,7 +26,8 @@ struct GemmLaunch {
   int res_rows = 0;          // > 0: residual row = token % res_rows (broadcast over the batch)
   // Un-patchify scatter (y is an image [B, sC, sh*8, sw*8]; feature order (c, py, px)).
   int sC = 0, sh = 0, sw = 0;
-  int stagger = 0;           // gemm2wg only: start delay (shader cycles) of second-resident workgroups
+  int direct_epi = 0;        // gemm.hip MODE 0: 1 = store straight from the MFMA layout (A/B only)
+  int stagger = 0;           // start delay (shader cycles) of staggered first-round workgroups (experiment)
 #ifdef AMD_DFT_GEMM_STAMPS
   long long* stamps = nullptr;  // diagnostic build only (bench/gemm_stamps.hip): per-block phase clocks
 #endif

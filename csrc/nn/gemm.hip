@@ -275,6 +275,13 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         gb[r][i] = (b * p.gC * (p.gh * 8) + ii * 8) * rowlen + jj * 8;
       }
   }
+  // optional first-round stagger: odd CUs of each XCD (blockIdx / 8 odd, first dispatch round)
+  // start p.stagger shader cycles late, so that the CUs' epilogue store bursts interleave with
+  // other CUs' main loops instead of all hitting HBM together
+  if (p.stagger > 0 && b < 256 && ((b >> 3) & 1)) {
+    const long long s0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - s0 < p.stagger) __builtin_amdgcn_s_sleep(8);
+  }
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
   stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
   stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
@@ -293,8 +300,8 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
 
 #ifndef GEMM_ABLATE
-#define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads
-#endif
+#define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads,
+#endif                 // bit 2 = epilogue computes but skips its stores
   for (int t = 0; t < KT; ++t) {
     char* cur = smem + (t & 1) * kStage;
     char* nxt = smem + ((t + 1) & 1) * kStage;
@@ -351,6 +358,104 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
+  if constexpr (MODE == 0) {
+    if (!p.direct_epi) {
+      // ---- LDS-staged epilogue (token-major outputs).  Writing straight from the MFMA layout
+      // makes every store instruction touch 16 rows with 32-64 B each (partial lines; the
+      // epilogue was 25 % of a bf16x3 fc1 tile and nearly all of it stores: profiles/
+      // gemm_epilogue_r2.txt).  Instead each wave parks act(acc + bias) as fp32 in its own 16 KB
+      // of the (now idle) stage buffers -- 64 tokens x 64 features per half, 16-byte chunks
+      // XOR-swizzled by row -- and reads it back row-contiguous: 16 B per lane, whole 128-byte
+      // lines per store instruction, the residual read the same coalesced way (prefetched
+      // before the half is staged), then the bf16 / fp32 / split-pair conversion.
+      barrier();  // every wave is past its last fragment read of the stage buffers
+      char* reg = smem + wave * (64 * 256);
+      const int tbase = t0 + wc * 64;
+      constexpr int LPR = OUT == 0 ? 8 : 16;    // lanes per token row
+      constexpr int RPI = 64 / LPR;             // rows per pass
+      constexpr int NIT = 64 / RPI;             // passes per half
+      const int c = lane % LPR, rsub = lane / LPR;
+      typedef typename std::conditional<OUT == 1, float4, uint4>::type RT;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
+        RT rr[RES ? NIT : 1];
+        if constexpr (RES) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16 features per lane
+#pragma unroll
+          for (int it = 0; it < NIT; ++it) {
+            const int64_t o = static_cast<int64_t>(min(tbase + it * RPI + rsub, M - 1)) * N + fh + (OUT == 1 ? 4 : 8) * c;
+            if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
+            else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+          }
+        }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = 4 * h + ii;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float a = acc[i][j][e];
+              if constexpr (LN) a = lst[j].y * fmaf(-lst[j].x, (&c14[i].x)[e], a);
+              v[e] = a + (&bias4[i].x)[e];
+              if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
+            }
+            const int row = j * 16 + r16, ch = ii * 4 + kq;
+            *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int row = it * RPI + rsub, t = tbase + row;
+          const char* rp = reg + row * 256;
+          if constexpr (OUT == 1) {
+            float4 v = *reinterpret_cast<const float4*>(rp + ((c ^ (row & 15)) << 4));
+            if constexpr (RES) {
+              v.x += rr[it].x;
+              v.y += rr[it].y;
+              v.z += rr[it].z;
+              v.w += rr[it].w;
+            }
+            if (t < M) *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
+          } else {
+            // OUT 0: lane = 8 features (chunks 2c, 2c+1); OUT 2: lane c = (half-chunk ch, part, sub)
+            const int fl = OUT == 0 ? 8 * c : (c >> 3) * 32 + (c & 3) * 8;
+            const float4 u0 = *reinterpret_cast<const float4*>(rp + (((fl >> 2) ^ (row & 15)) << 4));
+            const float4 u1 = *reinterpret_cast<const float4*>(rp + ((((fl >> 2) + 1) ^ (row & 15)) << 4));
+            float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+            if constexpr (OUT == 0 && RES) {
+              const uint32_t rw[4] = {rr[it].x, rr[it].y, rr[it].z, rr[it].w};
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                v[2 * k] += __uint_as_float(rw[k] << 16);
+                v[2 * k + 1] += __uint_as_float(rw[k] & 0xffff0000u);
+              }
+            }
+            if constexpr (OUT == 2) {
+              if ((c >> 2) & 1) {  // lo part
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] -= static_cast<float>(static_cast<__bf16>(v[k]));
+              }
+            }
+            const uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+            if (t < M) {
+              if constexpr (OUT == 0) {
+                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+              } else {
+                const int f = fh + fl;
+                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
+                                          ((c >> 2) & 1) * 32 + (f & 31)) = w;
+              }
+            }
+          }
+        }
+      }
+      GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
+      GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
+      return;
+    }
+  }
   constexpr bool ERES = RES;
   ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
   if constexpr (ERES) {
@@ -399,7 +504,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             v[3] += __uint_as_float(rr.y & 0xffff0000u);
           }
         }
-        if (tok(j) < M) {
+        if (tok(j) < M && !((GEMM_ABLATE & 4) && p.M > 0)) {
           if constexpr (OUT == 1) {
             *reinterpret_cast<float4*>(static_cast<float*>(p.y) + out_off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
           } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
@@ -487,6 +592,15 @@ static int gemm_variant() {
   return v;
 }
 
+// MI_DFT_GEMM_EPI=direct: the token-major epilogue stores straight from the MFMA layout (A/B only)
+static int gemm_direct_epi() {
+  static const int v = [] {
+    const char* e = std::getenv("MI_DFT_GEMM_EPI");
+    return (e && std::string(e) == "direct") ? 1 : 0;
+  }();
+  return v;
+}
+
 void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
   if (gemm_variant() == 4 && gemm4w_applicable(p_)) {
@@ -496,7 +610,7 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (gemm_variant() == 2 && gemm2wg_applicable(p_) && !(p_.split && p_.ln_stats) &&
       (p_.out != 0) == (p_.split != 0) && !(p_.ln_stats && !p_.ln_c1)) {
     static const int stagger = [] {
-      const char* e = std::getenv("MI_DFT_GEMM_STAGGER");  // experiment: cycles
+      const char* e = std::getenv("MI_DFT_GEMM2WG_STAGGER");  // experiment: cycles
       return e ? std::atoi(e) : 0;
     }();
     GemmLaunch q = p_;
@@ -509,7 +623,18 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
   if (p_.split && p_.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
   if (p_.split && !split_k_ok(p_.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
-  const GemmLaunch& p = p_;
+  GemmLaunch p = p_;
+  p.direct_epi = gemm_direct_epi();
+  {
+    // MI_DFT_GEMM_STAGGER: first-round start delay of odd CUs in percent of an estimated tile
+    // (~3300 shader cycles per K-tile + ~15k epilogue)
+    static const int pct = [] {
+      const char* e = std::getenv("MI_DFT_GEMM_STAGGER");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int kt = p.split ? p.K / 32 : p.K / kBK;
+    p.stagger = pct > 0 ? static_cast<int>((static_cast<int64_t>(kt) * 3300 + 15000) * pct / 100) : 0;
+  }
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);
