@@ -45,6 +45,7 @@
 #include <type_traits>
 
 #include "../fft/dev_check.h"
+#include "gelu.h"
 #include "gemm.h"
 
 namespace amd_dft {
@@ -61,18 +62,6 @@ constexpr int kThreads = 512;
 constexpr int kRegion = 128 * 128;     // 128 rows x 128 B (64 bf16 of K)
 constexpr int kStage = 4 * kRegion;    // one K-tile: 64 KB
 constexpr int kLds = 2 * kStage;       // two K-tiles: 128 KB
-
-__device__ __forceinline__ float gelu_erf(float v) {
-  const float z = fabsf(v) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = fmaf(-p, __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z), 1.f);
-  return 0.5f * v * (1.f + copysignf(e, v));
-}
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));

@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "../fft/dev_check.h"
+#include "gelu.h"
 #include "gemm.h"
 
 namespace amd_dft {
@@ -47,18 +48,6 @@ constexpr int kThreads = 256;
 constexpr int kA = 64 * 128;   // A region bytes
 constexpr int kB = 128 * 128;  // B region bytes
 constexpr int kLds = 3 * kA + 3 * kB;  // 72 KB
-
-__device__ __forceinline__ float gelu_erf(float v) {
-  const float z = fabsf(v) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = fmaf(-p, __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z), 1.f);
-  return 0.5f * v * (1.f + copysignf(e, v));
-}
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));

@@ -22,6 +22,7 @@
 #include <string>
 
 #include "../fft/dev_check.h"
+#include "gelu.h"
 #include "gemm.h"
 
 namespace amd_dft {
@@ -41,18 +42,6 @@ constexpr int kLds = 2 * kStage;        // double buffer (128 KB)
 constexpr int kDmaPerWave = 16;         // global_load_lds_dwordx4 per wave per stage
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
-
-__device__ __forceinline__ float gelu_erf(float v) {
-  const float z = fabsf(v) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = fmaf(-p, __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z), 1.f);
-  return 0.5f * v * (1.f + copysignf(e, v));
-}
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
