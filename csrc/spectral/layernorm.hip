@@ -6,6 +6,8 @@
 // (saves a separate elementwise kernel and one read of x).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <stdexcept>
 #include <string>
 
@@ -371,6 +373,64 @@ __global__ void __launch_bounds__(64 * kWaves) ln_split_kernel(const float* __re
   }
 }
 
+// Same output as ln_split_kernel, but every lane loads 4 UNIQUE columns per 1-KB row slice
+// (no duplicated loads across lane pairs: half the vector-memory requests) and the pair row is
+// assembled in LDS (3 KB per wave) before the full 1-KB wave stores.
+template <int NK, bool PRE>
+__global__ void __launch_bounds__(64 * kWaves) ln_split_lds_kernel(const float* __restrict__ x, const float* __restrict__ pre,
+                                                                   const float* __restrict__ g, const float* __restrict__ b,
+                                                                   uint16_t* __restrict__ y, int64_t rows, float eps) {
+  constexpr int cols = NK * 256;
+  __shared__ __attribute__((aligned(16))) uint16_t stage[kWaves][2 * cols];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + w;
+  if (row >= rows) return;  // no workgroup barrier below: each wave owns its LDS row
+  const float* xr = x + row * cols;
+  float v[NK][4];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = k * 256 + 4 * lane;
+    const float4 a = *reinterpret_cast<const float4*>(xr + c0);
+    v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+    if constexpr (PRE) {
+      const float4 pa = *reinterpret_cast<const float4*>(pre + c0);
+      v[k][0] += pa.x; v[k][1] += pa.y; v[k][2] += pa.z; v[k][3] += pa.w;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += v[k][i];
+  const float mean = wave_sum(s) * (1.f / cols);
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = v[k][i] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / cols) + eps);
+  uint16_t* st = stage[w];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = k * 256 + 4 * lane;
+    const float4 g4 = *reinterpret_cast<const float4*>(g + c0);
+    const float4 b4 = *reinterpret_cast<const float4*>(b + c0);
+    const float o0 = (v[k][0] - mean) * rstd * g4.x + b4.x, o1 = (v[k][1] - mean) * rstd * g4.y + b4.y;
+    const float o2 = (v[k][2] - mean) * rstd * g4.z + b4.z, o3 = (v[k][3] - mean) * rstd * g4.w + b4.w;
+    const uint32_t h0 = bfpack(o0, o1), h1 = bfpack(o2, o3);
+    uint16_t* e = st + (c0 >> 5) * 64 + (c0 & 31);  // k32-interleaved: hi at +0, lo at +32
+    *reinterpret_cast<uint2*>(e) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(e + 32) = make_uint2(bfpack_lo(o0, o1, h0), bfpack_lo(o2, o3, h1));
+  }
+  uint16_t* yr = y + row * (2 * cols);
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+    *reinterpret_cast<uint4*>(yr + k * 512 + lane * 8) = *reinterpret_cast<const uint4*>(st + k * 512 + lane * 8);
+}
+
 template <bool STATS, bool SPLIT>
 void launch_f32(const float* x, const float* pre, const float* g, const float* b, void* y, float2* st, int64_t rows,
                 int cols, float eps, hipStream_t s) {
@@ -455,8 +515,17 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
       const dim3 grid(static_cast<uint32_t>((p.rows + kWaves - 1) / kWaves)), blk(64 * kWaves);
       auto* y = static_cast<uint16_t*>(p.y);
       hipStream_t s = static_cast<hipStream_t>(stream);
-      if (p.pre) hipLaunchKernelGGL((ln_split_kernel<3, true>), grid, blk, 0, s, x, p.pre, g, b, y, p.rows, p.eps);
-      else hipLaunchKernelGGL((ln_split_kernel<3, false>), grid, blk, 0, s, x, nullptr, g, b, y, p.rows, p.eps);
+      static const bool dup = [] {  // MI_DFT_LN_SPLIT=dup: the duplicated-load kernel (A/B only)
+        const char* e = std::getenv("MI_DFT_LN_SPLIT");
+        return e && std::string(e) == "dup";
+      }();
+      if (dup) {
+        if (p.pre) hipLaunchKernelGGL((ln_split_kernel<3, true>), grid, blk, 0, s, x, p.pre, g, b, y, p.rows, p.eps);
+        else hipLaunchKernelGGL((ln_split_kernel<3, false>), grid, blk, 0, s, x, nullptr, g, b, y, p.rows, p.eps);
+      } else {
+        if (p.pre) hipLaunchKernelGGL((ln_split_lds_kernel<3, true>), grid, blk, 0, s, x, p.pre, g, b, y, p.rows, p.eps);
+        else hipLaunchKernelGGL((ln_split_lds_kernel<3, false>), grid, blk, 0, s, x, nullptr, g, b, y, p.rows, p.eps);
+      }
     } else if (p.split_out) {
       launch_f32<false, true>(x, p.pre, g, b, p.y, nullptr, p.rows, p.cols, p.eps, static_cast<hipStream_t>(stream));
     }
