@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
-  if constexpr (MODE == 0) {
+  if constexpr (MODE != 2) {  // token-major outputs (MODE 1 only gathers its B operand differently)
     if (!p.direct_epi) {
       // ---- LDS-staged epilogue (token-major outputs).  Writing straight from the MFMA layout
       // makes every store instruction touch 16 rows with 32-64 B each (partial lines; the
@@ -372,7 +372,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         if constexpr (RES) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16 features per lane
 #pragma unroll
           for (int it = 0; it < NIT; ++it) {
-            const int64_t o = static_cast<int64_t>(min(tbase + it * RPI + rsub, M - 1)) * N + fh + (OUT == 1 ? 4 : 8) * c;
+            int rt = min(tbase + it * RPI + rsub, M - 1);
+            if constexpr (MODE == 1) {
+              if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
+            }
+            const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
             if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
             else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
           }
@@ -581,7 +585,7 @@ static int gemm_variant() {
   return v;
 }
 
-// MI_DFT_GEMM_EPI=direct: the token-major epilogue stores straight from the MFMA layout (A/B only)
+// MI_DFT_GEMM_EPI=direct: the token-major (MODE 0 / 1) epilogue stores straight from the MFMA layout (A/B only)
 static int gemm_direct_epi() {
   static const int v = [] {
     const char* e = std::getenv("MI_DFT_GEMM_EPI");
