@@ -1,15 +1,15 @@
-// amd_dft-build-flags: -O1
+// amd_dft-build-flags: -O3 -mllvm -amdgpu-load-store-vectorizer=0
 // Fused AFNO spectral filter along H (FourCastNet AFNO2D, K5 in SURVEY §2.5).
 //
-// Built at -O1: at -O2/-O3 (hipcc, ROCm 7.2) both kernels of this file return wrong values
-// for a few workgroups of a launch, differently from launch to launch, but only when two or
-// more workgroups share a CU (bench grid B*KM*NB >> 256): e.g. rel-L2 2e-3 instead of 6e-6
-// for the bf16x3 kernel at B=2, KM=46, while every launch with <= 1 workgroup per CU (small
-// grids, or the LDS request padded to 1 per CU) is exact and deterministic.  The same source
-// at -O1 is exact at every grid (scripts/diag/afno_race_diag.py, profiles/afno_o1_fix_r2.txt).
-// The LDS images, index ranges and barriers were audited (no out-of-range access, every phase
-// barrier-separated; a standalone LDS-isolation test of co-resident workgroups is clean), so
-// the -O2 code generation is the suspect; the unit is kept at -O1 until that is isolated.
+// Built at -O3 WITHOUT the AMDGPU load/store vectorizer.  With it (hipcc, ROCm 7.2, -O2/-O3)
+// both kernels of this file return slightly wrong values (bf16x3: rel-L2 ~6e-3 instead of
+// 6.2e-6, i.e. the lo-plane products of some tiles lost), differently from launch to launch,
+// but only when two or more workgroups share a CU; every element is still written.  Forcing
+// every s_waitcnt to 0 or an s_nop before every instruction does not cure it; disabling the
+// vectorizer -- which merges the split-plane LDS writes into ds_write_b128 -- does, at every
+// grid, and is faster than the -O1 build used before (bf16 452 vs 477 us, bf16x3 842 vs
+// 881 us at [32, 90, 46, 768]; scripts/diag/afno_race_diag.py, afno_poison_diag.py,
+// profiles/afno_o1_fix_r2.txt).
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
