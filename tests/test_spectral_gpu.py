@@ -62,11 +62,15 @@ def test_afno2d_amd_fused_vs_reference(device):
     xd = x.to(device)
     out = afno2d_amd(xd, w1.to(device), b1.to(device), w2.to(device), b2.to(device), nb, 0.01, 1.0)
     assert S.afno_fused_available(xd, nb)
-    assert rel_l2(out, ref) < 1e-2
+    e32 = rel_l2(out, ref)
     # bf16 activations (model dtype)
     outb = afno2d_amd(xd.to(torch.bfloat16), w1.to(device), b1.to(device), w2.to(device), b2.to(device), nb, 0.01, 1.0)
     assert outb.dtype == torch.bfloat16
-    assert rel_l2(outb.float(), ref) < 2e-2
+    e16 = rel_l2(outb.float(), ref)
+    print(f"MEASURED afno2d_fused fp32 {e32:.3e} bf16 {e16:.3e}")
+    # MI355X: fp32 (bf16x3 GEMMs, fp32 spectra) 1.4e-6; bf16 activations 2.5e-3 (bf16 eps 3.9e-3)
+    assert e32 < 1e-5
+    assert e16 < 1e-2
 
 
 # every (H, block size) instance of the fused kernel beyond FourCastNet's (90, 96): the bf16 kernel
@@ -124,9 +128,13 @@ def test_afno2d_amd_fused_new_shapes(device, H, W, bs):
     assert S.afno_fused_available(xd, nb)
     p = [t.to(device) for t in (w1, b1, w2, b2)]
     out = afno2d_amd(xd, p[0], p[1], p[2], p[3], nb, 0.01, 1.0)
-    assert rel_l2(out, ref) < 1e-2
+    e32 = rel_l2(out, ref)
     outb = afno2d_amd(xd.to(torch.bfloat16), p[0], p[1], p[2], p[3], nb, 0.01, 1.0)
-    assert rel_l2(outb.float(), ref) < 2e-2
+    e16 = rel_l2(outb.float(), ref)
+    print(f"MEASURED afno2d_shape H={H} W={W} bs={bs} fp32 {e32:.3e} bf16 {e16:.3e}")
+    # MI355X: fp32 1.0e-6 .. 1.9e-6, bf16 2.4e-3 .. 2.7e-3 over the instances
+    assert e32 < 1e-5
+    assert e16 < 1e-2
 
 
 def test_layernorm_kernel(device):
@@ -169,8 +177,11 @@ def test_fourcastnet_amd_vs_reference(device, depth):
         out = m.set_backend("amd")(x)
         mb = m.to(torch.bfloat16)
         outb = mb(x.to(torch.bfloat16))
-    assert rel_l2(out, ref) < 1e-2
-    assert rel_l2(outb.float(), ref) < 5e-2
+    e32, e16 = rel_l2(out, ref), rel_l2(outb.float(), ref)
+    print(f"MEASURED fourcastnet depth={depth} fp32 {e32:.3e} bf16 {e16:.3e}")
+    # MI355X at depth 2: fp32 6.4e-6 (tests/test_fp32_path.py holds the 1e-4 headline bound), bf16 5.0e-3
+    assert e32 < 5e-5
+    assert e16 < 2e-2
 
 
 def test_patchify_kernels(device):
