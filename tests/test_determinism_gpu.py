@@ -1,7 +1,7 @@
 """Large-grid determinism + accuracy screen of every native kernel family (scripts/diag/determinism.py):
 workgroups co-resident on the CUs, each op run 3x, bit-identical outputs that match the CPU
-(ATen fp32) implementation.  Guards against cross-wave races and the -O2 miscompile that hit
-the AFNO spectral kernels (csrc/spectral/afno_spectral.hip header)."""
+(ATen fp32) implementation.  Guards against cross-wave races and the co-resident-workgroup corruption that the AMDGPU
+load/store vectorizer caused in the AFNO spectral kernels (csrc/spectral/afno_spectral.hip header)."""
 import os
 import runpy
 
