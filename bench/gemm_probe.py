@@ -1,5 +1,5 @@
 """Runs the hand GEMM (and hipBLASLt) on the FourCastNet MLP shapes a few times, for rocprofv3
-counter passes (scripts/pmc_cmd.sh).  Usage: python bench/gemm_probe.py [--iters 3] [--blas]"""
+counter passes (scripts/pmc_cmd.sh).  Usage: python bench/gemm_probe.py [--iters 3] [--blas] [--x3]"""
 import argparse
 import os
 import sys
@@ -14,6 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--rows", type=int, default=32 * 16200)
 ap.add_argument("--blas", action="store_true")
+ap.add_argument("--x3", action="store_true", help="only the bf16x3 (fp32-path) fc1 + GELU -> fc2 + residual pair")
 a = ap.parse_args()
 tdp.load_plugins()
 M, C, Hd = a.rows, 768, 3072
@@ -24,6 +25,16 @@ w2 = (torch.randn(C, Hd, device="cuda") * 0.02).to(torch.bfloat16)
 b1 = torch.randn(Hd, device="cuda") * 0.02
 b2 = torch.randn(C, device="cuda") * 0.02
 ops = torch.ops.amd_dft
+if a.x3:
+    xs = ops.split_bf16(x.float())
+    w1s, w2s = ops.split_bf16(w1.float()), ops.split_bf16(w2.float())
+    r32 = torch.randn(M, C, device="cuda")
+    for _ in range(a.iters):
+        hs = ops.linear3(xs, w1s, b1, 1, None, True)
+        ops.linear3(hs, w2s, None, 0, r32, False)
+    torch.cuda.synchronize()
+    print("ok")
+    sys.exit(0)
 for _ in range(a.iters):
     ops.linear(x, w1, b1, 1, None)
     ops.linear(x, w1, b1, 0, None)
