@@ -15,16 +15,25 @@ bf16 MFMA) is reported as ``bf16_samples_per_s``.  Every timed step runs the ful
 12 blocks) and the output all-gather; K steps are bracketed by barrier + synchronize, and the
 max over ranks is reported.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
+Scaling modes: weak (default; 32 samples per GPU, the driver's contract) or strong with
+``--global-batch G`` (G samples split over the ranks: SURVEY §5.8 sizes the output all-gather for
+global B=32 over 8 GPUs).  ``--gather-dtype bf16`` gathers a bf16 copy of an fp32 model's output
+(SURVEY §5.8 plan item 3).  On multi-GPU RCCL runs the JSON ``comm_env`` records what RCCL chose
+(channels, algorithm / protocol lines from its INIT/TUNING log, parsed by ``rccl_choices``).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16] [--global-batch G]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import re
 import sys
+import tempfile
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -42,6 +51,53 @@ METRIC = "rfft2 720×1440 µs + FourCastNet-FNO samples/sec at 1/2/4/8 MI355X"
 DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
 COMM_ENV = ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "RCCL_MSCCL_ENABLE",
             "NCCL_P2P_LEVEL", "MI_DFT_GATHER")
+
+
+def rccl_choices(text: str) -> dict:
+    """What RCCL chose, from its ``NCCL_DEBUG=INFO`` (INIT, TUNING) log: channel counts, the ring
+    order, and the algorithm / protocol lines of the tuner (kept verbatim, deduplicated)."""
+    out: dict = {}
+    m = re.search(r"(\d+) coll channels, (?:(\d+) collnet channels, )?(?:(\d+) nvls channels, )?(\d+) p2p channels", text)
+    if m:
+        out["coll_channels"] = int(m.group(1))
+        out["p2p_channels"] = int(m.group(4))
+    rings = re.findall(r"Channel (\d+)/(\d+) :((?: \d+)+)", text)
+    if rings:
+        out["ring_channels"] = int(rings[0][1])
+        out["ring0"] = rings[0][2].strip()
+    m = re.search(r"[RN]CCL version ([\d.]+\S*)", text)
+    if m:
+        out["version"] = m.group(1)
+    algo = []
+    for ln in text.splitlines():
+        if re.search(r"\b(algo|Algo|ALGO|proto|Proto|PROTO)\b", ln) and "NCCL_ALGO" not in ln:
+            t = re.sub(r"^.*?NCCL INFO\s*", "", ln).strip()
+            if t and t not in algo:
+                algo.append(t)
+    if algo:
+        out["tuning"] = algo[:8]
+    return out
+
+
+def _rccl_log_setup(world: int) -> str | None:
+    """Point RCCL's INFO log (INIT + TUNING only: nothing per collective) at a per-rank file."""
+    if world <= 1 or not os.environ.get("LOCAL_RANK") or os.environ.get("NCCL_DEBUG_FILE"):
+        return None
+    d = tempfile.mkdtemp(prefix="amd_dft_rccl_")
+    os.environ.setdefault("NCCL_DEBUG", "INFO")
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,TUNING")
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.%p.log")
+    return d
+
+
+def _rccl_log_read(d: str | None) -> dict:
+    if not d:
+        return {}
+    text = ""
+    for f in glob.glob(os.path.join(d, "rccl.*.log")):
+        with open(f, errors="replace") as fh:
+            text += fh.read()
+    return rccl_choices(text)
 
 
 def log(msg: str) -> None:
@@ -151,7 +207,7 @@ class _EngineFn:
         return self.eng.graph.run(x)[0]
 
 
-def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0):
+def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None):
     """Model -> (default) ONNX export with its com.amd.dft nodes -> serialized engine bytes ->
     deserialized engine -> hipGraph-captured DP runner: the timed step is the engine a user
     would load with ``dftexec --loadEngine`` (reference: export -> build -> serialize ->
@@ -174,7 +230,7 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0):
             f"{info['engine_build_load_s']}s")
     t0 = time.perf_counter()
     runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph,
-                                   gather_backend=a.gather)
+                                   gather_backend=a.gather, gather_dtype=gather_dtype)
     log(f"{dtype}: captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t0:.1f}s")
     return info, runner
 
@@ -185,6 +241,10 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="samples per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many samples in total, split over the ranks")
+    ap.add_argument("--gather-dtype", choices=["same", "bf16"], default="same",
+                    help="dtype of the gathered outputs (bf16: half the xGMI bytes of an fp32 model)")
     ap.add_argument("--depth", type=int, default=12)
     ap.add_argument("--dtype", choices=sorted(DTYPES), default="fp32", help="headline precision")
     ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of the other-precision extra (0: skip)")
@@ -199,6 +259,7 @@ def main(argv=None) -> int:
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
 
+    rccl_dir = _rccl_log_setup(int(os.environ.get("WORLD_SIZE", "1")))
     rank, world, local = init_distributed()
     if world != a.gpus and world > 1:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
@@ -208,25 +269,21 @@ def main(argv=None) -> int:
     if cuda:
         torch.cuda.set_device(dev)
     tdp.load_plugins()
-    gemm_table = None
+    gemm_table = None  # hipBLASLt solution tables: bench/experimental/gemm_tables.py (comparator only)
     from tensorrt_dft_plugins_amd.ops.spectral import mlp_on_hand_gemm
-
-    if cuda and not mlp_on_hand_gemm():
-        # hipBLASLt comparator path (MI_DFT_MLP=blas): fastest solutions for one GPU, no
-        # stream-K for DP (tensorrt_dft_plugins_amd/utils/gemm_tables.py)
-        from tensorrt_dft_plugins_amd.utils.gemm_tables import table_for_world, use_gemm_table
-
-        path = table_for_world(world)
-        if use_gemm_table(path):
-            gemm_table = os.path.basename(path)
-        log(f"GEMM solution table: {gemm_table}")
 
     if a.tiny:
         cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
     else:
         cfg = AFNOConfig(depth=a.depth)
     head_dt = DTYPES[a.dtype] if cuda else torch.float32
-    B = a.batch if not a.tiny else min(a.batch, 2)
+    if a.global_batch is not None:
+        if a.global_batch % world:
+            raise SystemExit(f"--global-batch {a.global_batch} is not divisible by {world} ranks")
+        B = a.global_batch // world
+    else:
+        B = a.batch if not a.tiny else min(a.batch, 2)
+    gdt = torch.bfloat16 if a.gather_dtype == "bf16" else None
 
     extra = {}
     if cuda and not a.no_fft and not a.tiny and rank == 0:
@@ -234,10 +291,11 @@ def main(argv=None) -> int:
         extra.update(time_fno_block_us())
         log(f"single-op probes: {extra}")
 
-    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234, rank)
+    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234, rank, gather_dtype=gdt)
     log(f"world={world} batch/GPU={B} dtype={head_dt}")
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
+    runner.close()
     del runner
     if cuda:
         torch.cuda.empty_cache()
@@ -247,12 +305,15 @@ def main(argv=None) -> int:
 
     if cuda and a.extra_steps > 0 and not a.tiny:
         other = "bf16" if a.dtype == "fp32" else "fp32"
-        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 4321, rank)
+        # same weight / input seeds as the headline: only the precision differs
+        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 1234, rank)
         e2 = run_steps(r2, a.extra_steps, 2, world, dev, cuda)
         extra[f"{other}_samples_per_s"] = round(world * B / (e2 / a.extra_steps), 3)
         extra[f"{other}_ms_per_step"] = round(e2 * 1000.0 / a.extra_steps, 3)
+        r2.close()
         del r2
 
+    rccl = _rccl_log_read(rccl_dir) if rank == 0 else {}
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -263,7 +324,7 @@ def main(argv=None) -> int:
             "warmup": a.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.global_batch is not None else "weak",
             "vs_baseline": None,
             "dtype": "bf16" if head_dt == torch.bfloat16 else "fp32",
             "data": "synthetic inputs, random-init weights",
@@ -284,7 +345,10 @@ def main(argv=None) -> int:
                 "gemm": "hipblaslt" if gemm_table or (cuda and not mlp_on_hand_gemm()) else "hand-mfma",
                 "gemm_precision": "bf16x3 split, fp32 accumulate" if head_dt == torch.float32 else "bf16, fp32 accumulate",
                 "gemm_table": gemm_table,
-                "comm_env": {k: os.environ[k] for k in COMM_ENV if k in os.environ},
+                "gather_dtype": ("bf16" if gdt is not None else ("bf16" if head_dt == torch.bfloat16 else "fp32"))
+                if world > 1 and gathered else None,
+                "comm_env": dict({k: os.environ[k] for k in COMM_ENV if k in os.environ},
+                                 **({"rccl": rccl} if rccl else {})),
             },
             "model_tflops_per_s": round(tflops, 2),
         }

@@ -1,4 +1,4 @@
-"""hipBLASLt solution tables for the FourCastNet MLP GEMMs (PyTorch TunableOp, lookup only).
+"""[comparator only; moved out of the package in round 3] hipBLASLt solution tables for the FourCastNet MLP GEMMs (PyTorch TunableOp, lookup only).
 
 Measured on MI355X (`scripts/gemm_candidates.py`, `scripts/gemm_forced.py`,
 `scripts/interference_probe.py` + `scripts/spin_hog.py`; profiles/gemm_tables_r1o.txt):
@@ -23,9 +23,9 @@ from typing import Optional
 
 import torch
 
-from .trace import get_logger
+from tensorrt_dft_plugins_amd.utils.trace import get_logger
 
-TABLE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
+TABLE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning")
 _loaded: Optional[str] = None
 
 

@@ -34,11 +34,5 @@ struct GemmLaunch {
 };
 bool gemm_supported(int64_t M, int64_t N, int64_t K);
 void launch_gemm(const GemmLaunch& p, void* stream);
-// four-wave 128x128-per-wave variant (gemm4w.hip) for plain token-major operands
-bool gemm4w_applicable(const GemmLaunch& p);
-void launch_gemm4w(const GemmLaunch& p, void* stream);
-// two-workgroups-per-CU 128x256 variant (gemm2wg.hip) for plain token-major operands
-bool gemm2wg_applicable(const GemmLaunch& p);
-void launch_gemm2wg(const GemmLaunch& p, void* stream);
 
 }  // namespace amd_dft

@@ -38,6 +38,7 @@
 // next GEMM's operand.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -522,11 +523,14 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
 template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
 void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT>;
-  static bool attr_done = false;
-  if (!attr_done) {
+  // the dynamic-LDS limit is a per-device function attribute: set it once per (instance, device)
+  static std::atomic<uint64_t> attr_done{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("amd_dft: gemm: bad device");
+  if (!(attr_done.load(std::memory_order_acquire) & (uint64_t(1) << dev))) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: gemm attr: ") + hipGetErrorString(e));
-    attr_done = true;
+    attr_done.fetch_or(uint64_t(1) << dev, std::memory_order_acq_rel);
   }
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
 }
@@ -570,21 +574,6 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K) {
 // logical K of a split (bf16x3) GEMM: 32-deep K-tiles, at least 2 (the pipeline prologue)
 static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
 
-// MI_DFT_GEMM_KERNEL=4w selects the four-wave 128x128-per-wave kernel (gemm4w.hip) where it applies;
-// default: the 8-wave ping-pong kernel below, measured faster on the FourCastNet shapes
-// (fc2 2127 vs 2466 us, fc1+GELU 3231 vs 3997 us, bf16x3 fc2 6360 vs 7639 us;
-// profiles/gemm_4w_vs_8w_r2.txt: hipcc keeps part of the 4-wave kernel's fragments in the
-// accumulator file and shuffles them back every few MFMAs)
-static int gemm_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("MI_DFT_GEMM_KERNEL");  // "4w" / "2wg" / "8w"
-    if (e && std::string(e) == "4w") return 4;
-    if (e && std::string(e) == "2wg") return 2;
-    return 8;
-  }();
-  return v;
-}
-
 // MI_DFT_GEMM_EPI=direct: the token-major (MODE 0 / 1) epilogue stores straight from the MFMA layout (A/B only)
 static int gemm_direct_epi() {
   static const int v = [] {
@@ -596,21 +585,6 @@ static int gemm_direct_epi() {
 
 void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
-  if (gemm_variant() == 4 && gemm4w_applicable(p_)) {
-    launch_gemm4w(p_, stream);
-    return;
-  }
-  if (gemm_variant() == 2 && gemm2wg_applicable(p_) && !(p_.split && p_.ln_stats) &&
-      (p_.out != 0) == (p_.split != 0) && !(p_.ln_stats && !p_.ln_c1)) {
-    static const int stagger = [] {
-      const char* e = std::getenv("MI_DFT_GEMM2WG_STAGGER");  // experiment: cycles
-      return e ? std::atoi(e) : 0;
-    }();
-    GemmLaunch q = p_;
-    q.stagger = stagger;
-    launch_gemm2wg(q, stream);
-    return;
-  }
   if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
   if (p_.out < 0 || p_.out > 2 || (p_.out != 0) != (p_.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");

@@ -15,6 +15,7 @@
 // The reference has no multi-GPU path at all ("assuming single GPU",
 // /root/reference/src/dft_plugins/dft_plugins.cpp:341).
 #include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
@@ -35,10 +36,12 @@ void hip_ok(hipError_t e, const char* what) {
 
 at::Tensor ipc_alloc(int64_t bytes, int64_t device) {
   TORCH_CHECK(bytes > 0, "amd_dft._ipc_alloc: bytes must be positive");
-  hip_ok(hipSetDevice(static_cast<int>(device)), "_ipc_alloc(hipSetDevice)");
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));  // restores the caller's device
   void* p = nullptr;
   hip_ok(hipMalloc(&p, static_cast<size_t>(bytes)), "_ipc_alloc(hipMalloc)");
   auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+  // freed only when the last tensor reference goes: IpcAllGather.close() drops it after a
+  // barrier, i.e. after every peer has closed its mapping and finished pushing into it
   return at::from_blob(p, {bytes}, [](void* q) { (void)hipFree(q); }, opts);
 }
 
@@ -59,7 +62,7 @@ hipIpcMemHandle_t as_mem_handle(const at::Tensor& h) {
 }
 
 int64_t ipc_open_mem(const at::Tensor& handle, int64_t device) {
-  hip_ok(hipSetDevice(static_cast<int>(device)), "_ipc_open_mem(hipSetDevice)");
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
   void* p = nullptr;
   hip_ok(hipIpcOpenMemHandle(&p, as_mem_handle(handle), hipIpcMemLazyEnablePeerAccess), "_ipc_open_mem");
   return reinterpret_cast<int64_t>(p);
@@ -68,7 +71,7 @@ int64_t ipc_open_mem(const at::Tensor& handle, int64_t device) {
 void ipc_close_mem(int64_t ptr) { hip_ok(hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)), "_ipc_close_mem"); }
 
 int64_t ipc_event_create(int64_t device) {
-  hip_ok(hipSetDevice(static_cast<int>(device)), "_ipc_event_create(hipSetDevice)");
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
   hipEvent_t ev;
   hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventInterprocess), "_ipc_event_create");
   return reinterpret_cast<int64_t>(ev);
@@ -85,7 +88,7 @@ at::Tensor ipc_event_handle(int64_t ev) {
 int64_t ipc_event_open(const at::Tensor& handle, int64_t device) {
   TORCH_CHECK(handle.numel() == HIP_IPC_HANDLE_SIZE && handle.scalar_type() == at::kByte,
               "amd_dft._ipc_event_open: IPC handles are uint8[64]");
-  hip_ok(hipSetDevice(static_cast<int>(device)), "_ipc_event_open(hipSetDevice)");
+  c10::hip::HIPGuard guard(static_cast<c10::DeviceIndex>(device));
   hipIpcEventHandle_t h;
   std::memcpy(&h, handle.contiguous().cpu().data_ptr(), HIP_IPC_HANDLE_SIZE);
   hipEvent_t ev;

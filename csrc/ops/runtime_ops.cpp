@@ -35,6 +35,11 @@ std::tuple<std::vector<std::string>, std::vector<int64_t>> fallback_counts() {
   return {names, counts};
 }
 
+// fallback_note(op, why): the Python-level generic paths (models/afno.py afno2d_amd's baddbmm
+// spectral MLP, ops/spectral.py's F.linear / hipBLASLt MLP) report into the same registry, so
+// fallback_counts() and MI_DFT_STRICT cover them too
+void fallback_note_op(const std::string& op, const std::string& why) { fallback_note(op.c_str(), why.c_str()); }
+
 void fallback_reset() {
   auto& r = fallback_registry();
   std::lock_guard<std::mutex> g(r.mu);
@@ -51,4 +56,5 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("wrap_host_ptr(int ptr, int[] shape, ScalarType dtype) -> Tensor", &amd_dft::wrap_host_ptr);
   m.def("fallback_counts() -> (str[], int[])", &amd_dft::fallback_counts);
   m.def("fallback_reset() -> ()", &amd_dft::fallback_reset);
+  m.def("fallback_note(str op, str why) -> ()", &amd_dft::fallback_note_op);
 }

@@ -133,10 +133,12 @@ def afno2d_amd(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_threshold
         # C2R along W from km stored modes, + bias (filter input) fused
         return S.c2r_w_add(yw, x, W, 1.0 / math.sqrt(H * W), residual)
     # generic path: pruned 2-D R2C/C2R + batched real-block GEMMs
+    S.note_fallback("afno_spectral", "no fused AFNO kernel for this (H, block size) / mode window: torch.baddbmm", x)
     xf = D._ops().r2c(x, [1, 2], scale_f, [H, 0, km, 0], torch.float32)[:, r0:r1]
     bs = C // num_blocks
     M = xf.shape[0] * xf.shape[1] * xf.shape[2]
     z = xf.reshape(M, num_blocks, bs, 2).permute(1, 0, 3, 2).reshape(num_blocks, M, 2 * bs)  # [nb, M, (re|im)*bs]
+    w1, b1, w2, b2 = w1.float(), b1.float(), w2.float(), b2.float()  # fp32 spectrum math for any model dtype
     W1 = torch.cat([torch.cat([w1[0], w1[1]], dim=2), torch.cat([-w1[1], w1[0]], dim=2)], dim=1)  # [nb, 2bs, 2bs]
     W2 = torch.cat([torch.cat([w2[0], w2[1]], dim=2), torch.cat([-w2[1], w2[0]], dim=2)], dim=1)
     h = torch.relu(torch.baddbmm(torch.cat([b1[0], b1[1]], 1).unsqueeze(1), z, W1))

@@ -463,7 +463,7 @@ AMD_DOMAIN = "com.amd.dft"
 
 
 _AMD_NODE_DENY = frozenset({"wrap_device_ptr", "wrap_host_ptr", "plan_cache_clear", "plan_cache_size", "plan_cache_pinned",
-                            "fallback_counts", "fallback_reset", "plugin_registry"})
+                            "fallback_counts", "fallback_reset", "fallback_note", "plugin_registry"})
 
 
 def _amd_node(opname: str):

@@ -33,7 +33,7 @@ from . import dft as D
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
            "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
            "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
-           "fallback_counts", "fallback_reset", "unsplit_bf16"]
+           "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16"]
 
 
 def _ops():
@@ -68,6 +68,14 @@ def fallback_counts() -> dict:
 
 def fallback_reset() -> None:
     _ops().fallback_reset()
+
+
+def note_fallback(op: str, why: str, x: torch.Tensor) -> None:
+    """Count a GPU call of ``op`` that left the hand kernels (Python-level generic paths), in the
+    same registry as the C++ ops: ``fallback_counts()`` lists it and ``MI_DFT_STRICT=1`` raises.
+    CPU tensors (the reference / plumbing path) and tracing (ONNX export) are not counted."""
+    if x.is_cuda and not torch.jit.is_tracing():
+        _ops().fallback_note(op, why)
 
 
 def split_bf16(t: torch.Tensor, rows: bool = True) -> torch.Tensor:
@@ -153,6 +161,7 @@ def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
     max |fused - gelu_tanh| = 4.8e-7, |fused - gelu_erf| = 4.7e-4).  FourCastNet's nn.GELU is
     the erf form, which the default hand MFMA GEMM computes (erf via A&S 7.1.26, |err| < 2e-7).
     """
+    note_fallback("mlp_fc1_gelu", "hipBLASLt / ATen fc1+GELU instead of the hand MFMA GEMM", y2)
     if y2.is_cuda and fc.bias is not None and hasattr(torch, "_addmm_activation"):
         return torch._addmm_activation(fc.bias, y2, fc.weight.t(), use_gelu=True)
     return F.gelu(F.linear(y2, fc.weight, fc.bias))
@@ -190,9 +199,20 @@ def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
         return False
     B, H, W, C = (int(d) for d in x.shape)
     r0, r1, km = kept_window(H, W, c.hard_thresholding_fraction)
-    if x.dtype == torch.float32 and not (C % 256 == 0 and (4 * C) % 256 == 0):
-        return False  # the bf16x3 MLP GEMMs tile 256 features
+    if not _mlp_gemm_ok(blk.mlp, x.dtype == torch.float32):
+        return False
     return r0 == 0 and r1 == H and afno_fused_available(x, c.num_blocks)
+
+
+def _mlp_gemm_ok(m, split: bool) -> bool:
+    """Both MLP GEMMs fit the hand kernel (csrc/nn/gemm.hip): output features in 256-tiles and
+    the reduction depth in 64-tiles (bf16) or 32-tiles of at least 64 (bf16x3 split)."""
+    def k_ok(k: int) -> bool:
+        return k % 32 == 0 and k >= 64 if split else k % 64 == 0
+
+    f1, f2 = m.fc1, m.fc2
+    return (f1.out_features % 256 == 0 and f2.out_features % 256 == 0 and k_ok(f1.in_features)
+            and k_ok(f2.in_features))
 
 
 def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
@@ -334,6 +354,7 @@ def afno_block_mlp(blk, yn: torch.Tensor) -> torch.Tensor:
     m = blk.mlp
     B, H, W, C = yn.shape
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
+    note_fallback("mlp_fc2", "ATen / hipBLASLt fc2 (generic AFNO shape)", yn)
     y = F.linear(hid, m.fc2.weight, m.fc2.bias)
     return y.reshape(B, H, W, C)
 

@@ -72,16 +72,28 @@ class DataParallelInference:
     ``gather_backend``: ``"rccl"`` (``all_gather_into_tensor``; Gloo on CPU) or ``"ipc"`` (direct
     pushes into every peer's buffer over xGMI, :mod:`.ipc_gather`); default from
     ``MI_DFT_GATHER``, else rccl.
+    ``gather_dtype``: e.g. ``torch.bfloat16`` gathers a reduced-precision copy of the output
+    (SURVEY §5.8 plan item 3: half the xGMI bytes of an fp32 model's output); the cast is part
+    of the captured graph, and the gathered buffers have that dtype.  Default: the output dtype.
     """
 
     def __init__(self, module, example: torch.Tensor, *, gather: bool = True,
-                 use_graph: bool = True, warmup: int = 2, gather_backend: Optional[str] = None):
+                 use_graph: bool = True, warmup: int = 2, gather_backend: Optional[str] = None,
+                 gather_dtype: Optional[torch.dtype] = None):
         self.rank, self.world = world_info()
         self.gather = gather and self.world > 1
         self.gather_backend = (gather_backend or os.environ.get("MI_DFT_GATHER", "rccl")).lower()
         if self.gather_backend not in ("rccl", "ipc"):
             raise ValueError(f"gather_backend must be 'rccl' or 'ipc', got {self.gather_backend!r}")
-        self.cap = CapturedModule(module, [example], warmup=warmup, n_graphs=2 if self.gather else 1,
+        self.gather_dtype = gather_dtype if self.gather else None
+        fn = module
+        if self.gather_dtype is not None:
+            gd = self.gather_dtype
+
+            def fn(*xs):  # noqa: F811  (cast captured with the forward)
+                o = module(*xs)
+                return o.to(gd) if o.dtype != gd else o
+        self.cap = CapturedModule(fn, [example], warmup=warmup, n_graphs=2 if self.gather else 1,
                                   use_graph=use_graph)
         self.device = example.device
         self.cuda = self.device.type == "cuda"
@@ -143,10 +155,30 @@ class DataParallelInference:
         return self.full[i]
 
     def drain(self) -> None:
-        """Make the current stream wait for all outstanding gathers."""
+        """Make the current stream wait for all outstanding gathers (CPU: until they are done)."""
         for i, w in enumerate(self.works):
             if w is not None:
                 w.wait()
                 self.works[i] = None
         if self.cuda:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        elif self.ipc is not None:
+            self.ipc.synchronize()
+
+    def close(self) -> None:
+        """Collective teardown: finish every gather, then (IPC) barrier and release the peer
+        handles before the gather buffers are freed (no peer may still push into them)."""
+        self.drain()
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+        if self.ipc is not None:
+            self.ipc.close()
+            self.ipc = None
+        self.full = [None, None]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

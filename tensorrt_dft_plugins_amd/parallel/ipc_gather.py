@@ -7,25 +7,37 @@ concurrent copies, one per link, each moving one shard (ring: ~7 x shard / link 
 mesh: ~1 x shard / link bandwidth, derived in SURVEY §5.8).
 
 Protocol per step (buffer slot ``i`` of ``nbuf``, all on the caller's current stream):
-  1. push: one kernel (csrc/parallel/ipc_push.hip) stores the local shard into slot ``i`` of every
+  1. release: record this rank's inter-process event ``rel[i]``.  Everything this rank enqueued
+     before the call -- in particular every consumer of the slot's previous contents (step
+     ``k - nbuf``) -- is ordered before it;
+  2. host handshake #1: a barrier on a Gloo group (every rank has enqueued its release record);
+  3. the stream waits on every peer's ``rel[i]``: a push never overwrites a peer's slot while
+     that peer's GPU may still read the old contents (write-after-read across processes);
+  4. push: one kernel (csrc/parallel/ipc_push.hip) stores the local shard into slot ``i`` of every
      rank's buffer at once (peer pointers from ``hipIpcOpenMemHandle``; one xGMI link per peer),
      at byte offset ``rank * shard_bytes``;
-  2. record this rank's inter-process event ``i`` after the pushes;
-  3. host handshake: a barrier on a Gloo group -- afterwards every producer has ENQUEUED its
-     pushes and its event record for this step (the host never waits for the GPU);
-  4. the stream waits on every peer's event ``i``: stream-ordered completion of all pushes.
-A slot is rewritten ``nbuf`` steps later, so the gathered buffer of a step stays valid while
-the next ``nbuf - 1`` steps are enqueued (the DP runner's double-buffer contract).
+  5. record this rank's inter-process event ``done[i]`` after the pushes;
+  6. host handshake #2: every producer has ENQUEUED its pushes and its ``done[i]`` record;
+  7. the stream waits on every peer's ``done[i]``: stream-ordered completion of all pushes.
+The host never waits for the GPU.  Contract: the gathered buffer of step ``k`` stays valid until
+the gather of step ``k + nbuf`` is called, and every read of it must be enqueued (in stream order
+on the calling stream, or joined into it) before that call.
 
 Transports: ``HipIpcTransport`` (GPU: hipMalloc'd buffers, IPC memory/event handles) and
-``ShmTransport`` (CPU: ``/dev/shm``-backed storages, synchronous copies) -- the latter runs the
-same slot / offset / handshake logic in multi-process Gloo tests without a GPU.
+``ShmTransport`` (CPU: ``/dev/shm``-backed storages).  The CPU transport emulates a GPU stream
+with one worker thread per rank and inter-process events with shared ``(enqueued, completed)``
+counters, so the multi-process Gloo tests exercise the same ordering the GPU relies on -- a
+deliberately slow consumer on one rank shows whether a peer's push waits for it
+(tests/test_dp.py::test_ipc_gather_slow_consumer_*).
 """
 from __future__ import annotations
 
 import os
+import queue
+import threading
+import time
 import uuid
-from typing import List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -43,9 +55,11 @@ class HipIpcTransport:
         self.ops = torch.ops.amd_dft
         self._opened: List[int] = []
         self._events: List[int] = []
+        self._bufs: List[torch.Tensor] = []
 
     def alloc(self, nbytes: int):
         buf = self.ops._ipc_alloc(nbytes, self.dev)
+        self._bufs.append(buf)
         return buf, self.ops._ipc_mem_handle(buf)
 
     def open(self, handle, local_buf, is_self: bool) -> int:
@@ -72,26 +86,89 @@ class HipIpcTransport:
     def wait(self, ev) -> None:
         self.ops._ipc_stream_wait(ev, self.dev)
 
+    def enqueue(self, fn: Callable[[], None]) -> None:
+        fn()  # device work is already stream-ordered: run the enqueueing code now
+
+    def synchronize(self) -> None:
+        torch.cuda.current_stream(self.device).synchronize()
+
     def close(self) -> None:
+        """Caller guarantees (barrier) that no peer still pushes into, or reads, these buffers."""
+        torch.cuda.synchronize(self.device)
         for p in self._opened:
             self.ops._ipc_close_mem(p)
         for ev in self._events:
             self.ops._ipc_event_destroy(ev)
         self._opened, self._events = [], []
+        self._bufs = []  # the last references: hipFree through the from_blob deleter
+
+
+class _HostStream:
+    """One worker thread executing enqueued closures in order: the CPU model of a GPU stream."""
+
+    def __init__(self):
+        self.q: "queue.Queue[Optional[Callable[[], None]]]" = queue.Queue()
+        self.error: Optional[BaseException] = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            fn = self.q.get()
+            if fn is None:
+                return
+            try:
+                if self.error is None:
+                    fn()
+            except BaseException as e:  # surfaced by synchronize()
+                self.error = e
+
+    def submit(self, fn: Callable[[], None]) -> None:
+        self.q.put(fn)
+
+    def synchronize(self, timeout: float = 120.0) -> None:
+        ev = threading.Event()
+        self.q.put(ev.set)
+        if not ev.wait(timeout):
+            raise TimeoutError("amd_dft ShmTransport: stream did not drain")
+        if self.error is not None:
+            raise RuntimeError("amd_dft ShmTransport: stream op failed") from self.error
+
+    def stop(self):
+        self.q.put(None)
+        self.t.join(timeout=10)
+
+
+class _ShmEvent:
+    """Inter-process event: shared int64 ``[enqueued, completed]`` record counters."""
+
+    def __init__(self, path: str, create: bool):
+        st = torch.UntypedStorage.from_file(path, shared=True, nbytes=16)
+        self.c = torch.empty(0, dtype=torch.int64).set_(st, 0, (2,))
+        if create:
+            self.c.zero_()
+        self.path = path
 
 
 class ShmTransport:
-    """CPU stand-in: each buffer is a ``/dev/shm`` file mapped by every rank; copies are
-    synchronous, events are no-ops (the host handshake already orders them)."""
+    """CPU stand-in: each buffer is a ``/dev/shm`` file mapped by every rank; pushes, event
+    records and event waits run asynchronously on a per-rank worker thread (a "stream"), so the
+    host runs ahead of its stream exactly as it runs ahead of a GPU."""
 
-    def __init__(self, device: torch.device = torch.device("cpu")):
+    def __init__(self, device: torch.device = torch.device("cpu"), spin_timeout_s: float = 120.0):
         self.device = device
         self._files: List[str] = []
+        self.stream = _HostStream()
+        self.spin_timeout_s = spin_timeout_s
+
+    def _path(self) -> str:
+        p = f"/dev/shm/amd_dft_ipc_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+        self._files.append(p)
+        return p
 
     def alloc(self, nbytes: int):
-        path = f"/dev/shm/amd_dft_ipc_{os.getpid()}_{uuid.uuid4().hex[:12]}"
+        path = self._path()
         st = torch.UntypedStorage.from_file(path, shared=True, nbytes=nbytes)
-        self._files.append(path)
         return torch.empty(0, dtype=torch.uint8).set_(st), (path, nbytes)
 
     def open(self, handle, local_buf, is_self: bool):
@@ -101,23 +178,52 @@ class ShmTransport:
         return torch.empty(0, dtype=torch.uint8).set_(torch.UntypedStorage.from_file(path, shared=True, nbytes=nbytes))
 
     def new_event(self):
-        return None, None
+        path = self._path()
+        return _ShmEvent(path, create=True), path
 
     def open_event(self, handle, local_ev, is_self: bool):
-        return None
+        return local_ev if is_self else _ShmEvent(handle, create=False)
 
     def push(self, src: torch.Tensor, dsts, offset: int) -> None:
-        b = src.contiguous().view(torch.uint8).reshape(-1)
-        for d in dsts:
-            d[offset:offset + b.numel()].copy_(b)
+        b = src.contiguous().view(torch.uint8).reshape(-1).clone()  # snapshot at enqueue time
 
-    def record(self, ev) -> None:
-        pass
+        def run():
+            for d in dsts:
+                d[offset:offset + b.numel()].copy_(b)
 
-    def wait(self, ev) -> None:
-        pass
+        self.stream.submit(run)
+
+    def record(self, ev: _ShmEvent) -> None:
+        ev.c[0] += 1
+        target = int(ev.c[0])
+
+        def run():
+            ev.c[1] = target
+
+        self.stream.submit(run)
+
+    def wait(self, ev: _ShmEvent) -> None:
+        target = int(ev.c[0])  # the peer's latest record enqueued so far (after the handshake)
+        deadline_s = self.spin_timeout_s
+
+        def run():
+            t0 = time.monotonic()
+            while int(ev.c[1]) < target:
+                if time.monotonic() - t0 > deadline_s:
+                    raise TimeoutError(f"amd_dft ShmTransport: event wait {int(ev.c[1])} < {target}")
+                time.sleep(0.0005)
+
+        self.stream.submit(run)
+
+    def enqueue(self, fn: Callable[[], None]) -> None:
+        self.stream.submit(fn)
+
+    def synchronize(self) -> None:
+        self.stream.synchronize()
 
     def close(self) -> None:
+        self.stream.synchronize()
+        self.stream.stop()
         for f in self._files:
             try:
                 os.unlink(f)
@@ -131,15 +237,17 @@ class IpcAllGather:
 
     ``gather(local, i)`` returns slot ``i``'s ``[world * shard_shape[0], ...]`` tensor, complete
     in stream order.  Collective: every rank constructs it with the same arguments.
+    ``release=False`` drops steps 1-3 of the protocol (tests only: shows the write-after-read race).
     """
 
     def __init__(self, shard_shape: Sequence[int], dtype: torch.dtype, device: torch.device, *, nbuf: int = 2,
-                 transport=None, group=None):
+                 transport=None, group=None, release: bool = True):
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.shard_shape = list(shard_shape)
         self.dtype = dtype
         self.nbuf = nbuf
         self.device = device
+        self.release = release
         self.transport = transport or (HipIpcTransport(device) if device.type == "cuda" else ShmTransport())
         # host-side handshake group: Gloo never waits for the GPU
         self.host_group = group if group is not None else (
@@ -149,31 +257,57 @@ class IpcAllGather:
         full_shape = [self.world * self.shard_shape[0]] + self.shard_shape[1:]
         self.full: List[torch.Tensor] = []
         self.peers: List[List[object]] = []
-        self.events: List[object] = []
+        self.events: List[object] = []      # done[i]: this rank's pushes into slot i are enqueued before it
         self.peer_events: List[List[object]] = []
+        self.rel: List[object] = []         # rel[i]: this rank no longer reads its slot i
+        self.peer_rel: List[List[object]] = []
         for _ in range(nbuf):
             buf, handle = self.transport.alloc(self.world * self.shard_bytes)
             ev, ev_handle = self.transport.new_event()
+            rel, rel_handle = self.transport.new_event()
             handles: List[Optional[object]] = [None] * self.world
-            dist.all_gather_object(handles, (handle, ev_handle), group=self.host_group)
+            dist.all_gather_object(handles, (handle, ev_handle, rel_handle), group=self.host_group)
             self.full.append(buf.view(dtype).view(full_shape))
             self.peers.append([self.transport.open(h[0], buf, p == self.rank) for p, h in enumerate(handles)])
             self.events.append(ev)
             self.peer_events.append([self.transport.open_event(h[1], ev, p == self.rank) for p, h in enumerate(handles)])
+            self.rel.append(rel)
+            self.peer_rel.append([self.transport.open_event(h[2], rel, p == self.rank) for p, h in enumerate(handles)])
         dist.barrier(group=self.host_group)
+        self._closed = False
 
     def gather(self, local: torch.Tensor, i: int) -> torch.Tensor:
         if list(local.shape) != self.shard_shape or local.dtype != self.dtype:
             raise ValueError(f"shard {list(local.shape)} {local.dtype} != {self.shard_shape} {self.dtype}")
         i %= self.nbuf
-        self.transport.push(local, self.peers[i], self.rank * self.shard_bytes)
-        self.transport.record(self.events[i])
+        t = self.transport
+        if self.release:
+            t.record(self.rel[i])
+            dist.barrier(group=self.host_group)
+            for p in range(self.world):
+                if p != self.rank:
+                    t.wait(self.peer_rel[i][p])
+        t.push(local, self.peers[i], self.rank * self.shard_bytes)
+        t.record(self.events[i])
         dist.barrier(group=self.host_group)
         for p in range(self.world):
             if p != self.rank:
-                self.transport.wait(self.peer_events[i][p])
+                t.wait(self.peer_events[i][p])
         return self.full[i]
 
+    def enqueue(self, fn: Callable[[], None]) -> None:
+        """Run ``fn`` in this rank's stream order (CPU transport: on its worker; GPU: now)."""
+        self.transport.enqueue(fn)
+
+    def synchronize(self) -> None:
+        self.transport.synchronize()
+
     def close(self) -> None:
+        """Collective: drain this rank's stream, wait until every rank has drained (no push into
+        or read of any buffer is still in flight anywhere), then release handles and buffers."""
+        if self._closed:
+            return
+        self.transport.synchronize()
         dist.barrier(group=self.host_group)
         self.transport.close()
+        self._closed = True

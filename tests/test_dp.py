@@ -96,6 +96,77 @@ def test_dp_allgather_gloo_world3(backend):
     _run_dp("cpu", backend, world=3)
 
 
+def _slow_consumer_worker(rank, world, port, q, release):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        sys.path.insert(0, ROOT)
+        import time
+
+        import torch.distributed as dist
+
+        from tensorrt_dft_plugins_amd.parallel import IpcAllGather
+
+        dist.init_process_group("gloo")
+        g = IpcAllGather([4, 8], torch.float32, torch.device("cpu"), nbuf=2, release=release)
+        seen = []
+        slow = rank == world - 1
+
+        def consume(full):  # runs in this rank's stream order
+            if slow:
+                time.sleep(0.15)  # a lagging GPU: still reading its slot when peers run ahead
+            seen.append(full.clone())
+
+        prev = None
+        for k in range(6):
+            full = g.gather(torch.full((4, 8), float(100 * k + rank)), k)
+            if prev is not None:  # pipelined consumer: step k-1's result is read after step k is enqueued
+                g.enqueue(lambda t=prev: consume(t))
+            prev = full
+        g.enqueue(lambda t=prev: consume(t))
+        g.synchronize()
+        bad = [k for k, t in enumerate(seen)
+               if not torch.equal(t.view(world, 4, 8)[:, 0, 0], torch.arange(world, dtype=torch.float32) + 100 * k)]
+        g.close()
+        q.put((rank, bad))
+        dist.destroy_process_group()
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+
+
+def _run_slow_consumer(world, release):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_slow_consumer_worker, args=(r, world, port, q, release)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert isinstance(v, list), f"rank {r} failed: {v}"
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_gather_slow_consumer_slot_reuse(world):
+    """Write-after-read across processes: every rank reads step k's gathered slot after it has
+    enqueued step k + 1 (the overlap the double buffer is for); the last rank's stream lags (each
+    read sleeps) while the others race ahead and reuse the slot at step k + 2.  The release events
+    (protocol steps 1-3, parallel/ipc_gather.py) make every push wait until the slow rank has
+    read the slot's previous contents: every rank sees every step intact."""
+    res = _run_slow_consumer(world, release=True)
+    assert all(v == [] for v in res.values()), res
+
+
+def test_ipc_gather_slow_consumer_detects_race_without_release():
+    """The same run with the release wait disabled corrupts the slow rank's reads: the test above
+    can see the race it guards against."""
+    res = _run_slow_consumer(2, release=False)
+    assert res[1], "expected the lagging rank to read overwritten slots"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("backend", ["rccl", "ipc"])
 def test_dp_allgather_gloo_world2_on_one_gpu(backend):
@@ -105,11 +176,13 @@ def test_dp_allgather_gloo_world2_on_one_gpu(backend):
     _run_dp("cuda", backend)
 
 
-def test_bench_harness_torchrun_gloo():
+@pytest.mark.parametrize("extra,scaling,gather_dtype", [([], "weak", None),
+                                                        (["--global-batch", "4", "--gather-dtype", "bf16"], "strong", "bf16")])
+def test_bench_harness_torchrun_gloo(extra, scaling, gather_dtype):
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--tiny", "--gpus", "2",
-           "--steps", "2", "--warmup", "1"]
+           "--steps", "2", "--warmup", "1"] + extra
     env = dict(os.environ)
     env.pop("CUDA_VISIBLE_DEVICES", None)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
@@ -119,8 +192,36 @@ def test_bench_harness_torchrun_gloo():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["parallelism"] == "dp2"
+    assert d["n_gpus"] == 2 and d["scaling"] == scaling and d["config"]["parallelism"] == "dp2"
     assert d["value"] > 0 and d["higher_is_better"] is True
+    if scaling == "strong":
+        assert d["config"]["global_batch"] == 4 and d["config"]["per_gpu_batch"] == 2
+    if gather_dtype:
+        assert d["config"]["gather_dtype"] == gather_dtype
+
+
+def test_rccl_choices_parser():
+    """bench.py records what RCCL chose from its INFO log."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_main", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # bench/ is a package: load the script by path
+    rccl_choices = mod.rccl_choices
+
+    log = "\n".join([
+        "host:1:1 [0] NCCL INFO RCCL version 2.26.6+hip7.0",
+        "host:1:1 [0] NCCL INFO Channel 00/32 : 0 1 2 3 4 5 6 7",
+        "host:1:1 [0] NCCL INFO Channel 01/32 : 0 2 4 6 1 3 5 7",
+        "host:1:1 [0] NCCL INFO 32 coll channels, 32 collnet channels, 0 nvls channels, 32 p2p channels, 4 p2p channels per peer",
+        "host:1:1 [0] NCCL INFO AllGather: algo Ring proto Simple nchannels 32 nthreads 256",
+        "host:1:1 [0] NCCL INFO AllGather: algo Ring proto Simple nchannels 32 nthreads 256",
+    ])
+    r = rccl_choices(log)
+    assert r["coll_channels"] == 32 and r["p2p_channels"] == 32 and r["ring_channels"] == 32
+    assert r["ring0"] == "0 1 2 3 4 5 6 7" and r["version"].startswith("2.26.6")
+    assert r["tuning"] == ["AllGather: algo Ring proto Simple nchannels 32 nthreads 256"]
+    assert rccl_choices("") == {}
 
 
 def test_rccl_sweep_harness_gloo():
