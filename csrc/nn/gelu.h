@@ -23,3 +23,29 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 }  // namespace amd_dft
+
+namespace amd_dft {
+
+// The same erf-GELU on two values with packed fp32 VALU (v_pk_fma_f32 / v_pk_mul_f32: one issue
+// slot for both values; rcp / exp2 / min / max stay per value).  Bit-identical to gelu_erf (same
+// operations in the same order, one rounding each).  For epilogues only: beside MFMAs packed
+// f32 VALU is an anti-lever (MI355X_MICROARCH.md, cycle constants), in an epilogue it halves the
+// polynomial's issue cost.
+typedef float gelu_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ gelu_f2 gelu_erf2(gelu_f2 x) {
+  const gelu_f2 ax = {fminf(fabsf(x.x), 1e30f), fminf(fabsf(x.y), 1e30f)};
+  const gelu_f2 d = __builtin_elementwise_fma(gelu_f2(0.3275911f * 0.70710678118654752f), ax, gelu_f2(1.f));
+  const gelu_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  gelu_f2 p = __builtin_elementwise_fma(gelu_f2(0.5f * 1.061405429f), t, gelu_f2(0.5f * -1.453152027f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(0.5f * 1.421413741f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(0.5f * -0.284496736f));
+  p = __builtin_elementwise_fma(p, t, gelu_f2(0.5f * 0.254829592f));
+  p *= t;
+  const gelu_f2 e = (x * x) * gelu_f2(-0.5f * 1.4426950408889634f);
+  const gelu_f2 ex = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  const gelu_f2 m = {fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
+  return __builtin_elementwise_fma(-ax * p, ex, m);
+}
+
+}  // namespace amd_dft

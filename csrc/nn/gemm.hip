@@ -106,8 +106,11 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
     const int chunk = pos ^ (row & 7);  // source swizzle = inverse of the read swizzle
     const int tr = region_row<REG>(row);
     const uint16_t* g;
+    // operands as a wave-uniform 64-bit base + a 32-bit lane offset (the SGPR-base form of
+    // global_load_lds: two fewer VGPRs per piece while the DMA issues inside an MFMA cluster)
     if constexpr (REG == 0 || REG == 3) {
-      g = W + static_cast<int64_t>(f0 + tr) * ld + kt * kBK + chunk * 8;
+      const uint16_t* base = W + static_cast<int64_t>(f0) * ld + kt * kBK;  // uniform
+      g = base + static_cast<uint32_t>(tr * static_cast<int>(ld) + chunk * 8);
     } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
       if constexpr (SPLIT) {  // channel kt / 2, patch rows (kt & 1) * 4 + c % 4 of the hi / lo plane
         const int py = (kt & 1) * 4 + (chunk & 3);
@@ -116,7 +119,8 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
         g = X + (gb[REG - 1][i] + (kt * (p.gh * 8) + chunk) * (p.gw * 8));
       }
     } else {
-      g = X + static_cast<int64_t>(min(t0 + tr, M - 1)) * ld + kt * kBK + chunk * 8;
+      const uint16_t* base = X + static_cast<int64_t>(t0) * ld + kt * kBK;  // uniform
+      g = base + static_cast<uint32_t>(min(tr, M - 1 - t0) * static_cast<int>(ld) + chunk * 8);
     }
     __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
   }
@@ -146,12 +150,23 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 // bf16: k-steps 0 and 1.  SPLIT: fragments [0..3] / [4..7] of A and [0..1] / [2..3] of B are
 // the hi / lo halves of one 32-deep K-tile: hi.hi + lo.hi + hi.lo, products outermost so
 // consecutive MFMAs never chain on one accumulator
-template <int MI, int NI, bool SPLIT>
-__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
+//
+// DMA placement (GEMM_DMA_MID, default on): the phase's two global_load_lds pieces are issued
+// by this (MFMA) wave after the first product's MFMAs, in the issue slots an MFMA leaves free
+// (a 16x16x32 MFMA holds the SIMD's issue for 8 of its 16 cycles), instead of by the partner
+// wave's read section, where their ~100-185-cycle issue cost (MI355X_MICROARCH.md, LDS-DMA
+// piece) made the read section longer than a 16-MFMA cluster.  Same pieces in the same order
+// per wave, so every vmcnt count is unchanged; each piece is issued half a phase later.
+#ifndef GEMM_DMA_MID
+#define GEMM_DMA_MID 1
+#endif
+template <int MI, int NI, bool SPLIT, class Mid>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
+                                              Mid&& mid) {
   __builtin_amdgcn_s_setprio(1);
   constexpr int NP = SPLIT ? 3 : 2;
 #pragma unroll
-  for (int s = 0; s < NP; ++s)
+  for (int s = 0; s < NP; ++s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -161,6 +176,12 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (
         acc[MI * 4 + i][NI * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[sa * 4 + i], b[sb * 2 + j],
                                                                                 acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
       }
+    if (GEMM_DMA_MID && s == 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -179,6 +200,26 @@ __device__ __forceinline__ void wait_regions(int n) {
 #else
 #define GEMM_STAMP(slot, v) do { } while (0)
 #endif
+
+// act(acc (LN-folded) + bias) of one accumulator tile (4 consecutive features of one token),
+// as two packed pairs: every FMA / MUL / ADD issues once for two values (epilogue VALU is 60 %
+// of a bf16x3 fc1 tile's epilogue).  Same operations and order as the per-value form.
+template <int ACT, bool LN>
+__device__ __forceinline__ void epi_act(const f32x4& a4, const float4& bias, const float4& c1, const float2& st,
+                                        gelu_f2 (&v)[2]) {
+  v[0] = gelu_f2{a4[0], a4[1]};
+  v[1] = gelu_f2{a4[2], a4[3]};
+  if constexpr (LN) {
+    v[0] = gelu_f2(st.y) * __builtin_elementwise_fma(gelu_f2(-st.x), gelu_f2{c1.x, c1.y}, v[0]);
+    v[1] = gelu_f2(st.y) * __builtin_elementwise_fma(gelu_f2(-st.x), gelu_f2{c1.z, c1.w}, v[1]);
+  }
+  v[0] += gelu_f2{bias.x, bias.y};
+  v[1] += gelu_f2{bias.z, bias.w};
+  if constexpr (ACT == 1) {
+    v[0] = gelu_erf2(v[0]);
+    v[1] = gelu_erf2(v[1]);
+  }
+}
 
 __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -298,35 +339,47 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     const int P = 4 * t;
     // ---- phase 0: quadrant (mi 0, ni 0)
     wait_regions(issued(P - 2) + issued(P - 1));
-    if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    auto dma0 = [&] {
+      if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    };
+    if (!GEMM_DMA_MID) dma0();
     if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 0, SPLIT>(acc, a0, b0);
+    mfma_quadrant<0, 0, SPLIT>(acc, a0, b0, dma0);
     barrier();
     // ---- phase 1: (0, 1)
     wait_regions(issued(P - 1) + issued(P));
-    if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    auto dma1 = [&] {
+      if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    };
+    if (!GEMM_DMA_MID) dma1();
     if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 1, SPLIT>(acc, a0, b1);
+    mfma_quadrant<0, 1, SPLIT>(acc, a0, b1, dma1);
     barrier();
     // ---- phase 2: (1, 1)
     wait_regions(issued(P) + issued(P + 1));
-    if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    auto dma2 = [&] {
+      if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+    };
+    if (!GEMM_DMA_MID) dma2();
     if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 1, SPLIT>(acc, a1, b1);
+    mfma_quadrant<1, 1, SPLIT>(acc, a1, b1, dma2);
     barrier();
     // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
     wait_regions(issued(P + 1) + issued(P + 2));
-    if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
+    auto dma3 = [&] {
+      if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
+    };
+    if (!GEMM_DMA_MID) dma3();
     if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
     barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 0, SPLIT>(acc, a1, b0);
+    mfma_quadrant<1, 0, SPLIT>(acc, a1, b0, dma3);
     barrier();
   }
   if (wr == 0) barrier();  // re-align the two wave groups
@@ -387,16 +440,10 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           const int i = 4 * h + ii;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float a = acc[i][j][e];
-              if constexpr (LN) a = lst[j].y * fmaf(-lst[j].x, (&c14[i].x)[e], a);
-              v[e] = a + (&bias4[i].x)[e];
-              if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
-            }
+            gelu_f2 v[2];
+            epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], v);
             const int row = j * 16 + r16, ch = ii * 4 + kq;
-            *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
           }
         }
 #pragma unroll
@@ -426,13 +473,18 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                 v[2 * k + 1] += __uint_as_float(rw[k] & 0xffff0000u);
               }
             }
-            if constexpr (OUT == 2) {
-              if ((c >> 2) & 1) {  // lo part
+            uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+            if constexpr (OUT == 2) {  // lanes with (c >> 2) & 1 store the lo part: v - hi, branch-free
+              const bool lo = (c >> 2) & 1;
+              uint32_t* wp = &w.x;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] -= static_cast<float>(static_cast<__bf16>(v[k]));
+              for (int k = 0; k < 4; ++k) {
+                const gelu_f2 hf = {__uint_as_float(wp[k] << 16), __uint_as_float(wp[k] & 0xffff0000u)};
+                const gelu_f2 d = gelu_f2{v[2 * k], v[2 * k + 1]} - hf;
+                const uint32_t lw = pk_bf16(d.x, d.y);
+                wp[k] = lo ? lw : wp[k];
               }
             }
-            const uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
             if (t < M) {
               if constexpr (OUT == 0) {
                 *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
@@ -472,18 +524,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     for (int ii = 0; ii < 2; ++ii) {
       const int i = 2 * ip + ii;
       const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-      const float bv[4] = {bias4[i].x, bias4[i].y, bias4[i].z, bias4[i].w};
-      const float cv[4] = {c14[i].x, c14[i].y, c14[i].z, c14[i].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float a = acc[i][j][e];
-          if constexpr (LN) a = lst[j].y * fmaf(-lst[j].x, cv[e], a);
-          v[e] = a + bv[e];
-          if constexpr (ACT == 1) v[e] = gelu_erf(v[e]);
-        }
+        gelu_f2 vp[2];
+        epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], vp);
+        float v[4] = {vp[0].x, vp[0].y, vp[1].x, vp[1].y};
         if constexpr (ERES) {
           const ResT rr = rq[ip & 1][ii][j];
           if constexpr (OUT == 1) {  // fp32 residual (in place allowed: same lane reads, then writes)
@@ -502,12 +547,12 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           if constexpr (OUT == 1) {
             *reinterpret_cast<float4*>(static_cast<float*>(p.y) + out_off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
           } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
-            float lo[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) lo[e] = v[e] - static_cast<float>(static_cast<__bf16>(v[e]));
+            const uint2 hw = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            const gelu_f2 d0 = gelu_f2{v[0], v[1]} - gelu_f2{__uint_as_float(hw.x << 16), __uint_as_float(hw.x & 0xffff0000u)};
+            const gelu_f2 d1 = gelu_f2{v[2], v[3]} - gelu_f2{__uint_as_float(hw.y << 16), __uint_as_float(hw.y & 0xffff0000u)};
             uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(tok(j)) * (2 * N) + (f >> 5) * 64 + (f & 31);
-            *reinterpret_cast<uint2*>(yr) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
-            *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]));
+            *reinterpret_cast<uint2*>(yr) = hw;
+            *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(d0.x, d0.y), pk_bf16(d1.x, d1.y));
           } else {
             *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + out_off(i, j)) =
                 make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));

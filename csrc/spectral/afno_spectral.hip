@@ -54,6 +54,16 @@ constexpr int kNT = 256;  // threads
 #ifndef AFNO_BPF3
 #define AFNO_BPF3 2  // k-steps of B-fragment prefetch in the bf16x3 block-MLP GEMMs
 #endif
+#ifndef AFNO_DIAG
+#define AFNO_DIAG 0  // diagnostic builds only (scripts/diag/afno_o3_bisect.sh): 1 = 32 wait states after every
+                     // k-step's MFMA group (fragment registers reloaded while MFMAs may still read them),
+                     // 2 = 32 wait states after each GEMM, before its accumulators are read
+#endif
+__device__ __forceinline__ void diag_guard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 #ifndef AFNO_ABLATE
 #define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs,
                        // 4 = x3 GEMM B fragments of k-step 0 reused (no weight loads after the first)
@@ -199,7 +209,9 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
         if constexpr (AFNO_ABLATE & 2) acc[mi][nj] += __builtin_bit_cast(f32x4, afr[mi]) + __builtin_bit_cast(f32x4, bq[ks % NQ][nj]);
         else acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
       }
+    if constexpr (AFNO_DIAG & 1) diag_guard();
   }
+  if constexpr (AFNO_DIAG & 2) diag_guard();
 }
 
 template <class S, bool BFI, bool BFO>
@@ -462,7 +474,9 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
         acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
       }
     }
+    if constexpr (AFNO_DIAG & 1) diag_guard();
   }
+  if constexpr (AFNO_DIAG & 2) diag_guard();
 }
 
 template <class S>

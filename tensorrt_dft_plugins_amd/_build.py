@@ -8,7 +8,12 @@ by ``hipcc --offload-arch=gfx950`` into objects under ``build/`` and linked into
 looks, like the reference's CMAKE_LIBRARY_OUTPUT_DIRECTORY).  No hipify step, no CUDA
 sources, no rocFFT/hipFFT/hipBLAS link.
 
-Usage: ``python -m tensorrt_dft_plugins_amd._build [--force] [-j N]``
+Usage: ``python -m tensorrt_dft_plugins_amd._build [--force] [-j N] [--out DIR]``
+
+``--out DIR`` builds a separate copy (objects under DIR/obj, library DIR/_C.so) without touching
+the in-tree one: scripts/ci_gpu.sh compiles every source on the GPU box this way and runs the
+GPU tier against that library (``MI_DFT_LIB=DIR/_C.so``), the reference's build-then-test
+practice (/root/reference/build_with_docker.sh:39).
 """
 from __future__ import annotations
 
@@ -20,6 +25,7 @@ import shutil
 import subprocess
 import sys
 import sysconfig
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
@@ -64,8 +70,10 @@ def _headers_mtime() -> float:
     return max([os.path.getmtime(h) for h in hs] + [0.0])
 
 
-def _obj_path(src: str, asan: bool = False) -> str:
+def _obj_path(src: str, asan: bool = False, obj_dir: str | None = None) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+    if obj_dir:
+        return os.path.join(obj_dir, rel + ".o")
     return os.path.join(BUILD_ASAN if asan and not src.endswith(".hip") else BUILD, rel + ".o")
 
 
@@ -79,8 +87,8 @@ def _file_flags(src: str) -> list:
     return []
 
 
-def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False) -> str:
-    obj = _obj_path(src, asan)
+def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False, obj_dir: str | None = None) -> str:
+    obj = _obj_path(src, asan, obj_dir)
     cmd = [_hipcc(), "-c", "-fPIC", "-std=c++17", "-O3", "-Wall", "-Wno-unused-function",
            "-Wno-unused-variable", "-Wno-sign-compare", "-I" + CSRC,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-o", obj]
@@ -110,33 +118,39 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False) ->
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True, asan: bool = False) -> str:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, asan: bool = False,
+          out: str | None = None) -> str:
     """Compile every HIP/C++ source for gfx950 and link ``_C.so``; returns its path.
-    ``asan``: host C++ with AddressSanitizer into build/asan/_C.so (device objects shared)."""
-    os.makedirs(BUILD, exist_ok=True)
+    ``asan``: host C++ with AddressSanitizer into build/asan/_C.so (device objects shared).
+    ``out``: a separate build directory (objects in out/obj, library out/_C.so)."""
+    if out and asan:
+        raise ValueError("--out and --asan are exclusive")
+    obj_dir = os.path.join(os.path.abspath(out), "obj") if out else None
+    os.makedirs(obj_dir or BUILD, exist_ok=True)
     if asan:
         os.makedirs(BUILD_ASAN, exist_ok=True)
-    lib = LIB_ASAN if asan else LIB
+    lib = os.path.join(os.path.abspath(out), "_C.so") if out else (LIB_ASAN if asan else LIB)
     tinc, tlib, abi = _torch_paths()
     hdr = _headers_mtime()
     srcs = sources()
     todo = []
     for src, nt in srcs:
-        obj = _obj_path(src, asan)
+        obj = _obj_path(src, asan, obj_dir)
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
             todo.append((src, nt))
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    t0 = time.time()
     if todo:
         if verbose:
             print(f"[amd_dft build] compiling {len(todo)} file(s) for {ARCH} with {jobs} jobs"
                   + (" (host ASan)" if asan else ""), flush=True)
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = {ex.submit(_compile, s, nt, tinc, abi, asan): s for s, nt in todo}
+            futs = {ex.submit(_compile, s, nt, tinc, abi, asan, obj_dir): s for s, nt in todo}
             for f in cf.as_completed(futs):
                 f.result()
                 if verbose:
                     print("  built", os.path.relpath(futs[f], ROOT), flush=True)
-    objs = [_obj_path(s, asan) for s, _ in srcs]
+    objs = [_obj_path(s, asan, obj_dir) for s, _ in srcs]
     if todo or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
         tmp = lib + ".tmp"
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
@@ -149,7 +163,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, lib)
         if verbose:
-            print("[amd_dft build] linked", os.path.relpath(lib, ROOT), flush=True)
+            print(f"[amd_dft build] linked {os.path.relpath(lib, ROOT)} ({len(todo)} compiled, "
+                  f"{time.time() - t0:.0f} s)", flush=True)
     return lib
 
 
@@ -158,8 +173,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--asan", action="store_true", help="host AddressSanitizer build into build/asan/_C.so")
+    ap.add_argument("--out", default=None, help="separate build directory (library at OUT/_C.so)")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.j, asan=a.asan)
+    build(force=a.force, jobs=a.j, asan=a.asan, out=a.out)
 
 
 if __name__ == "__main__":

@@ -305,17 +305,35 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     ops = _ops()
     pre32 = None if pre is None else _f32(blk, "pre", pre)
     g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
+    dup = _DUP  # diagnostic (MI_DFT_DUP): run one stage twice to measure its in-step marginal cost
     stats = ops.ln_stats(xs, pre32, n1.eps)
+    if dup == "ln_stats":
+        stats = ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
+    if dup == "r2c":
+        xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
+    if dup == "spectral":
+        yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
     x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    if dup == "c2r":
+        x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
     yn = ops.layer_norm_split(x1.reshape(-1, C), n2.weight, n2.bias, n2.eps, None)
+    if dup == "ln_split":
+        yn = ops.layer_norm_split(x1.reshape(-1, C), n2.weight, n2.bias, n2.eps, None)
     w1s = module_cached(m, "fc1_split", (m.fc1.weight,), lambda: split_bf16(m.fc1.weight))
     w2s = module_cached(m, "fc2_split", (m.fc2.weight,), lambda: split_bf16(m.fc2.weight))
     b1 = _f32(m, "fc1_b", m.fc1.bias)
     hid = ops.linear3(yn, w1s, b1, 1, None, True)
+    if dup == "fc1":
+        hid = ops.linear3(yn, w1s, b1, 1, None, True)
     x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
+    if dup == "fc2":
+        x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
     return x1, m.fc2.bias
+
+
+_DUP = os.environ.get("MI_DFT_DUP", "")
 
 
 _MLP_HAND: Optional[bool] = None

@@ -183,8 +183,8 @@ def test_bench_harness_torchrun_gloo(extra, scaling, gather_dtype):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--tiny", "--gpus", "2",
            "--steps", "2", "--warmup", "1"] + extra
-    env = dict(os.environ)
-    env.pop("CUDA_VISIBLE_DEVICES", None)
+    # a CPU-tier test: hide any GPU (on the GPU box two ranks would otherwise pick RCCL on one device)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", MI_DFT_DIST_BACKEND="gloo")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     import json
@@ -229,8 +229,8 @@ def test_rccl_sweep_harness_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench", "bench_rccl.py"), "--mb", "0.01",
            "--iters", "2", "--dtype", "fp32"]
-    env = dict(os.environ)
-    env.pop("CUDA_VISIBLE_DEVICES", None)
+    # a CPU-tier test: hide any GPU (on the GPU box two ranks would otherwise pick RCCL on one device)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", MI_DFT_DIST_BACKEND="gloo")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     import json
