@@ -73,6 +73,22 @@ struct FL {
 };
 
 constexpr __host__ __device__ int lds_pad(int i) { return i + (i >> 4); }
+// Row-layout padding per length: one float2 every 2^S elements (S = 0: none).  Chosen from a
+// bank-conflict simulation of the Stockham read / write patterns (ds_read_b64 / ds_write_b64,
+// two 32-lane groups): 1440 = (10, 12, 12) at 144 threads is conflict-free unpadded (the n/16
+// pad made its writes 3x), and an unpadded index is linear in the radix step, so the compiler
+// folds it into ds_read / ds_write immediate offsets (no per-element index arithmetic);
+// 720 = (8, 9, 10) is best with one pad per 8.  Column layouts (position-major, T signals per
+// position) use a stride of T + 1 slots per position for T >= 4: the same or fewer conflicts than
+// the n/16 pad on every configured shape and, again, an index linear in the position.
+template <bool COLS, int L>
+constexpr __host__ __device__ int row_pad_shift() {
+  return COLS ? 4 : (L == 1440 ? 0 : (L == 720 ? 3 : 4));
+}
+template <bool COLS, int L>
+constexpr __host__ __device__ int lds_padl(int i) {
+  return row_pad_shift<COLS, L>() == 0 ? i : i + (i >> row_pad_shift<COLS, L>());
+}
 
 __device__ __forceinline__ float bf_to_f(uint32_t u16) { return __uint_as_float(u16 << 16); }
 __device__ __forceinline__ uint32_t f_to_bf(float f) {
@@ -149,9 +165,10 @@ __device__ __forceinline__ float2 ln_pair(const Ctx& x, int n, float2 v, float2&
 
 template <bool COLS, int T, int L>
 __device__ __forceinline__ int lidx(const Ctx& x, int n) {
-  constexpr int LP = lds_pad(L) + 1;
-  if constexpr (COLS) return lds_pad(n * T + x.t);
-  else return x.t * LP + lds_pad(n);
+  constexpr int LP = lds_padl<COLS, L>(L) + 1;
+  if constexpr (COLS && T >= 4) return n * (T + 1) + x.t;  // one pad slot per position: linear in n
+  else if constexpr (COLS) return lds_pad(n * T + x.t);
+  else return x.t * LP + lds_padl<COLS, L>(n);
 }
 
 // First-pass element fetch (includes the C2R Hermitian assembly and input pruning).
@@ -469,7 +486,7 @@ __device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int 
 // LDS image of one tile (float2 entries) for T signal slots
 template <bool COLS, int T, int L>
 constexpr int tile_lds(int slots = T) {
-  return COLS ? lds_pad(L * T) + 2 : slots * (lds_pad(L) + 1);
+  return COLS ? (T >= 4 ? L * (T + 1) + 2 : lds_pad(L * T) + 2) : slots * (lds_padl<COLS, L>(L) + 1);
 }
 
 template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>

@@ -14,28 +14,37 @@
 
 namespace amd_dft {
 
-__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 c_neg(float2 a) { return make_float2(-a.x, -a.y); }
-__device__ __forceinline__ float2 c_mul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+// One complex value as (re, im) in a register pair: every add / sub / scale is ONE packed fp32
+// instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32; broadcasts and the re/im swap of a
+// quarter turn fold into op_sel / neg modifiers), half the VALU issue of the scalar form.  The
+// FFT passes are VALU-issue bound at about one wave per SIMD (profiles/fft_xcd_r2.txt), so the
+// instruction count per point is their cost.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v v2(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 f2(f2v a) { return make_float2(a.x, a.y); }
+__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return f2(v2(a) + v2(b)); }
+__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return f2(v2(a) - v2(b)); }
+__device__ __forceinline__ float2 c_neg(float2 a) { return f2(-v2(a)); }
+__device__ __forceinline__ float2 c_mul(float2 a, float2 b) {  // (ax bx - ay by, ax by + ay bx)
+  const f2v va = v2(a), vb = v2(b);
+  return f2(__builtin_elementwise_fma(va.yy, f2v{-vb.y, vb.x}, va.xx * vb));
 }
-// a * e^{-i theta} with (c, s) = (cos theta, sin theta)
+// a * e^{-i theta} with (c, s) = (cos theta, sin theta): (ax c + ay s, ay c - ax s)
 __device__ __forceinline__ float2 c_mul_w(float2 a, float c, float s) {
-  return make_float2(a.x * c + a.y * s, a.y * c - a.x * s);
+  const f2v va = v2(a);
+  return f2(__builtin_elementwise_fma(va.yx, f2v{s, -s}, va * f2v{c, c}));
 }
 __device__ __forceinline__ float2 c_mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // -i*a
 __device__ __forceinline__ float2 c_mul_posi(float2 a) { return make_float2(-a.y, a.x); }  //  i*a
-__device__ __forceinline__ float2 c_scale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 c_scale(float2 a, float s) { return f2(v2(a) * f2v{s, s}); }
 __device__ __forceinline__ float2 c_fmas(float s, float2 a, float2 acc) {  // acc + s * a
-  return make_float2(fmaf(s, a.x, acc.x), fmaf(s, a.y, acc.y));
+  return f2(__builtin_elementwise_fma(f2v{s, s}, v2(a), v2(acc)));
 }
 
 // Two complex signals that share every twiddle (e.g. two adjacent channels of a batched FFT),
 // held as planes: re = (re0, re1), im = (im0, im1).  Every butterfly op is then one packed
 // fp32 instruction (v_pk_add/mul/fma_f32) per plane with no re/im shuffles, and a quarter
 // turn (+-i) is a free plane swap -- half the VALU issue of two scalar float2 signals.
-typedef float f2v __attribute__((ext_vector_type(2)));
 struct cpair {
   f2v re, im;
 };

@@ -151,14 +151,14 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 // the hi / lo halves of one 32-deep K-tile: hi.hi + lo.hi + hi.lo, products outermost so
 // consecutive MFMAs never chain on one accumulator
 //
-// DMA placement (GEMM_DMA_MID, default on): the phase's two global_load_lds pieces are issued
-// by this (MFMA) wave after the first product's MFMAs, in the issue slots an MFMA leaves free
-// (a 16x16x32 MFMA holds the SIMD's issue for 8 of its 16 cycles), instead of by the partner
-// wave's read section, where their ~100-185-cycle issue cost (MI355X_MICROARCH.md, LDS-DMA
-// piece) made the read section longer than a 16-MFMA cluster.  Same pieces in the same order
-// per wave, so every vmcnt count is unchanged; each piece is issued half a phase later.
+// DMA placement (GEMM_DMA_MID, experiment, default OFF): the phase's two global_load_lds pieces
+// issued by this (MFMA) wave after the first product's MFMAs, in the issue slots an MFMA leaves
+// free, instead of by the partner wave's read section.  Same pieces in the same order per wave,
+// so every vmcnt count is unchanged.  Measured slower (profiles/gemm_dma_mid_r3.txt: bf16x3 fc1
+// 5.99 vs 5.50-5.57 ms, fc2 5.10-5.15 vs 4.55 ms, bf16 fc2 2.20 vs 2.11 ms, ABAB on one box):
+// the pieces then start half a phase later and the MFMA cluster itself stalls on their issue.
 #ifndef GEMM_DMA_MID
-#define GEMM_DMA_MID 1
+#define GEMM_DMA_MID 0
 #endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
