@@ -22,6 +22,7 @@ def main(argv=None):
     ap.add_argument("--rows", type=int, default=32 * 16200)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--x3", action="store_true", help="bf16x3 split GEMMs (fp32 path) + the bf16 hand GEMMs")
+    ap.add_argument("--iters", type=int, default=3, help="calls per captured graph (sustained-load check: e.g. 30)")
     a = ap.parse_args(argv)
     tdp.load_plugins()
     M, C, Hd = a.rows, 768, 3072
@@ -56,7 +57,7 @@ def main(argv=None):
     res = {k: [] for k in v}
     for _ in range(a.rounds):
         for k, f in v.items():
-            res[k].append(time_graph(f, 3))
+            res[k].append(time_graph(f, a.iters))
     flop = 2.0 * M * C * Hd
     out = {}
     for k, t in res.items():

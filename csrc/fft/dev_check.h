@@ -17,8 +17,21 @@
       return;                                                                                    \
     }                                                                                            \
   } while (0)
+// LDS access check for vectorised (ds_read/write_b128) staging: prints when a byte offset is not
+// aligned to the access width or the access ends past the workgroup's LDS size (no return: it
+// sits inside inline helpers)
+#define AMD_DFT_DEV_LDS(off, width, limit, what)                                                    \
+  do {                                                                                            \
+    const long long o_ = static_cast<long long>(off);                                             \
+    if ((o_ % (width)) != 0 || o_ < 0 || o_ + (width) > static_cast<long long>(limit))            \
+      printf("amd_dft LDS check failed in %s: offset %lld width %d limit %lld (block %u thread %u)\n", what, o_, \
+             static_cast<int>(width), static_cast<long long>(limit), blockIdx.x, threadIdx.x);    \
+  } while (0)
 #else
 #define AMD_DFT_DEV_CHECK(cond, kernel) \
   do {                                  \
+  } while (0)
+#define AMD_DFT_DEV_LDS(off, width, limit, what) \
+  do {                                           \
   } while (0)
 #endif

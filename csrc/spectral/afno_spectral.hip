@@ -10,6 +10,18 @@
 // grid, and is faster than the -O1 build used before (bf16 452 vs 477 us, bf16x3 842 vs
 // 881 us at [32, 90, 46, 768]; scripts/diag/afno_race_diag.py, afno_poison_diag.py,
 // profiles/afno_o1_fix_r2.txt).
+// Round-3 bisection (profiles/afno_o3_bisect_r3.txt): 32 wait states after every MFMA k-step
+// group or after each GEMM (AFNO_DIAG=1/2) do NOT cure the vectorizer-on build, so it is no
+// MFMA read/write hazard; a static dataflow check of the compiled code
+// (scripts/diag/barrier_lds_check.py) finds no s_barrier reachable with LDS operations in
+// flight, in either build; the fp32 W-transforms (afno_wfft.hip) use the same 16-byte
+// ds_read/write_b128 staging at 3 workgroups per CU and are exact, and in the bf16 kernel the
+// vectorizer changes no LDS or global access at all -- only the kernel-argument scalar loads
+// (merged into s_load_dwordx4/x8, one moved into a conditional block) and the schedule.  The
+// cause is therefore a code-generation difference outside the memory operations, not a data
+// race in this source; the vectorizer stays off for this file, the determinism screen
+// (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids, and
+// MI_DFT_DEVICE_CHECKS builds check every 16-byte staging access for alignment and bounds.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
@@ -400,10 +412,17 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
 // bf16 planes [16 MT][APitch] (hi, lo) when it is written to LDS; the weights arrive pre-split
 // as k32-interleaved rows [NB][2BS n][2 * 2BS k].  76.8 KB of LDS at H = 90, BS = 96: 2
 // workgroups per CU.
+// LIMIT: the workgroup's dynamic LDS bytes; MI_DFT_DEVICE_CHECKS builds check every 16-byte
+// staging access against it and its alignment (the accesses the -O3 vectorizer turns into
+// ds_read_b128 / ds_write_b128)
+template <int64_t LIMIT>
 __device__ __forceinline__ void st_fp(float2* p, int i, const cpair& v) {
+  AMD_DFT_DEV_LDS(static_cast<int64_t>(i) * 8, 16, LIMIT, "afno st_fp");
   *reinterpret_cast<float4*>(p + i) = make_float4(v.re[0], v.im[0], v.re[1], v.im[1]);
 }
+template <int64_t LIMIT>
 __device__ __forceinline__ cpair ld_fp(const float2* p, int i) {
+  AMD_DFT_DEV_LDS(static_cast<int64_t>(i) * 8, 16, LIMIT, "afno ld_fp");
   const float4 q = *reinterpret_cast<const float4*>(p + i);
   return cpair{f2v{q.x, q.z}, f2v{q.y, q.w}};
 }
@@ -483,6 +502,7 @@ template <class S>
 __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs a) {
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
+  constexpr int64_t LDSB = (2LL * L * BS * 4 > 4LL * plane) ? 2LL * L * BS * 4 : 4LL * plane;  // == make_instance lds_x3
   extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][BS] complex fp32
   uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [16 MT][APitch] bf16 hi
   uint16_t* Al = Ah + plane;                                     //          [16 MT][APitch] bf16 lo
@@ -521,7 +541,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_fp<LDSB>(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
@@ -535,7 +555,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
@@ -610,7 +630,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp(ldsf, (j + r * P0::LR) * BS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * BS + 2 * tp);
       }
     }
     __syncthreads();
@@ -621,7 +641,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) st_fp(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
+        for (int r = 0; r < R0; ++r) st_fp<LDSB>(ldsf, (j * R0 + r) * BS + 2 * tp, v[q][r]);
       }
     }
   }
@@ -635,7 +655,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P1::NB % kNT == 0 || bb < P1::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
     h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);

@@ -28,6 +28,10 @@
 
 #include "dft_gemm.h"
 
+#ifndef FNO_EPI_STAGED
+#define FNO_EPI_STAGED 1  // output through a per-wave LDS tile in full-line stores (0: straight from the MFMA layout)
+#endif
+
 namespace amd_dft {
 namespace {
 
@@ -124,6 +128,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // stalled every chunk)
   // (launch_fno_c2r_pw guarantees nch * 16 KS <= kFnoRotMax)
   __shared__ float2 rots[kFnoRotMax];
+#if FNO_EPI_STAGED
+  // per-wave output staging: [32 channel rows][PXS pixels] (64 bytes of a row), pitch + 16 B (bank
+  // spread); 10 KB per workgroup, so two workgroups still share a CU
+  // (m > 32: the larger twiddle table leaves no room -- straight stores)
+  constexpr bool STG = KS <= 2;
+  constexpr int PXS = 64 / ES, EP = 64 + 16;
+  __shared__ __attribute__((aligned(16))) char es_raw[STG ? 4 : 1][STG ? 32 * EP : 16];
+#endif
   const int nrot = nch * 16 * KS;
   for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -176,6 +188,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // space and the stores become flat stores, which every later LDS wait would also drain)
   int64_t yrow[CO];  // &y[b][16 ot + l15][h][4 lq] - y  (clamped to a valid channel)
   int64_t yrowp = 0;  // same for the packed channel tile: channel 16 + (l15 & 3)
+  int64_t ybase = 0;  // &y[b][0][h][0] - y (staged epilogue)
   char* const yb = static_cast<char*>(y);
 
   // x staging: this lane's 8-pixel pieces of channel rows st_ch + RPI*q of unit u, kept in
@@ -219,6 +232,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
           }
       const int64_t y0 = ((b * Cout * H + h) * W + 4 * lq) * ES;
+      ybase = (b * Cout * H + h) * W * ES;
 #pragma unroll
       for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
       yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
@@ -312,6 +326,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
       // ---- epilogue: activation + store, 4 consecutive pixels of one channel per lane
       const int pxg = w0 + 64 * pg + 4 * lq;  // pixel of row i = 0 in tile p4 = 0
+#if FNO_EPI_STAGED
+      // Through LDS: straight from the MFMA layout every store instruction would write 16
+      // channel rows x 32 B (partial lines); staged, a lane stores 16 B and 8 (bf16) / 16 (fp32)
+      // lanes fill one 128 / 256-byte run of a channel row.
+      if constexpr (STG) {
+        char* es = es_raw[wv];
+        constexpr int TPS = PXS / 16;  // pixel tiles per staging pass
+#pragma unroll
+        for (int hp = 0; hp < 4 / TPS; ++hp) {
+          wave_lds_fence();
+#pragma unroll
+          for (int ot = 0; ot < CO; ++ot) {
+            const int ch = 16 * ot + l15;
+#pragma unroll
+            for (int pp = 0; pp < TPS; ++pp) {
+              const int p4 = hp * TPS + pp;
+              float v[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
+              if (ch < Cout) store4<BF>(es + ch * EP + (16 * pp + 4 * lq) * ES, v);
+            }
+          }
+          wave_lds_fence();
+          // 4 lanes x 16 B = one 64-byte run of a channel row; 16 rows per store instruction
+          const int sub = lane >> 2, px = (lane & 3) * (16 / ES);
+          const int wpx = w0 + 64 * pg + PXS * hp + px;
+#pragma unroll
+          for (int r0 = 0; r0 < 32; r0 += 16) {
+            const int ch = r0 + sub;
+            if (r0 < Cout && ch < Cout && wpx < W) {
+              const uint4 q = *reinterpret_cast<const uint4*>(es + ch * EP + px * ES);
+              *reinterpret_cast<uint4*>(yb + ybase + ch * plane + static_cast<int64_t>(wpx) * ES) = q;
+            }
+          }
+        }
+      }
+      if constexpr (!STG)
+#endif
+      {
 #pragma unroll
       for (int ot = 0; ot < CO; ++ot) {
         if (ot == 1 && pack) break;
@@ -336,6 +389,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
         const int o = 16 + cc;
         if (o < Cout && pxg + 16 * s < W) store4<BF>(yb + yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
+      }
       }
     }
   }
