@@ -227,7 +227,20 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
+// sum over a 16-lane DPP row (every lane gets the total): quad swaps, then the 8- and 16-lane mirrors
+__device__ __forceinline__ float row_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));  // row_mirror
+  return x;
+}
+
+// STATS (fp32 output, LDS-staged epilogue): per token and 64-feature chunk of the output plus the
+// per-channel p.stats_pre, the chunk's (mean, M2 = sum of squared deviations) into
+// p.stats_part[t][chunk] -- the next LayerNorm's statistics without a pass over the output
+// (merged per token by ln_stats_merge, Chan's formula)
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
   const uint16_t* __restrict__ W = p.w;
@@ -446,6 +459,10 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
           }
         }
+        float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (STATS) {
+          if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
+        }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
           const int row = it * RPI + rsub, t = tbase + row;
@@ -459,6 +476,15 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               v.w += rr[it].w;
             }
             if (t < M) *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
+            if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
+              const float w0 = v.x + spre.x, w1 = v.y + spre.y, w2 = v.z + spre.z, w3 = v.w + spre.w;
+              const float mean = row_sum16((w0 + w1) + (w2 + w3)) * (1.f / 64.f);
+              const float d0 = w0 - mean, d1 = w1 - mean, d2 = w2 - mean, d3 = w3 - mean;
+              const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+              if (c == 0 && t < M)
+                *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
+                    make_float2(mean, m2);
+            }
           } else {
             // OUT 0: lane = 8 features (chunks 2c, 2c+1); OUT 2: lane c = (half-chunk ch, part, sub)
             const int fl = OUT == 0 ? 8 * c : (c >> 3) * 32 + (c & 3) * 8;
@@ -565,9 +591,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT>
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false>
 void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
-  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT>;
+  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS>;
   // the dynamic-LDS limit is a per-device function attribute: set it once per (instance, device)
   static std::atomic<uint64_t> attr_done{0};
   int dev = 0;
@@ -599,6 +625,13 @@ void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   if (p.out == 2) {
     if (p.residual) throw std::runtime_error("amd_dft: gemm: split-pair output takes no residual");
     launch_one<ACT, BIAS, false, false, 0, true, 2>(p, st, grid);
+  } else if (p.residual && p.stats_part) {  // fc2 of the fp32 block: + next LayerNorm's partial statistics
+    if constexpr (ACT == 0 && !BIAS) {
+      if (p.direct_epi) throw std::runtime_error("amd_dft: gemm: statistics need the LDS-staged epilogue");
+      launch_one<ACT, BIAS, true, false, 0, true, 1, true>(p, st, grid);
+    } else {
+      throw std::runtime_error("amd_dft: gemm: output statistics only without activation and bias");
+    }
   } else if (p.residual) {
     launch_one<ACT, BIAS, true, false, 0, true, 1>(p, st, grid);
   } else {

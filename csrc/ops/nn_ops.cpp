@@ -433,6 +433,64 @@ at::Tensor linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10:
   return y;
 }
 
+// fc2 of the fp32 FourCastNet block: y = xs ws^T + residual (bf16x3, fp32 out) and, from the same
+// epilogue, the next LayerNorm's partial statistics of y + pre: part [M, N/64, 2] = per 64-feature
+// chunk (mean, M2); ln_stats_merge turns them into (mean, rstd) without another pass over y
+std::tuple<at::Tensor, at::Tensor> linear3_stats_cpu(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor& residual,
+                                                     const c10::optional<at::Tensor>& pre) {
+  at::Tensor y = linear3_cpu(xs, ws, c10::nullopt, 0, residual, false);
+  const int64_t N = ws.size(0);
+  TORCH_CHECK(N % 64 == 0, "amd_dft.linear3_stats: N must be a multiple of 64");
+  at::Tensor w = y.reshape({-1, N});
+  if (pre.has_value() && pre->defined()) w = w + pre->to(at::kFloat).reshape({1, N});
+  w = w.reshape({w.size(0), N / 64, 64});
+  at::Tensor mean = w.mean(2);
+  at::Tensor m2 = (w - mean.unsqueeze(2)).pow(2).sum(2);
+  return {y, at::stack({mean, m2}, 2).contiguous()};
+}
+
+std::tuple<at::Tensor, at::Tensor> linear3_stats_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const at::Tensor& residual,
+                                                      const c10::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(xs_.device());
+  check_split_linear(xs_, ws_, c10::nullopt, "linear3_stats");
+  TORCH_CHECK(xs_.size(-1) == ws_.size(1), "amd_dft.linear3_stats: xs [..., 2K], ws [N, 2K]");
+  const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_stats: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0");
+  TORCH_CHECK(residual.numel() == M * N, "amd_dft.linear3_stats: residual must have the output's shape");
+  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous(), r = residual.to(at::kFloat).contiguous();
+  at::Tensor pre;
+  if (pre_.has_value() && pre_->defined()) {
+    pre = pre_->to(at::kFloat).contiguous();
+    TORCH_CHECK(pre.numel() == N, "amd_dft.linear3_stats: pre must have N entries");
+  }
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = N;
+  at::Tensor y = at::empty(os, xs.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({M, N / 64, 2}, xs.options().dtype(at::kFloat));
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(xs.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  p.residual = r.data_ptr();
+  p.y = y.data_ptr();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.split = 1;
+  p.out = 1;
+  p.stats_part = part.data_ptr<float>();
+  p.stats_pre = pre.defined() ? pre.data_ptr<float>() : nullptr;
+  if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
+  return {y, part};
+}
+
+std::tuple<at::Tensor, at::Tensor> linear3_stats_meta(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor&,
+                                                      const c10::optional<at::Tensor>&) {
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = ws.size(0);
+  const int64_t M = xs.numel() / std::max<int64_t>(xs.size(-1), 1);
+  return {at::empty(os, xs.options().dtype(at::kFloat)), at::empty({M, ws.size(0) / 64, 2}, xs.options().dtype(at::kFloat))};
+}
+
 at::Tensor linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>&, int64_t,
                         const c10::optional<at::Tensor>&, bool split_out) {
   std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
@@ -555,6 +613,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("linear_unpatch(Tensor t, Tensor w, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
   m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
   m.def("linear3(Tensor xs, Tensor ws, Tensor? bias=None, int act=0, Tensor? residual=None, bool split_out=False) -> Tensor");
+  m.def("linear3_stats(Tensor xs, Tensor ws, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("patch_linear3(Tensor xs, Tensor ws, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
   m.def("linear_unpatch3(Tensor ts, Tensor ws, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
 }
@@ -567,6 +626,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cuda));
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cuda));
+  m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cuda));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cuda));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cuda));
 }
@@ -579,6 +639,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("linear_unpatch", AMD_DFT_TRACED("amd_dft::linear_unpatch", amd_dft::linear_unpatch_cpu));
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cpu));
+  m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cpu));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cpu));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cpu));
 }
@@ -591,6 +652,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("linear_unpatch", &amd_dft::linear_unpatch_meta);
   m.impl("split_bf16", &amd_dft::split_bf16_meta);
   m.impl("linear3", &amd_dft::linear3_meta);
+  m.impl("linear3_stats", &amd_dft::linear3_stats_meta);
   m.impl("patch_linear3", &amd_dft::patch_linear3_meta);
   m.impl("linear_unpatch3", &amd_dft::linear_unpatch3_meta);
 }

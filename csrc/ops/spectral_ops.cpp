@@ -454,6 +454,29 @@ at::Tensor ln_stats_meta(const at::Tensor& x, const std::optional<at::Tensor>&, 
   return at::empty({x.numel() / std::max<int64_t>(x.size(-1), 1), 2}, x.options().dtype(at::kFloat));
 }
 
+// (mean, rstd) per row from [rows, nc, 2] per-64-chunk (mean, M2) partials (linear3_stats)
+at::Tensor ln_stats_merge_cpu(const at::Tensor& part, double eps) {
+  TORCH_CHECK(part.dim() == 3 && part.size(2) == 2, "amd_dft.ln_stats_merge: part must be [rows, chunks, 2]");
+  at::Tensor p = part.to(at::kFloat);
+  at::Tensor m = p.select(2, 0), q = p.select(2, 1);
+  at::Tensor mean = m.mean(1);
+  at::Tensor m2 = q.sum(1) + 64.0 * (m - mean.unsqueeze(1)).pow(2).sum(1);
+  return at::stack({mean, at::rsqrt(m2 / (64.0 * p.size(1)) + eps)}, 1).contiguous();
+}
+
+at::Tensor ln_stats_merge_cuda(const at::Tensor& part_, double eps) {
+  const c10::DeviceGuard guard(part_.device());
+  TORCH_CHECK(part_.dim() == 3 && part_.size(2) == 2 && part_.scalar_type() == at::kFloat,
+              "amd_dft.ln_stats_merge: part must be fp32 [rows, chunks, 2]");
+  at::Tensor part = part_.contiguous();
+  at::Tensor st = at::empty({part.size(0), 2}, part.options());
+  launch_ln_stats_merge(part.data_ptr<float>(), st.data_ptr<float>(), part.size(0), static_cast<int>(part.size(1)), 64,
+                        static_cast<float>(eps), c10::hip::getCurrentHIPStream(part.device().index()).stream());
+  return checked(st, "ln_stats_merge");
+}
+
+at::Tensor ln_stats_merge_meta(const at::Tensor& part, double) { return at::empty({part.size(0), 2}, part.options()); }
+
 at::Tensor afno_spectral_meta(const at::Tensor& xw, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                               const at::Tensor&, double) {
   return at::empty_like(xw);
@@ -468,6 +491,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral_shapes() -> int[]", &amd_dft::afno_spectral_shape_list);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
+  m.def("ln_stats_merge(Tensor part, float eps=1e-6) -> Tensor");
   m.def("layer_norm_split(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? pre=None) -> Tensor");
   m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
@@ -478,6 +502,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cuda));
   m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cuda));
   m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cuda));
+  m.impl("ln_stats_merge", AMD_DFT_TRACED("amd_dft::ln_stats_merge", amd_dft::ln_stats_merge_cuda));
   m.impl("layer_norm_split", AMD_DFT_TRACED("amd_dft::layer_norm_split", amd_dft::layer_norm_split_cuda));
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cuda));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cuda));
@@ -488,6 +513,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("afno_spectral", AMD_DFT_TRACED("amd_dft::afno_spectral", amd_dft::afno_spectral_cpu));
   m.impl("layer_norm", AMD_DFT_TRACED("amd_dft::layer_norm", amd_dft::layer_norm_cpu));
   m.impl("ln_stats", AMD_DFT_TRACED("amd_dft::ln_stats", amd_dft::ln_stats_cpu));
+  m.impl("ln_stats_merge", AMD_DFT_TRACED("amd_dft::ln_stats_merge", amd_dft::ln_stats_merge_cpu));
   m.impl("layer_norm_split", AMD_DFT_TRACED("amd_dft::layer_norm_split", amd_dft::layer_norm_split_cpu));
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cpu));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cpu));
@@ -498,6 +524,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("afno_spectral", &amd_dft::afno_spectral_meta);
   m.impl("layer_norm", &amd_dft::layer_norm_meta);
   m.impl("ln_stats", &amd_dft::ln_stats_meta);
+  m.impl("ln_stats_merge", &amd_dft::ln_stats_merge_meta);
   m.impl("layer_norm_split", &amd_dft::layer_norm_split_meta);
   m.impl("fno_mix", &amd_dft::fno_mix_meta);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);

@@ -474,6 +474,37 @@ __global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict
 
 }  // namespace
 
+// (mean, rstd) per row from per-chunk partials (mean_c, M2_c) of equal chunk width W (Chan et al.:
+// mean = avg mean_c, M2 = sum M2_c + W sum (mean_c - mean)^2): the statistics the fp32 fc2 GEMM
+// epilogue leaves for the next block's LayerNorm (csrc/nn/gemm.hip, STATS)
+__global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __restrict__ part, float2* __restrict__ st,
+                                                             int64_t rows, int nc, float width, float eps) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= rows) return;
+  const float2* pp = part + t * nc;
+  float s = 0.f;
+  for (int c = 0; c < nc; ++c) s += pp[c].x;
+  const float mean = s / static_cast<float>(nc);
+  float m2 = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float2 q = pp[c];
+    const float d = q.x - mean;
+    m2 += fmaf(width * d, d, q.y);
+  }
+  st[t] = make_float2(mean, rsqrtf(m2 / (width * static_cast<float>(nc)) + eps));
+}
+
+void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream) {
+  if (rows <= 0) return;
+  if (nc <= 0 || width <= 0) throw std::runtime_error("amd_dft: ln_stats_merge: bad chunking");
+  const dim3 grid(static_cast<uint32_t>((rows + 255) / 256));
+  hipLaunchKernelGGL(ln_stats_merge_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const float2*>(part), reinterpret_cast<float2*>(stats), rows, nc,
+                     static_cast<float>(width), eps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ln_stats_merge launch: ") + hipGetErrorString(e));
+}
+
 void launch_ln_stats(const LnStatsLaunch& p, void* stream) {
   if (p.f32) {
     if (p.cols % 4 != 0 || p.cols > 64 * 4 * 8) throw std::runtime_error("amd_dft: ln_stats: fp32 rows need cols % 4 == 0, <= 2048");

@@ -180,7 +180,7 @@ class Block(nn.Module):
             from ..ops import spectral as S
 
             x, y = S.afno_block_amd(self, x)
-            return x + y
+            return x + S.pending_bias(y)
         residual = x
         x = self.filter(self.norm1(x))
         x = x + residual  # double skip
@@ -243,6 +243,7 @@ class AFNONet(nn.Module):
                 with trace_range(f"afno.block{i}"):
                     t, pending = S.afno_block_amd(blk, t, pending)
             hb = None
+            pending = S.pending_bias(pending)  # the head needs no LayerNorm statistics
             if pending is not None and pending.dim() == 1:
                 # per-channel residual bias left by the LN-fused blocks: folded into the
                 # head GEMM's bias, head(t + p) = head(t) + W_head p

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Callable, Optional, Sequence, Tuple
+from typing import Callable, NamedTuple, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -33,7 +33,7 @@ from . import dft as D
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
            "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
            "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
-           "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16"]
+           "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16", "LnCarry", "pending_bias"]
 
 
 def _ops():
@@ -167,19 +167,35 @@ def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
     return F.gelu(F.linear(y2, fc.weight, fc.bias))
 
 
-def afno_block_amd(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
+class LnCarry(NamedTuple):
+    """A per-channel pending bias plus the next LayerNorm's statistics of ``x + bias`` as
+    per-64-channel partials (``linear3_stats``), carried from one fp32 block to the next."""
+    bias: torch.Tensor
+    part: torch.Tensor
+
+
+def pending_bias(pending):
+    """The residual-stream tensor part of a block's ``pending`` (drops carried statistics)."""
+    return pending.bias if isinstance(pending, LnCarry) else pending
+
+
+def afno_block_amd(blk, x: torch.Tensor, pending=None):
     """One FourCastNet block on the MI355X path.
 
     Residual-stream fusion: the block returns ``(x, p)`` with the true block output being
     ``x + p``.  ``p`` is either a per-channel vector (the fc2 bias; LayerNorm-fused paths, see
-    :func:`afno_block_fused` / :func:`afno_block_fused_f32`) or a full tensor (the fc2 output;
+    :func:`afno_block_fused` / :func:`afno_block_fused_f32`), an :class:`LnCarry` (that vector
+    plus the next LayerNorm's partial statistics, fp32 path), or a full tensor (the fc2 output;
     generic path, where the addition is fused into the next block's LN1).
     """
+    part = None
+    if isinstance(pending, LnCarry):
+        pending, part = pending.bias, pending.part
     if pending is not None and pending.dim() == 1 and not _ln_fused_ok(blk, x):
-        x, pending = x + pending, None
+        x, pending, part = x + pending, None, None
     if (pending is None or pending.dim() == 1) and _ln_fused_ok(blk, x):
         if x.dtype == torch.float32:
-            return afno_block_fused_f32(blk, x, pending)
+            return afno_block_fused_f32(blk, x, pending, part)
         return afno_block_fused(blk, x, pending)
     x, yn = afno_block_spectral(blk, x, pending)
     return x, afno_block_mlp(blk, yn)
@@ -282,7 +298,7 @@ def _ln_folded_fc(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
                          build)
 
 
-def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
+def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None):
     """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
 
       stats = (mean, rstd) of x                  ln_stats (fp32 rows)
@@ -291,9 +307,13 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
       x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32
       yn    = split(LN2(x1))                     layer_norm_split: [hi | lo] bf16 pair rows
       h     = split(GELU(yn W1^T + b1))          bf16x3 GEMM, erf GELU, split-pair epilogue
-      x1    = x1 + h W2^T                        bf16x3 GEMM, fp32 residual epilogue
+      x1    = x1 + h W2^T                        bf16x3 GEMM, fp32 residual epilogue, which also
+                                                 emits the next LN1's statistics of x1 + b2 as
+                                                 per-64-channel partials (no ln_stats pass over x1
+                                                 in the next block: ln_stats_merge, 50 MB)
 
-    Returns (x1, fc2.bias) like :func:`afno_block_fused`."""
+    ``part``: those partials from the previous block (else ln_stats runs).  Returns
+    (x1, LnCarry(fc2.bias, partials))."""
     from ..models.afno import kept_window
 
     f = blk.filter
@@ -306,7 +326,10 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     pre32 = None if pre is None else _f32(blk, "pre", pre)
     g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
     dup = _DUP  # diagnostic (MI_DFT_DUP): run one stage twice to measure its in-step marginal cost
-    stats = ops.ln_stats(xs, pre32, n1.eps)
+    if part is not None and os.environ.get("MI_DFT_FC2_STATS", "1") != "0":
+        stats = ops.ln_stats_merge(part, n1.eps)
+    else:
+        stats = ops.ln_stats(xs, pre32, n1.eps)
     if dup == "ln_stats":
         stats = ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
@@ -327,10 +350,11 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     hid = ops.linear3(yn, w1s, b1, 1, None, True)
     if dup == "fc1":
         hid = ops.linear3(yn, w1s, b1, 1, None, True)
-    x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
+    b2 = _f32(m, "fc2_b", m.fc2.bias)
+    x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
     if dup == "fc2":
-        x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
-    return x1, m.fc2.bias
+        x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
+    return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
 
 
 _DUP = os.environ.get("MI_DFT_DUP", "")

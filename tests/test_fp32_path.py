@@ -63,6 +63,29 @@ def test_linear3_cpu_semantics():
     assert rel_l2(unsplit_bf16(ys), F.linear(x, w, b)) < 3e-5
 
 
+def _ln_stats_ref(y, pre=None):
+    v = y.double() + (0 if pre is None else pre.double())
+    return torch.stack([v.mean(-1), torch.rsqrt(v.var(-1, unbiased=False) + 1e-6)], -1).float()
+
+
+def test_linear3_stats_cpu_semantics():
+    """fc2 + residual with the next LayerNorm's per-64-channel partial statistics; merged they
+    equal ln_stats of (output + pre)."""
+    torch.manual_seed(3)
+    x, w, r, pre = torch.randn(37, 128), torch.randn(256, 128) * 0.1, torch.randn(37, 256), torch.randn(256)
+    y, part = ops.linear3_stats(ops.split_bf16(x, True), ops.split_bf16(w, True), r, pre)
+    assert part.shape == (37, 4, 2)
+    assert rel_l2(y, F.linear(x, w) + r) < 3e-5
+    st = ops.ln_stats_merge(part, 1e-6)
+    assert torch.allclose(st, ops.ln_stats(y, pre, 1e-6), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(st, _ln_stats_ref(y, pre), rtol=1e-5, atol=1e-6)
+    m = torch.empty(5, 768, device="meta")
+    assert ops.ln_stats_merge(torch.empty(5, 12, 2, device="meta")).shape == (5, 2)
+    yo, po = ops.linear3_stats(torch.empty(5, 6144, device="meta", dtype=torch.bfloat16),
+                               torch.empty(768, 6144, device="meta", dtype=torch.bfloat16), m)
+    assert yo.shape == (5, 768) and po.shape == (5, 12, 2)
+
+
 def test_linear3_rejects_bad_bias():
     xs = torch.zeros(4, 128, dtype=torch.bfloat16)
     ws = torch.zeros(256, 128, dtype=torch.bfloat16)
@@ -126,6 +149,24 @@ def test_linear3_gpu_vs_fp32(device, M, N, K, act, bias, res, split_out):
     else:
         assert y.shape == (M, N) and y.dtype == torch.float32
     assert rel_l2(y.cpu(), ref) < 2e-5  # bf16x3: ~5e-6 (bf16 alone: ~3e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,with_pre", [(777, 768, 3072, True), (300, 256, 64, False), (1, 512, 128, True)])
+def test_linear3_stats_gpu(device, M, N, K, with_pre):
+    """The fc2 epilogue's LayerNorm partials (DPP row reductions over 16 lanes) merged by
+    ln_stats_merge match an fp64 LayerNorm-statistics reference of the output + pre."""
+    torch.manual_seed(M + N + K)
+    x, w, r = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(M, N) * 3 + 1
+    pre = torch.randn(N) * 0.5 if with_pre else None
+    y, part = ops.linear3_stats(ops.split_bf16(x.to(device), True), ops.split_bf16(w.to(device), True), r.to(device),
+                                None if pre is None else pre.to(device))
+    assert part.shape == (M, N // 64, 2)
+    assert rel_l2(y.cpu(), F.linear(x, w) + r) < 2e-5
+    st = ops.ln_stats_merge(part, 1e-6).cpu()
+    ref = _ln_stats_ref(y.cpu(), pre)
+    assert torch.allclose(st, ref, rtol=2e-5, atol=2e-6), (st - ref).abs().max()
+    assert torch.allclose(st, ops.ln_stats(y, None if pre is None else pre.to(device), 1e-6).cpu(), rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.gpu
