@@ -29,7 +29,11 @@
 #include "dft_gemm.h"
 
 #ifndef FNO_EPI_STAGED
-#define FNO_EPI_STAGED 1  // output through a per-wave LDS tile in full-line stores (0: straight from the MFMA layout)
+// 1: output through a per-wave LDS tile in 64-byte row pieces; 0 (default): straight from the MFMA
+// layout.  Measured slower staged (profiles/fno_epilogue_r3.txt: FNO block bf16 61.7-62.3 vs
+// 59.2-59.6 us, fp32 89.5-92.5 vs 84.4 us, ABAB on one box): the block is latency-bound, and the
+// staging adds an LDS round trip and a wave barrier per tile for no store-efficiency gain.
+#define FNO_EPI_STAGED 0
 #endif
 
 namespace amd_dft {
