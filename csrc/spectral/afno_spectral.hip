@@ -19,9 +19,13 @@
 // vectorizer changes no LDS or global access at all -- only the kernel-argument scalar loads
 // (merged into s_load_dwordx4/x8, one moved into a conditional block) and the schedule.  The
 // cause is therefore a code-generation difference outside the memory operations, not a data
-// race in this source; the vectorizer stays off for this file, the determinism screen
-// (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids, and
-// MI_DFT_DEVICE_CHECKS builds check every 16-byte staging access for alignment and bounds.
+// race in this source.  Two further leads were tested and refuted: an MI_DFT_DEVICE_CHECKS build
+// with the vectorizer on (every 16-byte fp32 staging access checked for alignment and bounds)
+// reproduces the errors without a single failed check, and the vectorizer-on code with every
+// v_swap_b32 (the one instruction it adds that no exact kernel here contains) rewritten as a
+// three-XOR swap still fails (scripts/diag/afno_swap_xor.sh).  The vectorizer stays off for this
+// file, the determinism screen (tests/test_determinism_gpu.py) runs every kernel family at
+// co-resident grids, and MI_DFT_DEVICE_CHECKS builds check every 16-byte staging access.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
@@ -79,6 +83,16 @@ __device__ __forceinline__ void diag_guard() {
 #ifndef AFNO_ABLATE
 #define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs,
                        // 4 = x3 GEMM B fragments of k-step 0 reused (no weight loads after the first)
+#endif
+
+#ifdef AFNO_STAMPS
+// phase clocks (bench/afno_stamps.hip): thread 0 of each workgroup records s_memtime after every
+// phase barrier of the bf16x3 kernel (slot 0 / 11: s_memrealtime at entry / exit, 12: s_memtime at exit; 16 per workgroup)
+__device__ long long* g_afno_stamps;
+#define AFNO_STAMP(slot, v) \
+  do { if (threadIdx.x == 0) g_afno_stamps[static_cast<int64_t>(blockIdx.x) * 16 + (slot)] = static_cast<long long>(v); } while (0)
+#else
+#define AFNO_STAMP(slot, v) do { } while (0)
 #endif
 
 // Compile-time geometry of one instance: H = L = R0 x R1, block size BS.
@@ -439,8 +453,25 @@ __device__ __forceinline__ void put_split2(uint16_t* Ahi, uint16_t* Alo, int idx
       (static_cast<uint32_t>(f2bf16(b - __uint_as_float(static_cast<uint32_t>(hb) << 16))) << 16);
 }
 
+// four consecutive values (8-byte aligned idx) as bf16 hi / lo pieces
+__device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx, float a, float b, float c, float d) {
+  const uint16_t ha = f2bf16(a), hb = f2bf16(b), hc = f2bf16(c), hd = f2bf16(d);
+  const auto up = [](uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); };
+  *reinterpret_cast<uint2*>(Ahi + idx) = make_uint2(static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16),
+                                                    static_cast<uint32_t>(hc) | (static_cast<uint32_t>(hd) << 16));
+  *reinterpret_cast<uint2*>(Alo + idx) =
+      make_uint2(static_cast<uint32_t>(f2bf16(a - up(ha))) | (static_cast<uint32_t>(f2bf16(b - up(hb))) << 16),
+                 static_cast<uint32_t>(f2bf16(c - up(hc))) | (static_cast<uint32_t>(f2bf16(d - up(hd))) << 16));
+}
+
 // [16 MT x 2BS] = (Ah + Al) x (Bh + Bl)^T without Al.Bl; wave w owns column tiles NTW w ..
-template <class S>
+// TR: the same products with the MFMA operands swapped, so the accumulator tile is the transpose:
+// a lane holds 4 CONSECUTIVE output columns n of one row m (instead of 4 rows of one column) --
+// the epilogue then writes 8-byte bf16x4 pieces instead of single bf16 values.
+#ifndef AFNO_X3_T
+#define AFNO_X3_T 1
+#endif
+template <class S, bool TR = false>
 __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
                                              const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
   constexpr int K2 = 2 * S::K;  // split weight row: k32-interleaved [hi(32) | lo(32)] chunks
@@ -488,9 +519,15 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
                          __builtin_bit_cast(f32x4, ah) + __builtin_bit_cast(f32x4, bl[ks % NQ][nj]);
           continue;
         }
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
-        acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+        if constexpr (TR) {
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ks % NQ][nj], al, acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ks % NQ][nj], ah, acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ks % NQ][nj], ah, acc[mi][nj], 0, 0, 0);
+        } else {
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
+        }
       }
     }
     if constexpr (AFNO_DIAG & 1) diag_guard();
@@ -500,6 +537,8 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
 
 template <class S>
 __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs a) {
+  AFNO_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  AFNO_STAMP(1, __builtin_amdgcn_s_memtime());
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
   constexpr int64_t LDSB = (2LL * L * BS * 4 > 4LL * plane) ? 2LL * L * BS * 4 : 4LL * plane;  // == make_instance lds_x3
@@ -546,6 +585,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
   }
   __syncthreads();
+  AFNO_STAMP(2, __builtin_amdgcn_s_memtime());
   // ---------------- pass 1: LDS -> registers -> A planes ([h][re 0..BS-1 | im BS..2BS-1], hi / lo)
   {
     cpair v[P1::Q][R1];
@@ -559,6 +599,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       }
     }
     __syncthreads();
+    AFNO_STAMP(3, __builtin_amdgcn_s_memtime());
     h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
@@ -576,29 +617,44 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   }
   // rows L..16 MT - 1 of A (GEMM M padding) are never written: their outputs are discarded
   __syncthreads();
+  AFNO_STAMP(4, __builtin_amdgcn_s_memtime());
   const int lane = tid & 63, w = tid >> 6;
   const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * 2 * K;
   const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * 2 * K;
   const float* b1 = a.b1 + blk * K;
   const float* b2 = a.b2 + blk * K;
   f32x4 acc[S::MT][S::NTW];
-  gemm_tile_x3<S>(Ah, Al, w1t, acc);
+  gemm_tile_x3<S, AFNO_X3_T>(Ah, Al, w1t, acc);
   __syncthreads();
+  AFNO_STAMP(5, __builtin_amdgcn_s_memtime());
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
-    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
-    const float bias = b1[n];
+    if constexpr (AFNO_X3_T) {  // lane: columns n0 .. n0 + 3 of row m -> one 8-byte piece per plane
+      const int n0 = (S::NTW * w + nj) * 16 + 4 * (lane >> 4);
+      const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mi * 16 + 4 * (lane >> 4) + i;
-        put_split(Ah, Al, m * AP + n, fmaxf(acc[mi][nj][i] + bias, 0.f));
+      for (int mi = 0; mi < S::MT; ++mi) {
+        const int m = mi * 16 + (lane & 15);
+        put_split4(Ah, Al, m * AP + n0, fmaxf(acc[mi][nj][0] + bias.x, 0.f), fmaxf(acc[mi][nj][1] + bias.y, 0.f),
+                   fmaxf(acc[mi][nj][2] + bias.z, 0.f), fmaxf(acc[mi][nj][3] + bias.w, 0.f));
       }
+    } else {
+      const int n = (S::NTW * w + nj) * 16 + (lane & 15);
+      const float bias = b1[n];
+#pragma unroll
+      for (int mi = 0; mi < S::MT; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mi * 16 + 4 * (lane >> 4) + i;
+          put_split(Ah, Al, m * AP + n, fmaxf(acc[mi][nj][i] + bias, 0.f));
+        }
+    }
   }
   __syncthreads();
+  AFNO_STAMP(6, __builtin_amdgcn_s_memtime());
   gemm_tile_x3<S>(Ah, Al, w2t, acc);
   __syncthreads();
+  AFNO_STAMP(7, __builtin_amdgcn_s_memtime());
   float* X = reinterpret_cast<float*>(ldsf);
   const float lam = a.lambda;
 #pragma unroll
@@ -621,6 +677,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       }
   }
   __syncthreads();
+  AFNO_STAMP(8, __builtin_amdgcn_s_memtime());
   // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
   {
     cpair v[P0::Q][R0];
@@ -634,6 +691,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       }
     }
     __syncthreads();
+    AFNO_STAMP(9, __builtin_amdgcn_s_memtime());
     h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
@@ -646,6 +704,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
   }
   __syncthreads();
+  AFNO_STAMP(10, __builtin_amdgcn_s_memtime());
   // ---------------- pass 1: LDS -> registers -> global (conj back)
   {
     cpair v[P1::Q][R1];
@@ -673,6 +732,8 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       }
     }
   }
+  AFNO_STAMP(12, __builtin_amdgcn_s_memtime());
+  AFNO_STAMP(11, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------ instance table

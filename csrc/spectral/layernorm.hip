@@ -6,6 +6,8 @@
 // (saves a separate elementwise kernel and one read of x).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cstdlib>
 
 #include <stdexcept>
@@ -477,11 +479,21 @@ __global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict
 // (mean, rstd) per row from per-chunk partials (mean_c, M2_c) of equal chunk width W (Chan et al.:
 // mean = avg mean_c, M2 = sum M2_c + W sum (mean_c - mean)^2): the statistics the fp32 fc2 GEMM
 // epilogue leaves for the next block's LayerNorm (csrc/nn/gemm.hip, STATS)
+// 256 rows per workgroup: the block's partials ([256][nc] float2, contiguous) are staged in LDS
+// with coalesced 16-byte loads, then every thread merges its own row (Chan: M2 = sum M2_c +
+// width * sum (mean_c - mean)^2)
+constexpr int kMergeMaxNc = 64;  // dynamic LDS 2 KB per chunk: <= 128 KB
 __global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __restrict__ part, float2* __restrict__ st,
                                                              int64_t rows, int nc, float width, float eps) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (t >= rows) return;
-  const float2* pp = part + t * nc;
+  extern __shared__ float4 tile[];  // [256 rows][nc] float2
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * 256;
+  const int nrow = static_cast<int>(rows - r0 < 256 ? rows - r0 : 256);
+  const int n4 = nrow * nc / 2;  // nc is even (checked on the host)
+  const float4* src = reinterpret_cast<const float4*>(part + r0 * nc);
+  for (int i = threadIdx.x; i < n4; i += 256) tile[i] = src[i];
+  __syncthreads();
+  if (static_cast<int>(threadIdx.x) >= nrow) return;
+  const float2* pp = reinterpret_cast<const float2*>(tile) + threadIdx.x * nc;
   float s = 0.f;
   for (int c = 0; c < nc; ++c) s += pp[c].x;
   const float mean = s / static_cast<float>(nc);
@@ -491,14 +503,27 @@ __global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __res
     const float d = q.x - mean;
     m2 += fmaf(width * d, d, q.y);
   }
-  st[t] = make_float2(mean, rsqrtf(m2 / (width * static_cast<float>(nc)) + eps));
+  st[r0 + threadIdx.x] = make_float2(mean, rsqrtf(m2 / (width * static_cast<float>(nc)) + eps));
 }
 
 void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream) {
   if (rows <= 0) return;
-  if (nc <= 0 || width <= 0) throw std::runtime_error("amd_dft: ln_stats_merge: bad chunking");
+  if (nc <= 0 || nc % 2 || nc > kMergeMaxNc || width <= 0)
+    throw std::runtime_error("amd_dft: ln_stats_merge: needs an even chunk count <= 64");
   const dim3 grid(static_cast<uint32_t>((rows + 255) / 256));
-  hipLaunchKernelGGL(ln_stats_merge_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+  const int lds = 256 * nc * 8;
+  if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (per device, like the GEMM's)
+    static std::atomic<uint64_t> attr_done{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("amd_dft: ln_stats_merge: bad device");
+    if (!(attr_done.load(std::memory_order_acquire) & (uint64_t(1) << dev))) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ln_stats_merge_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 256 * kMergeMaxNc * 8);
+      if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ln_stats_merge attr: ") + hipGetErrorString(e));
+      attr_done.fetch_or(uint64_t(1) << dev, std::memory_order_acq_rel);
+    }
+  }
+  hipLaunchKernelGGL(ln_stats_merge_kernel, grid, dim3(256), lds, static_cast<hipStream_t>(stream),
                      reinterpret_cast<const float2*>(part), reinterpret_cast<float2*>(stats), rows, nc,
                      static_cast<float>(width), eps);
   hipError_t e = hipGetLastError();

@@ -350,6 +350,9 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     hid = ops.linear3(yn, w1s, b1, 1, None, True)
     if dup == "fc1":
         hid = ops.linear3(yn, w1s, b1, 1, None, True)
+    if C > 64 * 64:  # ln_stats_merge takes <= 64 chunks of 64 channels
+        x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
+        return x1, m.fc2.bias
     b2 = _f32(m, "fc2_b", m.fc2.bias)
     x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
     if dup == "fc2":
