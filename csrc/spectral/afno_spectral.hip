@@ -106,6 +106,13 @@ struct AfnoShape {
   static constexpr int NTW = BS / 32;     // 16-wide column tiles per wave (2BS / 16 over 4 waves)
   static constexpr int KS = BS / 16;      // 32-deep k-steps
   static constexpr int OCC = BS <= 96 ? 3 : 2;  // workgroups per SIMD the bf16 register budget targets
+  // dynamic LDS: the FFT staging / GEMM A tile(s) (bf16 kernel: fp16 staging | one bf16 plane;
+  // x3: fp32 staging | hi + lo planes), then the pass-1 twiddles (TWN float2, copied from the plan
+  // table at kernel start: an LDS read instead of an L2 round trip after each pass-1 barrier)
+  static constexpr int TWN = (R1 - 1) * R0;
+  static constexpr int64_t MAIN16 = L * BS * 4 > 32 * MT * APitch ? L * BS * 4 : 32 * MT * APitch;
+  static constexpr int64_t MAIN32 = 2 * L * BS * 4 > 64 * MT * APitch ? 2 * L * BS * 4 : 64 * MT * APitch;
+  static constexpr int64_t LDS16 = MAIN16 + TWN * 8, LDS32 = MAIN32 + TWN * 8;
   static_assert(R0 * R1 == L && BS % 32 == 0 && L <= 128, "AFNO instance geometry");
 };
 
@@ -245,7 +252,9 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   extern __shared__ __attribute__((aligned(16))) h2_t lds[];  // [L][BS] complex fp16
   uint16_t* A = reinterpret_cast<uint16_t*>(lds);             // aliases lds: [16 MT][APitch] bf16
+  float2* twl = reinterpret_cast<float2*>(reinterpret_cast<char*>(lds) + S::MAIN16);
   const int tid = threadIdx.x;
+  for (int i = tid; i < S::TWN; i += kNT) twl[i] = a.tw[i];  // visible after the pass-0 barrier
   const int blk = blockIdx.x % a.NB;
   const int bk = blockIdx.x / a.NB;  // b * KM + kw
   const int kw = bk % a.KM;
@@ -274,7 +283,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         v[q][r] = make_cpair(c0, c1);
       }
     }
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -299,7 +308,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -377,7 +386,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
       }
     }
     __syncthreads();
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -401,7 +410,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -541,11 +550,14 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   AFNO_STAMP(1, __builtin_amdgcn_s_memtime());
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
-  constexpr int64_t LDSB = (2LL * L * BS * 4 > 4LL * plane) ? 2LL * L * BS * 4 : 4LL * plane;  // == make_instance lds_x3
+  constexpr int64_t LDSB = S::MAIN32;  // the staging / A-plane area (twiddles follow it)
+  static_assert(S::MAIN32 == ((2LL * L * BS * 4 > 4LL * plane) ? 2LL * L * BS * 4 : 4LL * plane), "x3 LDS layout");
   extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][BS] complex fp32
   uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [16 MT][APitch] bf16 hi
   uint16_t* Al = Ah + plane;                                     //          [16 MT][APitch] bf16 lo
+  float2* twl = reinterpret_cast<float2*>(reinterpret_cast<char*>(ldsf) + S::MAIN32);
   const int tid = threadIdx.x;
+  for (int i = tid; i < S::TWN; i += kNT) twl[i] = a.tw[i];  // visible after the pass-0 barrier
   const int blk = blockIdx.x % a.NB;
   const int bk = blockIdx.x / a.NB;
   const int kw = bk % a.KM;
@@ -573,7 +585,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         v[q][r] = make_cpair(c0, c1);
       }
     }
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -600,7 +612,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
     __syncthreads();
     AFNO_STAMP(3, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -692,7 +704,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
     __syncthreads();
     AFNO_STAMP(9, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, a.tw);
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -717,7 +729,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, a.tw);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -760,9 +772,7 @@ struct AfnoInstance {
 
 template <class S>
 AfnoInstance make_instance() {
-  constexpr int64_t plane = 16LL * S::MT * S::APitch * 2;  // bytes of one bf16 A tile
-  constexpr int64_t st16 = static_cast<int64_t>(S::L) * S::BS * 4, st32 = 2 * st16;
-  AfnoInstance r{S::L, S::R0, S::R1, S::BS, st16 > plane ? st16 : plane, st32 > 2 * plane ? st32 : 2 * plane,
+  AfnoInstance r{S::L, S::R0, S::R1, S::BS, S::LDS16, S::LDS32,
                  {{afno_spectral_kernel<S, false, false>, afno_spectral_kernel<S, false, true>},
                   {afno_spectral_kernel<S, true, false>, afno_spectral_kernel<S, true, true>}},
                  afno_spectral_x3_kernel<S>};
