@@ -286,9 +286,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     }
     return out_off(i, j);
   };
-  typedef typename std::conditional<OUT == 1, float4, uint2>::type ResT;
+  typedef typename std::conditional<OUT != 0, float4, uint2>::type ResT;  // split modes: fp32 residual
   auto load_res = [&](int i, int j) -> ResT {
-    if constexpr (OUT == 1) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + res_off(i, j));
+    if constexpr (OUT != 0) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + res_off(i, j));
     else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + res_off(i, j));
   };
   f32x4 acc[8][4];
@@ -431,7 +431,10 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       constexpr int RPI = 64 / LPR;             // rows per pass
       constexpr int NIT = 64 / RPI;             // passes per half
       const int c = lane % LPR, rsub = lane / LPR;
-      typedef typename std::conditional<OUT == 1, float4, uint4>::type RT;
+      // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32 (the hi and the lo
+      // lane of a feature group both load it)
+      struct F8 { float4 a, b; };
+      typedef typename std::conditional<OUT == 1, float4, typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
@@ -443,9 +446,15 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             if constexpr (MODE == 1) {
               if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
             }
-            const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
-            if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
-            else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+            if constexpr (OUT == 2) {
+              const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
+              const float* rp = static_cast<const float*>(p.residual) + o;
+              rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
+            } else {
+              const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
+              if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
+              else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+            }
           }
         }
 #pragma unroll
@@ -491,6 +500,12 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             const float4 u0 = *reinterpret_cast<const float4*>(rp + (((fl >> 2) ^ (row & 15)) << 4));
             const float4 u1 = *reinterpret_cast<const float4*>(rp + ((((fl >> 2) + 1) ^ (row & 15)) << 4));
             float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+            if constexpr (OUT == 2 && RES) {
+              const float r8[8] = {rr[it].a.x, rr[it].a.y, rr[it].a.z, rr[it].a.w,
+                                   rr[it].b.x, rr[it].b.y, rr[it].b.z, rr[it].b.w};
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] += r8[k];
+            }
             if constexpr (OUT == 0 && RES) {
               const uint32_t rw[4] = {rr[it].x, rr[it].y, rr[it].z, rr[it].w};
 #pragma unroll
@@ -557,7 +572,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         float v[4] = {vp[0].x, vp[0].y, vp[1].x, vp[1].y};
         if constexpr (ERES) {
           const ResT rr = rq[ip & 1][ii][j];
-          if constexpr (OUT == 1) {  // fp32 residual (in place allowed: same lane reads, then writes)
+          if constexpr (OUT != 0) {  // fp32 residual (in place allowed: same lane reads, then writes)
             v[0] += rr.x;
             v[1] += rr.y;
             v[2] += rr.z;
@@ -623,7 +638,14 @@ void launch_res(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 template <int ACT, bool BIAS>
 void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   if (p.out == 2) {
-    if (p.residual) throw std::runtime_error("amd_dft: gemm: split-pair output takes no residual");
+    if (p.residual) {  // last fp32 block: x + h W2^T straight to the head GEMM's split-pair operand
+      if constexpr (ACT == 0 && !BIAS) {
+        launch_one<0, false, true, false, 0, true, 2>(p, st, grid);
+      } else {
+        throw std::runtime_error("amd_dft: gemm: a split-pair output takes a residual only without activation and bias");
+      }
+      return;
+    }
     launch_one<ACT, BIAS, false, false, 0, true, 2>(p, st, grid);
   } else if (p.residual && p.stats_part) {  // fc2 of the fp32 block: + next LayerNorm's partial statistics
     if constexpr (ACT == 0 && !BIAS) {

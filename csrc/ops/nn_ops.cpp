@@ -405,8 +405,9 @@ at::Tensor linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10:
   const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
   TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0 (got N=",
               N, ", K=", K, ")");
-  TORCH_CHECK(!(split_out && residual.has_value() && residual->defined()),
-              "amd_dft.linear3: a split-pair output takes no residual");
+  TORCH_CHECK(!(split_out && residual.has_value() && residual->defined() &&
+                (act != 0 || (bias.has_value() && bias->defined()))),
+              "amd_dft.linear3: a split-pair output takes a residual only without activation and bias");
   at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
   std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
   os.back() = split_out ? 2 * N : N;

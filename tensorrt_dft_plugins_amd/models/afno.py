@@ -239,9 +239,10 @@ class AFNONet(nn.Module):
             from ..ops import spectral as S
 
             pending = None
+            nblk = len(self.blocks)
             for i, blk in enumerate(self.blocks):
                 with trace_range(f"afno.block{i}"):
-                    t, pending = S.afno_block_amd(blk, t, pending)
+                    t, pending = S.afno_block_amd(blk, t, pending, split_out=f32 and i == nblk - 1)
             hb = None
             pending = S.pending_bias(pending)  # the head needs no LayerNorm statistics
             if pending is not None and pending.dim() == 1:
@@ -252,11 +253,12 @@ class AFNONet(nn.Module):
                 t = t + pending
             # head GEMM (features permuted to (c_out, p1, p2)) with the un-patchify folded into its
             # output scatter
-            tt = t.reshape(-1, cfg.embed_dim)
             if f32:
                 hw = self._head_weight_cpp()
                 ws = S.module_cached(self, "head_split", (hw,), lambda: S.split_bf16(hw))
-                return torch.ops.amd_dft.linear_unpatch3(S.split_bf16(tt), ws, hb, cfg.out_chans, cfg.h, cfg.w, p)
+                ts = t.pairs if isinstance(t, S.SplitRows) else S.split_bf16(t.reshape(-1, cfg.embed_dim))
+                return torch.ops.amd_dft.linear_unpatch3(ts, ws, hb, cfg.out_chans, cfg.h, cfg.w, p)
+            tt = t.reshape(-1, cfg.embed_dim)
             return torch.ops.amd_dft.linear_unpatch(tt, self._head_weight_cpp(), hb, cfg.out_chans, cfg.h, cfg.w, p)
         for blk in self.blocks:
             t = blk(t)

@@ -33,7 +33,7 @@ from . import dft as D
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
            "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
            "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
-           "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16", "LnCarry", "pending_bias"]
+           "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16", "LnCarry", "pending_bias", "SplitRows"]
 
 
 def _ops():
@@ -174,12 +174,18 @@ class LnCarry(NamedTuple):
     part: torch.Tensor
 
 
+class SplitRows(NamedTuple):
+    """A block output already in the bf16x3 pair-row layout [tokens, 2C] (the last fp32 block
+    writes the head GEMM's operand straight from its fc2 epilogue)."""
+    pairs: torch.Tensor
+
+
 def pending_bias(pending):
     """The residual-stream tensor part of a block's ``pending`` (drops carried statistics)."""
     return pending.bias if isinstance(pending, LnCarry) else pending
 
 
-def afno_block_amd(blk, x: torch.Tensor, pending=None):
+def afno_block_amd(blk, x: torch.Tensor, pending=None, split_out: bool = False):
     """One FourCastNet block on the MI355X path.
 
     Residual-stream fusion: the block returns ``(x, p)`` with the true block output being
@@ -187,6 +193,8 @@ def afno_block_amd(blk, x: torch.Tensor, pending=None):
     :func:`afno_block_fused` / :func:`afno_block_fused_f32`), an :class:`LnCarry` (that vector
     plus the next LayerNorm's partial statistics, fp32 path), or a full tensor (the fc2 output;
     generic path, where the addition is fused into the next block's LN1).
+    ``split_out`` (last block before the fp32 head): the fp32 fused path may return its output as
+    :class:`SplitRows` instead of an fp32 tensor.
     """
     part = None
     if isinstance(pending, LnCarry):
@@ -195,7 +203,7 @@ def afno_block_amd(blk, x: torch.Tensor, pending=None):
         x, pending, part = x + pending, None, None
     if (pending is None or pending.dim() == 1) and _ln_fused_ok(blk, x):
         if x.dtype == torch.float32:
-            return afno_block_fused_f32(blk, x, pending, part)
+            return afno_block_fused_f32(blk, x, pending, part, split_out)
         return afno_block_fused(blk, x, pending)
     x, yn = afno_block_spectral(blk, x, pending)
     return x, afno_block_mlp(blk, yn)
@@ -298,7 +306,8 @@ def _ln_folded_fc(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
                          build)
 
 
-def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None):
+def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None,
+                         split_out: bool = False):
     """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
 
       stats = (mean, rstd) of x                  ln_stats (fp32 rows)
@@ -313,7 +322,8 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
                                                  in the next block: ln_stats_merge, 50 MB)
 
     ``part``: those partials from the previous block (else ln_stats runs).  Returns
-    (x1, LnCarry(fc2.bias, partials))."""
+    (x1, LnCarry(fc2.bias, partials)); with ``split_out`` (last block) fc2 writes x1 as bf16x3
+    pair rows for the head GEMM instead (no statistics, no separate split pass): (SplitRows, fc2.bias)."""
     from ..models.afno import kept_window
 
     f = blk.filter
@@ -350,6 +360,8 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     hid = ops.linear3(yn, w1s, b1, 1, None, True)
     if dup == "fc1":
         hid = ops.linear3(yn, w1s, b1, 1, None, True)
+    if split_out and os.environ.get("MI_DFT_HEAD_SPLIT", "1") != "0":
+        return SplitRows(ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), True)), m.fc2.bias
     if C > 64 * 64:  # ln_stats_merge takes <= 64 chunks of 64 channels
         x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
         return x1, m.fc2.bias

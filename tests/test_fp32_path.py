@@ -86,6 +86,14 @@ def test_linear3_stats_cpu_semantics():
     assert yo.shape == (5, 768) and po.shape == (5, 12, 2)
 
 
+def test_linear3_split_out_with_residual_cpu():
+    torch.manual_seed(5)
+    x, w, r = torch.randn(7, 128), torch.randn(256, 128) * 0.1, torch.randn(7, 256)
+    ys = ops.linear3(ops.split_bf16(x, True), ops.split_bf16(w, True), None, 0, r, True)
+    assert ys.shape == (7, 512) and ys.dtype == torch.bfloat16
+    assert rel_l2(unsplit_bf16(ys), F.linear(x, w) + r) < 3e-5
+
+
 def test_linear3_rejects_bad_bias():
     xs = torch.zeros(4, 128, dtype=torch.bfloat16)
     ws = torch.zeros(256, 128, dtype=torch.bfloat16)
@@ -128,6 +136,7 @@ def test_module_cache_follows_parameters():
     (777, 768, 3072, 0, False, True, False),   # fc2 + fp32 residual, ragged M
     (300, 256, 64, 0, True, False, False),
     (33, 512, 128, 1, True, True, False),
+    (777, 768, 3072, 0, False, True, True),    # last block's fc2: + fp32 residual -> split pair rows for the head
 ])
 def test_linear3_gpu_vs_fp32(device, M, N, K, act, bias, res, split_out):
     torch.manual_seed(M + N)
