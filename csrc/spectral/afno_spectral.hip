@@ -898,7 +898,12 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   if (p.x3) {
     if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
     // persistent grid: the resident workgroups (occupancy x CUs, a multiple of 8 NB when possible)
-    const int64_t res = resident_workgroups(in->x3, in->lds_x3);
+    // MI_DFT_AFNO_PERSIST=0 (A/B): one tile per workgroup (the input DMA is then waited for at once)
+    static const bool persist = [] {
+      const char* e = std::getenv("MI_DFT_AFNO_PERSIST");
+      return !(e && std::string(e) == "0");
+    }();
+    const int64_t res = persist ? resident_workgroups(in->x3, in->lds_x3) : nblocks;
     int64_t grid = std::min(nblocks, res);
     if (grid > 8 * p.NB) grid -= grid % (8 * p.NB);
     launch_kernel(in->x3, in->lds_x3, grid, a, stream);

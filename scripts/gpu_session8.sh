@@ -16,5 +16,8 @@ step s8_build_stamps 300 hipcc -O3 -mllvm -amdgpu-load-store-vectorizer=0 --offl
   -fno-slp-vectorize -DAFNO_STAMPS -Icsrc bench/afno_stamps.hip -o /tmp/afno_stamps || exit 1
 TAILN=14 step s8_afno_stamps 120 /tmp/afno_stamps
 TAILN=2 step s8_spec1 200 python -u bench/bench_afno_spec.py
+TAILN=2 step s8_spec1_np 200 env MI_DFT_AFNO_PERSIST=0 python -u bench/bench_afno_spec.py
 TAILN=2 step s8_spec2 200 python -u bench/bench_afno_spec.py
+TAILN=2 step s8_spec2_np 200 env MI_DFT_AFNO_PERSIST=0 python -u bench/bench_afno_spec.py
 TAILN=2 step s8_bench 600 python -u bench.py --steps 10 --warmup 3
+TAILN=2 step s8_bench_np 600 env MI_DFT_AFNO_PERSIST=0 python -u bench.py --steps 10 --warmup 3 --no-fft --extra-steps 0
