@@ -46,11 +46,8 @@
 // are discarded) and 2BS / 16 column tiles over the 4 waves.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
-#include <map>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -90,11 +87,10 @@ __device__ __forceinline__ void diag_guard() {
 
 #ifdef AFNO_STAMPS
 // phase clocks (bench/afno_stamps.hip): thread 0 of each workgroup records s_memtime after every
-// phase barrier of the bf16x3 kernel, per tile (slot 0 / 11: s_memrealtime at tile start / end, 12: s_memtime at
-// tile end; 16 per tile)
+// phase barrier of the bf16x3 kernel (slot 0 / 11: s_memrealtime at entry / exit, 12: s_memtime at exit; 16 per workgroup)
 __device__ long long* g_afno_stamps;
 #define AFNO_STAMP(slot, v) \
-  do { if (threadIdx.x == 0) g_afno_stamps[static_cast<int64_t>(afno_stamp_id) * 16 + (slot)] = static_cast<long long>(v); } while (0)
+  do { if (threadIdx.x == 0) g_afno_stamps[static_cast<int64_t>(blockIdx.x) * 16 + (slot)] = static_cast<long long>(v); } while (0)
 #else
 #define AFNO_STAMP(slot, v) do { } while (0)
 #endif
@@ -172,13 +168,13 @@ struct HPass {
 };
 
 template <int R, int L, int NP, int Ns, int Q>
-__device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw, int tid = threadIdx.x) {
+__device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
   using P = HPass<R, L, NP>;
   static_assert(P::Q == Q, "pass geometry");
   if constexpr (AFNO_ABLATE & 1) return;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
-    const int b = tid + q * kNT;
+    const int b = threadIdx.x + q * kNT;
     if (P::NB % kNT == 0 || b < P::NB) {
       const int j = b / NP;
       if constexpr (Ns > 1) {
@@ -204,7 +200,6 @@ struct AfnoArgs {
   const float2* tw;     // plan twiddles for length H ([R0, R1] order)
   int KM, C, NB, H;
   float lambda;
-  int ntiles;           // B * KM * NB (the x3 kernel is persistent: tiles blockIdx.x + k gridDim.x)
 };
 
 // GEMM [16 MT x 2BS] = A (LDS bf16, pitch APitch) x Bt^T (global bf16 [n][k]); wave w owns
@@ -487,11 +482,10 @@ __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx
 #endif
 template <class S, bool TR = false>
 __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
-                                             const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW],
-                                             int tid = threadIdx.x) {
+                                             const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
   constexpr int K2 = 2 * S::K;  // split weight row: k32-interleaved [hi(32) | lo(32)] chunks
-  const int lane = tid & 63;
-  const int w = tid >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int mi = 0; mi < S::MT; ++mi)
@@ -552,6 +546,8 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
 
 template <class S>
 __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs a) {
+  AFNO_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  AFNO_STAMP(1, __builtin_amdgcn_s_memtime());
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
   constexpr int64_t LDSB = S::MAIN32;  // the staging / A-plane area (twiddles follow it)
@@ -561,62 +557,35 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   uint16_t* Al = Ah + plane;                                     //          [16 MT][APitch] bf16 lo
   float2* twl = reinterpret_cast<float2*>(reinterpret_cast<char*>(ldsf) + S::MAIN32);
   const int tid = threadIdx.x;
-  for (int i = tid; i < S::TWN; i += kNT) twl[i] = a.tw[i];  // visible after the first pass-0 barrier
-  const int row_stride = a.KM * a.C * 2;
-  using P0 = HPass<R0, L, NP>;
-  using P1 = HPass<R1, L, NP>;
-  // Persistent: tiles blockIdx.x, blockIdx.x + gridDim.x, ... (grid = resident workgroups).  The
-  // next tile's input rows are DMA'd (global_load_lds, no VGPRs) into the staging area while this
-  // tile's last pass runs (it only reads registers and stores to global), so pass 0 starts from LDS
-  // instead of waiting for HBM.  With a grid that is a multiple of 8 x NB, every workgroup of one
-  // XCD works on one channel block (tile % NB), so that XCD's L2 holds one block's weights.
-  constexpr int ROWB = BS * 8;                       // bytes of one input row (BS complex fp32)
-  constexpr int NCH = (L * ROWB + 1023) / 1024;      // 1 KB DMA chunks (one wave instruction each)
-  static_assert(static_cast<int64_t>(NCH) * 1024 <= LDSB, "x3 input DMA must fit the staging area");
-  auto dma_pass0 = [&](int tile) {
-    const int bk = tile / a.NB;
-    const int64_t base = ((static_cast<int64_t>(bk / a.KM) * L * a.KM + bk % a.KM) * a.C + (tile % a.NB) * BS) * 2;
-    const char* xin = reinterpret_cast<const char*>(static_cast<const float*>(a.x) + base);
-    const int w = tid >> 6, lane = tid & 63;
-    for (int c = w; c < NCH; c += kNT / 64) {
-      const int o = min(c * 1024 + lane * 16, L * ROWB - 16);  // tail lanes: a valid address, bytes past the rows
-      const int row = o / ROWB, col = o - row * ROWB;
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(xin + static_cast<int64_t>(row) * row_stride * 4 + col),
-                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(ldsf) + c * 1024),
-                                       16, 0, 0);
-    }
-  };
-  if (static_cast<int>(blockIdx.x) < a.ntiles) dma_pass0(blockIdx.x);
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-  // the thread index laundered per tile: index / address arithmetic stays inside the loop instead
-  // of being hoisted and held in registers across it (that spilled the GEMM phases)
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  [[maybe_unused]] const int afno_stamp_id = tile;
-  AFNO_STAMP(0, __builtin_amdgcn_s_memrealtime());
-  AFNO_STAMP(1, __builtin_amdgcn_s_memtime());
-  const int blk = tile % a.NB;
-  const int bk = tile / a.NB;
+  for (int i = tid; i < S::TWN; i += kNT) twl[i] = a.tw[i];  // visible after the pass-0 barrier
+  const int blk = blockIdx.x % a.NB;
+  const int bk = blockIdx.x / a.NB;
   const int kw = bk % a.KM;
   const int b = bk / a.KM;
   AMD_DFT_DEV_CHECK((blk + 1) * BS <= a.C && kw < a.KM && L == a.H, "afno_spectral_x3_kernel");
+  const int row_stride = a.KM * a.C * 2;
   const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * BS) * 2;
+  const float* xin = static_cast<const float*>(a.x) + base;
   float* yout = static_cast<float*>(a.y) + base;
-  // ---------------- forward FFT_H: pass 0 on the DMA'd input rows (LDS -> registers -> LDS)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA chunks have landed
-  __syncthreads();                                   // ... and every other wave's
+  using P0 = HPass<R0, L, NP>;
+  using P1 = HPass<R1, L, NP>;
+  // ---------------- forward FFT_H: pass 0 straight from global
   {
     cpair v[P0::Q][R0];
 #pragma unroll
-    for (int q = 0; q < P0::Q; ++q) {  // unconditional (clamped item): no partially defined registers
+    for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
-      const int bc = (P0::NB % kNT == 0 || bb < P0::NB) ? bb : 0;
+      const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
+      const int bc = ok ? bb : 0;
       const int tp = bc % NP, j = bc / NP;
 #pragma unroll
-      for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * BS + 2 * tp);
+      for (int r = 0; r < R0; ++r) {
+        float2 c0, c1;
+        ldc2<false>(xin, (j + r * P0::LR) * row_stride + 4 * tp, c0, c1);
+        v[q][r] = make_cpair(c0, c1);
+      }
     }
-    __syncthreads();
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr, tid);  // first pass: no twiddles
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -633,16 +602,17 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   {
     cpair v[P1::Q][R1];
 #pragma unroll
-    for (int q = 0; q < P1::Q; ++q) {  // unconditional (clamped item): no partially defined registers
+    for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
-      const int bc = (P1::NB % kNT == 0 || bb < P1::NB) ? bb : 0;
-      const int tp = bc % NP, j = bc / NP;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-      for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+      }
     }
     __syncthreads();
     AFNO_STAMP(3, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl, tid);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -666,7 +636,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   const float* b1 = a.b1 + blk * K;
   const float* b2 = a.b2 + blk * K;
   f32x4 acc[S::MT][S::NTW];
-  gemm_tile_x3<S, AFNO_X3_T>(Ah, Al, w1t, acc, tid);
+  gemm_tile_x3<S, AFNO_X3_T>(Ah, Al, w1t, acc);
   __syncthreads();
   AFNO_STAMP(5, __builtin_amdgcn_s_memtime());
 #pragma unroll
@@ -694,7 +664,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   }
   __syncthreads();
   AFNO_STAMP(6, __builtin_amdgcn_s_memtime());
-  gemm_tile_x3<S>(Ah, Al, w2t, acc, tid);
+  gemm_tile_x3<S>(Ah, Al, w2t, acc);
   __syncthreads();
   AFNO_STAMP(7, __builtin_amdgcn_s_memtime());
   float* X = reinterpret_cast<float*>(ldsf);
@@ -724,16 +694,17 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   {
     cpair v[P0::Q][R0];
 #pragma unroll
-    for (int q = 0; q < P0::Q; ++q) {  // unconditional (clamped item): no partially defined registers
+    for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
-      const int bc = (P0::NB % kNT == 0 || bb < P0::NB) ? bb : 0;
-      const int tp = bc % NP, j = bc / NP;
+      if (P0::NB % kNT == 0 || bb < P0::NB) {
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-      for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * BS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * BS + 2 * tp);
+      }
     }
     __syncthreads();
     AFNO_STAMP(9, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr, tid);  // first pass: no twiddles
+    h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -750,16 +721,15 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   {
     cpair v[P1::Q][R1];
 #pragma unroll
-    for (int q = 0; q < P1::Q; ++q) {  // unconditional (clamped item): no partially defined registers
+    for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
-      const int bc = (P1::NB % kNT == 0 || bb < P1::NB) ? bb : 0;
-      const int tp = bc % NP, j = bc / NP;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-      for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
+      }
     }
-    __syncthreads();  // every wave has its rows: the staging area takes the next tile's input
-    if (tile + static_cast<int>(gridDim.x) < a.ntiles) dma_pass0(tile + gridDim.x);
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl, tid);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -776,7 +746,6 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   }
   AFNO_STAMP(12, __builtin_amdgcn_s_memtime());
   AFNO_STAMP(11, __builtin_amdgcn_s_memrealtime());
-  }
 }
 
 // ------------------------------------------------------------------ instance table
@@ -820,29 +789,6 @@ const AfnoInstance* find_instance(int H, int bs) {
   for (const auto& i : instances())
     if (i.H == H && i.BS == bs) return &i;
   return nullptr;
-}
-
-// workgroups of `kern` (kNT threads, `lds` dynamic bytes) resident on the current device at once;
-// cached per (kernel, device)
-int64_t resident_workgroups(KernFn kern, int64_t lds) {
-  static std::mutex mu;
-  static std::map<std::pair<const void*, int>, int64_t> cache;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) throw std::runtime_error("amd_dft: afno_spectral: no device");
-  std::lock_guard<std::mutex> g(mu);
-  const auto key = std::make_pair(reinterpret_cast<const void*>(kern), dev);
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     static_cast<int>(lds));
-  int per_cu = 0, cus = 0;
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kNT,
-                                                                       static_cast<size_t>(lds));
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral occupancy: ") + hipGetErrorString(e));
-  const int64_t r = static_cast<int64_t>(std::max(per_cu, 1)) * std::max(cus, 1);
-  cache.emplace(key, r);
-  return r;
 }
 
 void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a, void* stream) {
@@ -893,20 +839,9 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   a.lambda = p.lambda;
   const int64_t nblocks = static_cast<int64_t>(p.B) * p.KM * p.NB;
   if (nblocks <= 0) return;
-  if (nblocks >= (int64_t(1) << 31)) throw std::runtime_error("amd_dft: afno_spectral: too many tiles");
-  a.ntiles = static_cast<int>(nblocks);
   if (p.x3) {
     if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
-    // persistent grid: the resident workgroups (occupancy x CUs, a multiple of 8 NB when possible)
-    // MI_DFT_AFNO_PERSIST=0 (A/B): one tile per workgroup (the input DMA is then waited for at once)
-    static const bool persist = [] {
-      const char* e = std::getenv("MI_DFT_AFNO_PERSIST");
-      return !(e && std::string(e) == "0");
-    }();
-    const int64_t res = persist ? resident_workgroups(in->x3, in->lds_x3) : nblocks;
-    int64_t grid = std::min(nblocks, res);
-    if (grid > 8 * p.NB) grid -= grid % (8 * p.NB);
-    launch_kernel(in->x3, in->lds_x3, grid, a, stream);
+    launch_kernel(in->x3, in->lds_x3, nblocks, a, stream);
     return;
   }
   launch_kernel(in->bf16[p.bf16_in ? 1 : 0][p.bf16_out ? 1 : 0], in->lds_bf16, nblocks, a, stream);
