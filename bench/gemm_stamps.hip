@@ -5,15 +5,9 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -fno-slp-vectorize -DAMD_DFT_GEMM_STAMPS \
 //         -Icsrc bench/gemm_stamps.hip -o /tmp/gemm_stamps && /tmp/gemm_stamps
-//   (-DGEMM_ABLATE=4: the epilogue computes everything but skips its stores)
+//   (-DGEMM_ABLATE=4: the epilogue computes everything but skips its stores; 1: no main-loop DMA, 2: no
+//   main-loop fragment reads -- timing-only, profiles/gemm_mainloop_ablation_r3.txt)
 #include "nn/gemm.hip"
-
-namespace amd_dft {  // the 4-wave and 2-workgroup variants are not part of this harness
-bool gemm4w_applicable(const GemmLaunch&) { return false; }
-void launch_gemm4w(const GemmLaunch&, void*) {}
-bool gemm2wg_applicable(const GemmLaunch&) { return false; }
-void launch_gemm2wg(const GemmLaunch&, void*) {}
-}  // namespace amd_dft
 
 #include <algorithm>
 #include <cstdio>
