@@ -204,7 +204,12 @@ struct AfnoArgs {
 
 // GEMM [16 MT x 2BS] = A (LDS bf16, pitch APitch) x Bt^T (global bf16 [n][k]); wave w owns
 // column tiles NTW w .. NTW w + NTW - 1 for all MT row tiles.
-template <class S>
+// TR: MFMA operands swapped (transposed accumulator: a lane holds 4 consecutive columns of one row)
+// AFNO_X3_T: GEMM 1 of both kernels runs transposed, so its epilogue writes 8-byte pieces
+#ifndef AFNO_X3_T
+#define AFNO_X3_T 1
+#endif
+template <class S, bool TR = false>
 __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                                           f32x4 (&acc)[S::MT][S::NTW]) {
   const int lane = threadIdx.x & 63;
@@ -240,6 +245,7 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
         if constexpr (AFNO_ABLATE & 2) acc[mi][nj] += __builtin_bit_cast(f32x4, afr[mi]) + __builtin_bit_cast(f32x4, bq[ks % NQ][nj]);
+        else if constexpr (TR) acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks % NQ][nj], afr[mi], acc[mi][nj], 0, 0, 0);
         else acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
       }
     if constexpr (AFNO_DIAG & 1) diag_guard();
@@ -333,19 +339,33 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   const float* b1 = a.b1 + blk * K;
   const float* b2 = a.b2 + blk * K;
   f32x4 acc[S::MT][S::NTW];
-  gemm_tile<S>(A, w1t, acc);
+  gemm_tile<S, AFNO_X3_T>(A, w1t, acc);
   __syncthreads();
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
-    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
-    const float bias = b1[n];
+    if constexpr (AFNO_X3_T) {  // lane: columns n0 .. n0 + 3 of row m -> one 8-byte write
+      const int n0 = (S::NTW * w + nj) * 16 + 4 * (lane >> 4);
+      const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mi * 16 + 4 * (lane >> 4) + i;
-        A[m * AP + n] = f2bf16(fmaxf(acc[mi][nj][i] + bias, 0.f));
+      for (int mi = 0; mi < S::MT; ++mi) {
+        const int m = mi * 16 + (lane & 15);
+        *reinterpret_cast<uint2*>(A + m * AP + n0) =
+            make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
+                           (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
+                       static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][2] + bias.z, 0.f))) |
+                           (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][3] + bias.w, 0.f))) << 16));
       }
+    } else {
+      const int n = (S::NTW * w + nj) * 16 + (lane & 15);
+      const float bias = b1[n];
+#pragma unroll
+      for (int mi = 0; mi < S::MT; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mi * 16 + 4 * (lane >> 4) + i;
+          A[m * AP + n] = f2bf16(fmaxf(acc[mi][nj][i] + bias, 0.f));
+        }
+    }
   }
   __syncthreads();
   // ---------------- GEMM2 + bias + softshrink -> X (fp16 complex, conjugated for the inverse)
@@ -477,9 +497,6 @@ __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx
 // TR: the same products with the MFMA operands swapped, so the accumulator tile is the transpose:
 // a lane holds 4 CONSECUTIVE output columns n of one row m (instead of 4 rows of one column) --
 // the epilogue then writes 8-byte bf16x4 pieces instead of single bf16 values.
-#ifndef AFNO_X3_T
-#define AFNO_X3_T 1
-#endif
 template <class S, bool TR = false>
 __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
                                              const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
