@@ -39,6 +39,21 @@
 namespace amd_dft {
 namespace {
 
+#ifdef FNO_STAMPS
+// phase clocks (bench/fno_stamps.hip): per wave, s_memtime cycles summed over its units per phase
+// -- [0] setup, [1] spectrum (re)load on a row change, [2] x staging + rotation/split, [3] MFMAs,
+// [4] epilogue; [5] units, [6] s_memrealtime at entry; 8 per wave, written by lane 0 at exit
+__device__ long long* g_fno_stamps;
+#define FNO_T(slot)                                       \
+  do {                                                    \
+    const long long tn_ = __builtin_amdgcn_s_memtime();   \
+    fno_acc[slot] += tn_ - fno_tp;                        \
+    fno_tp = tn_;                                         \
+  } while (0)
+#else
+#define FNO_T(slot) do { } while (0)
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -140,6 +155,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr int PXS = 64 / ES, EP = 64 + 16;
   __shared__ __attribute__((aligned(16))) char es_raw[STG ? 4 : 1][STG ? 32 * EP : 16];
 #endif
+#ifdef FNO_STAMPS
+  long long fno_acc[6] = {0, 0, 0, 0, 0, 0};
+  const long long fno_rt0 = __builtin_amdgcn_s_memrealtime();
+  long long fno_tp = __builtin_amdgcn_s_memtime();
+#endif
   const int nrot = nch * 16 * KS;
   for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -177,6 +197,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + wv;
   const int64_t u0 = gw * units / nw, u1 = (gw + 1) * units / nw;
   if (u0 >= u1) return;  // no barriers below this point
+  FNO_T(0);
 
   char* xs = xs_raw[wv];
   lds_v4s* xs_tr = (lds_v4s*)(xs_raw[wv]);
@@ -241,6 +262,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
       yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
     }
+    FNO_T(1);
     const int w0 = c * CH;
     // ---- x chunk (channels x pixels) into this wave's LDS tile
     wave_lds_fence();
@@ -277,6 +299,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     // branch, the waits after the join would be merged conservatively to vmcnt(0) and drain it)
     load_x(u + 1 < u1 ? u + 1 : u);
     wave_lds_fence();
+    FNO_T(2);
     // ---- MFMA, 4 pixel tiles at a time: conv + spectral into bias-initialised accumulators
 #pragma unroll
     for (int pg = 0; pg < PT / 4; ++pg) {
@@ -328,6 +351,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           }
         }
       }
+      FNO_T(3);
       // ---- epilogue: activation + store, 4 consecutive pixels of one channel per lane
       const int pxg = w0 + 64 * pg + 4 * lq;  // pixel of row i = 0 in tile p4 = 0
 #if FNO_EPI_STAGED
@@ -395,8 +419,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         if (o < Cout && pxg + 16 * s < W) store4<BF>(yb + yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
       }
       }
+      FNO_T(4);
     }
   }
+#ifdef FNO_STAMPS
+  if (lane == 0) {
+    long long* st = g_fno_stamps + gw * 8;
+    for (int i = 0; i < 5; ++i) st[i] = fno_acc[i];
+    st[5] = u1 - u0;
+    st[6] = fno_rt0;
+  }
+#endif
 }
 
 // workgroups of one kernel instance resident on the current device (occupancy x CUs), cached
