@@ -58,9 +58,6 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
   // there would sit on every block's critical path
   // (launch_dftw_r2c guarantees nblk * 16 G <= kDftwPhMax)
   __shared__ float2 phs[kDftwPhMax];
-  const int nph = nblk * 16 * G;
-  for (int t = threadIdx.x; t < nph; t += 64 * NW) phs[t] = ph[t];
-  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row0 = blockIdx.x * 16;
   const int rowA = min(row0 + (lane & 15), R - 1);
@@ -102,10 +99,19 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
   // sink each load down to its use, which serialises the batch into one round trip per block.
   // PF divides the per-wave block count of the 1440-wide FNO rows (8 at NW = 3, 6 at NW = 4).
   constexpr int PF = G >= 4 ? 2 : BF ? (NW == 3 ? 4 : 6) : 3;
-  for (int s0 = wv; s0 < nblk; s0 += NW * PF) {
-    Raw buf[PF][kNKS][NR];
+  // The first batch is requested before the phase table is copied and the workgroup synchronises,
+  // so the table's and the samples' global round trips overlap instead of following each other.
+  Raw buf[PF][kNKS][NR];
 #pragma unroll
-    for (int j = 0; j < PF; ++j) load(min(s0 + NW * j, nblk - 1), buf[j]);
+  for (int j = 0; j < PF; ++j) load(min(wv + NW * j, nblk - 1), buf[j]);
+  const int nph = nblk * 16 * G;
+  for (int t = threadIdx.x; t < nph; t += 64 * NW) phs[t] = ph[t];
+  __syncthreads();
+  for (int s0 = wv; s0 < nblk; s0 += NW * PF) {
+    if (s0 != wv) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) load(min(s0 + NW * j, nblk - 1), buf[j]);
+    }
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const bool live = s0 + NW * j < nblk;

@@ -160,44 +160,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   const long long fno_rt0 = __builtin_amdgcn_s_memrealtime();
   long long fno_tp = __builtin_amdgcn_s_memtime();
 #endif
-  const int nrot = nch * 16 * KS;
-  for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l15 = lane & 15, lq = lane >> 4;
-
-  for (int t = threadIdx.x; t < KS * PT * NG * 64; t += 256) {
-    const int ln = t & 63, r = t >> 6;
-    const int hl = r % NG, f = r / NG;  // f = ks * PT + pt
-    (&g0s[0][0][0][0])[t] = g0[(f * 2 + hl) * 64 + ln];
-  }
-  // conv B operand: Wc^T[i][o], lane holds i = 8lq + j of channel 16ot + l15
-  bf16x8 Wh[CO], Wl[CO];
-  float bo[CO];
-#pragma unroll
-  for (int ot = 0; ot < CO; ++ot) {
-    const int o = 16 * ot + l15;
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = 8 * lq + 2 * j;
-      const float v0 = (o < Cout && i < Cin) ? wc[o * Cin + i] : 0.f;
-      const float v1 = (o < Cout && i + 1 < Cin) ? wc[o * Cin + i + 1] : 0.f;
-      split_pk(v0, v1, hi[j], lo[j]);
-    }
-    Wh[ot] = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-    Wl[ot] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-    bo[ot] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
-  }
-  // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not)
-  for (int t = threadIdx.x; t < 4 * 32 * XP * ES / 16; t += 256)
-    reinterpret_cast<uint4*>(&xs_raw[0][0])[t] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
 
   const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
   const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + wv;
   const int64_t u0 = gw * units / nw, u1 = (gw + 1) * units / nw;
-  if (u0 >= u1) return;  // no barriers below this point
-  FNO_T(0);
 
   char* xs = xs_raw[wv];
   lds_v4s* xs_tr = (lds_v4s*)(xs_raw[wv]);
@@ -239,29 +207,71 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int t = 0; t < NR; ++t) xr[q][t] = sp[t];
     }
   };
-  load_x(u0);
+  // the spectrum operand of one (b, h) row and its output row offsets
+  auto load_row = [&](int64_t row) {
+    cur_row = row;
+    const int64_t b = row / H, h = row - b * H;
+#pragma unroll
+    for (int ot = 0; ot < CO; ++ot)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
+          Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
+        }
+    const int64_t y0 = ((b * Cout * H + h) * W + 4 * lq) * ES;
+    ybase = (b * Cout * H + h) * W * ES;
+#pragma unroll
+    for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
+    yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
+  };
+  // this wave's first x chunk and spectrum row are requested before the table setup below, so the
+  // three global round trips overlap instead of following each other (the setup was ~17 % of a
+  // wave's time, profiles/fno_phases_r3.txt)
+  if (u0 < u1) {
+    load_x(u0);
+    load_row(u0 / nch);
+  }
+
+
+  const int nrot = nch * 16 * KS;
+  for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
+  for (int t = threadIdx.x; t < KS * PT * NG * 64; t += 256) {
+    const int ln = t & 63, r = t >> 6;
+    const int hl = r % NG, f = r / NG;  // f = ks * PT + pt
+    (&g0s[0][0][0][0])[t] = g0[(f * 2 + hl) * 64 + ln];
+  }
+  // conv B operand: Wc^T[i][o], lane holds i = 8lq + j of channel 16ot + l15
+  bf16x8 Wh[CO], Wl[CO];
+  float bo[CO];
+#pragma unroll
+  for (int ot = 0; ot < CO; ++ot) {
+    const int o = 16 * ot + l15;
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 8 * lq + 2 * j;
+      const float v0 = (o < Cout && i < Cin) ? wc[o * Cin + i] : 0.f;
+      const float v1 = (o < Cout && i + 1 < Cin) ? wc[o * Cin + i + 1] : 0.f;
+      split_pk(v0, v1, hi[j], lo[j]);
+    }
+    Wh[ot] = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+    Wl[ot] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
+    bo[ot] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+  }
+  // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not)
+  for (int t = threadIdx.x; t < 4 * 32 * XP * ES / 16; t += 256)
+    reinterpret_cast<uint4*>(&xs_raw[0][0])[t] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  if (u0 >= u1) return;  // no barriers below this point
+  FNO_T(0);
 
   for (int64_t u = u0; u < u1; ++u) {
     const int64_t row = u / nch;
     const int c = static_cast<int>(u - row * nch);
-    if (row != cur_row) {
-      cur_row = row;
-      const int64_t b = row / H, h = row - b * H;
-#pragma unroll
-      for (int ot = 0; ot < CO; ++ot)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
-            Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
-          }
-      const int64_t y0 = ((b * Cout * H + h) * W + 4 * lq) * ES;
-      ybase = (b * Cout * H + h) * W * ES;
-#pragma unroll
-      for (int ot = 0; ot < CO; ++ot) yrow[ot] = y0 + min(16 * ot + l15, Cout - 1) * plane;
-      yrowp = y0 + min(16 + (l15 & 3), Cout - 1) * plane;
-    }
+    if (row != cur_row) load_row(row);
     FNO_T(1);
     const int w0 = c * CH;
     // ---- x chunk (channels x pixels) into this wave's LDS tile
