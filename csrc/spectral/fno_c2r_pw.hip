@@ -28,6 +28,9 @@
 
 #include "dft_gemm.h"
 
+#ifndef FNO_EPI_SWAP
+#define FNO_EPI_SWAP 1  // bf16 output: lane-transposed 16-byte stores (v_permlane16/32_swap), see the epilogue
+#endif
 #ifndef FNO_EPI_STAGED
 // 1: output through a per-wave LDS tile in 64-byte row pieces; 0 (default): straight from the MFMA
 // layout.  Measured slower staged (profiles/fno_epilogue_r3.txt: FNO block bf16 61.7-62.3 vs
@@ -407,12 +410,46 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int ot = 0; ot < CO; ++ot) {
         if (ot == 1 && pack) break;
         const int o = 16 * ot + l15;
+        if constexpr (BF && FNO_EPI_SWAP) {
+          // 4x4 transpose of the 8-byte pieces across the lanes of one channel (rows lq of the
+          // wave): lane (c, lq) ends up with pixel tile lq's four 4-pixel groups, i.e. 32
+          // contiguous bytes -> two 16-byte stores instead of four 8-byte ones (same bytes, half
+          // the store instructions).  permlane32_swap exchanges rows {2,3} of its first operand
+          // with rows {0,1} of its second; permlane16_swap rows {1,3} with {0,2}.
+          uint32_t d[4][2];
 #pragma unroll
-        for (int p4 = 0; p4 < 4; ++p4) {
-          float v[4];
+          for (int p4 = 0; p4 < 4; ++p4) {
+            d[p4][0] = pk_bf16(act<ACT>(acc[p4][ot][0]), act<ACT>(acc[p4][ot][1]));
+            d[p4][1] = pk_bf16(act<ACT>(acc[p4][ot][2]), act<ACT>(acc[p4][ot][3]));
+          }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
-          if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yb + yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
+          for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              const auto r = __builtin_amdgcn_permlane32_swap(d[pp][w], d[pp + 2][w], false, false);
+              d[pp][w] = r[0];
+              d[pp + 2][w] = r[1];
+            }
+#pragma unroll
+          for (int pp = 0; pp < 4; pp += 2)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              const auto r = __builtin_amdgcn_permlane16_swap(d[pp][w], d[pp + 1][w], false, false);
+              d[pp][w] = r[0];
+              d[pp + 1][w] = r[1];
+            }
+          const int px0 = w0 + 64 * pg + 16 * lq;  // this lane's 16 pixels
+          char* dst = yb + yrow[ot] + static_cast<int64_t>(w0 + 64 * pg + 12 * lq) * ES;  // yrow carries +4 lq pixels
+          if (o < Cout && px0 + 8 <= W) *reinterpret_cast<uint4*>(dst) = make_uint4(d[0][0], d[0][1], d[1][0], d[1][1]);
+          if (o < Cout && px0 + 16 <= W) *reinterpret_cast<uint4*>(dst + 16) = make_uint4(d[2][0], d[2][1], d[3][0], d[3][1]);
+        } else {
+#pragma unroll
+          for (int p4 = 0; p4 < 4; ++p4) {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
+            if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yb + yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
+          }
         }
       }
       if (CO == 2 && pack) {

@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU session 13 (round 3): FNO kernels with their first loads issued before the table setup -- tests, phase
-# clocks, and the FNO block A/B against the previous build (build_diag/fnoprev).
+# clocks, and the FNO block A/B/C: + lane-transposed 16-byte bf16 stores (in-tree), without them
+# (build_diag/fnonoswap), the previous build (build_diag/fnoprev).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -18,6 +19,7 @@ step s13_build_stamps 300 hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -f
 TAILN=16 step s13_fno_stamps 120 /tmp/fno_stamps
 for r in 1 2; do
   TAILN=3 step s13_fno_new_$r 300 python -u bench/bench_fno.py --amd-only --rounds 10
+  TAILN=3 step s13_fno_noswap_$r 300 env MI_DFT_LIB=$PWD/build_diag/fnonoswap/_C.so python -u bench/bench_fno.py --amd-only --rounds 10
   TAILN=3 step s13_fno_prev_$r 300 env MI_DFT_LIB=$PWD/build_diag/fnoprev/_C.so python -u bench/bench_fno.py --amd-only --rounds 10
 done
 TAILN=30 step s13_kernels 300 python -u bench/bench_kernels_fno.py
