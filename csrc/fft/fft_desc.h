@@ -52,6 +52,13 @@ struct PassDesc {
   const float* ln_gamma = nullptr;  // [I] fp32
   const float* ln_beta = nullptr;   // [I] fp32
   const float* ln_pre = nullptr;    // [I] fp32 or null
+  // FNO mode mixing fused into the first-pass gather of a pruned C2C (fixed column kernels,
+  // fp32): the transform input is never stored; element (outer o = b * mix_cout + oc, signal c,
+  // stored mode s) is  sum_i in[b][i][s][c] * mix_w[i][oc][s][c]  (complex), where `in` is the
+  // [B, mix_cin, S, I] mode tensor and mix_w the [mix_cin, mix_cout, S, I] weights (the per-outer
+  // stride So_in is that of one [S, I] channel slice).
+  const float* mix_w = nullptr;
+  int32_t mix_cin = 0, mix_cout = 0;
 
   int32_t L = 1;       // transform length
   int32_t npass = 0;   // number of Stockham passes (0 when L == 1)

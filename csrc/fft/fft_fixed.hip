@@ -28,7 +28,31 @@ using namespace fixed_detail;
 
 const std::vector<FixedCfg>& fixed_configs() { return table(); }
 
+// The radix order of the first configuration of length L (the plan adopts it).
+// MI_DFT_FFT_RADICES="L:r,r,...;L:..." picks another configured order for L (A/B runs; read
+// when the plan of L is first built).
 std::vector<int32_t> fixed_radices(int32_t L) {
+  if (const char* e = std::getenv("MI_DFT_FFT_RADICES")) {
+    const std::string spec(e);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      size_t end = spec.find(';', pos);
+      if (end == std::string::npos) end = spec.size();
+      const std::string item = spec.substr(pos, end - pos);
+      pos = end + 1;
+      const size_t colon = item.find(':');
+      if (colon == std::string::npos || std::atoi(item.substr(0, colon).c_str()) != L) continue;
+      std::vector<int32_t> want;
+      for (size_t q = colon + 1; q < item.size();) {
+        size_t c = item.find(',', q);
+        if (c == std::string::npos) c = item.size();
+        want.push_back(std::atoi(item.substr(q, c - q).c_str()));
+        q = c + 1;
+      }
+      for (const auto& c : fixed_configs())
+        if (c.L == L && std::vector<int32_t>(c.radix, c.radix + c.npass) == want) return want;
+    }
+  }
   for (const auto& c : fixed_configs())
     if (c.L == L) return std::vector<int32_t>(c.radix, c.radix + c.npass);
   return {};
@@ -120,6 +144,15 @@ bool prepare_fixed(const PassDesc& d, int& best_out, FixedArgs& a, int64_t& nblo
     for (const void* ad : {d.add1, d.add2})
       pv = pv && (ad == nullptr || reinterpret_cast<uintptr_t>(ad) % (2 * rout * eso) == 0);
     a.pairvec = pv ? 1 : 0;
+  }
+  a.mix_w = d.mix_w;
+  a.mix_cin = d.mix_cin;
+  a.mix_cout = d.mix_cout;
+  if (d.mix_w) {  // mixing gather: pruned fp32 C2C over a column layout (outer = batch x Cout)
+    const bool ok = cfg.cols && d.kind == Kind::C2C && !a.bf16_in && !a.bf16_out && d.mix_cin > 0 && d.mix_cout > 0 &&
+                    d.O % d.mix_cout == 0 && (d.in_lo + d.in_hi != d.L || d.out_lo + d.out_hi != d.L) &&
+                    d.So_in * d.mix_cin * d.mix_cout < 0x7fffffffLL;
+    if (!ok) return false;
   }
   if (d.ln_stats) {  // LayerNorm IO: channel-last bf16 pairs, R2C input / C2R addend only
     const bool ok = cfg.cols && d.kind != Kind::C2C && a.pairvec && a.bf16_in && a.bf16_out && d.ln_gamma &&

@@ -40,6 +40,9 @@ struct FixedArgs {
   const float* ln_gamma;
   const float* ln_beta;
   const float* ln_pre;
+  // NADD == 4 (C2C only): FNO mode mixing on the first-pass gather (see PassDesc::mix_w)
+  const float* mix_w;
+  int32_t mix_cin, mix_cout;
 #ifdef AMD_DFT_FFT_STAMPS
   long long* stamps;  // diagnostic build only (bench/fft_stamps.hip): per-block phase clocks
 #endif
@@ -179,7 +182,36 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
   const FixedArgs& a = x.a;
   float2 z;
   if constexpr (K == Kind::C2C) {
-    if constexpr (PR) {
+    if constexpr (PR && NADD == 4) {
+      // mixed input: x.in = this batch's [Cin][S][I] modes, x.add1 = this output channel's
+      // weights (input-channel stride Cout * So_in).  Only stored modes run the channel loop
+      // (at most one or two of a thread's R elements), so the branch costs less than the loads.
+      const int s = n < a.in_lo ? n : (n >= L - a.in_hi ? a.in_lo + (n - (L - a.in_hi)) : -1);
+      float zr = 0.f, zi = 0.f;
+      if (x.ok0 && s >= 0) {
+        const int32_t off = x.cc * a.Si_in + s * a.Sn_in;
+        const int32_t sx = static_cast<int32_t>(a.So_in), sw = static_cast<int32_t>(a.So_in) * a.mix_cout;
+        // batches of 10 channels: all 20 loads of a batch in flight before the first FMA
+        // (clamped channel index, masked product) -- one L2 round trip per batch
+        constexpr int U = 10;
+        for (int i0 = 0; i0 < a.mix_cin; i0 += U) {
+          float2 xv[U], wv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int i = min(i0 + u, a.mix_cin - 1);
+            xv[u] = ld_c<false>(x.in, i * sx + off);
+            wv[u] = ld_c<false>(x.add1, i * sw + off);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float m = i0 + u < a.mix_cin ? 1.f : 0.f;
+            zr = fmaf(m * xv[u].x, wv[u].x, fmaf(-m * xv[u].y, wv[u].y, zr));
+            zi = fmaf(m * xv[u].x, wv[u].y, fmaf(m * xv[u].y, wv[u].x, zi));
+          }
+        }
+      }
+      z = make_float2(zr, zi);
+    } else if constexpr (PR) {
       const int s = n < a.in_lo ? n : (n >= L - a.in_hi ? a.in_lo + (n - (L - a.in_hi)) : -1);
       const bool ok = x.ok0 && s >= 0;
       z = sel(ok, ld_c<BF>(x.in, x.cc * a.Si_in + (s < 0 ? 0 : s) * a.Sn_in));
@@ -436,9 +468,15 @@ __device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int 
     x.ok0 = false;  // LDS slot (barriers stay uniform), store nothing
     x.ok1 = false;
   }
-  x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
+  if constexpr (K == Kind::C2C && NADD == 4) {  // mixing gather: batch / output-channel bases
+    const int32_t b = o / a.mix_cout, oc = o - b * a.mix_cout;
+    x.in = static_cast<const float*>(a.in) + static_cast<int64_t>(b) * a.mix_cin * a.So_in;
+    x.add1 = a.mix_w + static_cast<int64_t>(oc) * a.So_in;
+  } else {
+    x.in = static_cast<const char*>(a.in) + static_cast<int64_t>(o) * a.So_in * (BFI ? 2 : 4);
+  }
   x.out = static_cast<char*>(a.out) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
-  if constexpr (NADD >= 1) x.add1 = static_cast<const char*>(a.add1) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
+  if constexpr (NADD >= 1 && NADD <= 3) x.add1 = static_cast<const char*>(a.add1) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
   if constexpr (NADD == 2) x.add2 = static_cast<const char*>(a.add2) + static_cast<int64_t>(o) * a.So_out * (BFO ? 2 : 4);
   if constexpr (NADD == 3) {
     x.st = reinterpret_cast<const float2*>(a.ln_stats) + static_cast<int64_t>(o) * L;
@@ -507,6 +545,8 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(256, false, 16, 4, 16, 16)            \
   X(720, true, 90, 4, 8, 9, 10)           \
   X(720, true, 90, 2, 8, 9, 10)           \
+  X(1440, false, 288, 1, 5, 6, 6, 8)      \
+  X(720, true, 180, 4, 4, 4, 5, 9)        \
   X(720, true, 45, 8, 8, 9, 10)           \
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \
@@ -533,6 +573,12 @@ void launch_one(const FixedArgs& a, dim3 grid, hipStream_t st) {
   // (cheap, Hermitian) truncation in the common path.  Column layouts (channel-last) get the
   // paired-vector variant (PV) and the C2R addend epilogue (NADD).
   const bool pr = K == Kind::C2C && (a.in_lo + a.in_hi != F::L || a.out_lo + a.out_hi != F::L);
+  if constexpr (K == Kind::C2C && COLS) {
+    if (a.mix_w) {  // FNO mixing gather: fp32 pruned column transforms only (host-checked)
+      hipLaunchKernelGGL((fft_fixed_kernel<K, COLS, TP, T, F, false, false, true, 4, false>), grid, dim3(TP * T), 0, st, a);
+      return;
+    }
+  }
   if constexpr (K == Kind::C2C) {
     if (pr) return launch_dt<K, COLS, TP, T, F, true, 0, false>(a, grid, st);
   }

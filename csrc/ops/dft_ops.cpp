@@ -98,12 +98,18 @@ struct LnIO {
   const float* pre = nullptr;
 };
 
-// Returns false only for an LnIO pass that no specialised kernel covers (nothing launched).
+// FNO mode mixing fused into the gather of a pruned C2C (see PassDesc::mix_w)
+struct MixIO {
+  const float* w = nullptr;
+  int cin = 0, cout = 0;
+};
+
+// Returns false only for an LnIO / MixIO pass that no specialised kernel covers (nothing launched).
 bool run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std::vector<int64_t>& in_shape,
               const std::vector<int64_t>& out_shape, int axis, int64_t L, int in_lo, int in_hi, int out_lo,
               int out_hi, float scale, bool inverse, const void* add1 = nullptr, const void* add2 = nullptr,
-              const LnIO* ln = nullptr) {
-  if (ln && L > lds_limit()) return false;
+              const LnIO* ln = nullptr, const MixIO* mix = nullptr) {
+  if ((ln || mix) && L > lds_limit()) return false;
   if (L > lds_limit()) {
     run_pass_large(kind, in, out, in_shape, out_shape, axis, L, in_lo, in_hi, out_lo, out_hi, scale, inverse, add1,
                    add2);
@@ -142,6 +148,12 @@ bool run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
     d.ln_gamma = ln->gamma;
     d.ln_beta = ln->beta;
     d.ln_pre = ln->pre;
+    return launch_fft_fixed(d, stream);
+  }
+  if (mix) {
+    d.mix_w = mix->w;
+    d.mix_cin = mix->cin;
+    d.mix_cout = mix->cout;
     return launch_fft_fixed(d, stream);
   }
   launch_fft_pass(d, stream);
@@ -594,6 +606,64 @@ at::Tensor c2c_axis_cpu(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_
   return at::view_as_real(r.to(at::kComplexFloat).contiguous()).contiguous();
 }
 
+// FNO spectral layer middle, inverse half: ym[b, o, s, c] = sum_i xm[b, i, s, c] w[i, o, s, c]
+// (complex mode mixing), then the pruned inverse C2C along s (stored modes [0, in_lo) u
+// [n - in_hi, n) of a length-n transform, all n outputs), times `scale`:
+//   xm [B, Cin, in_lo + in_hi, I, 2], w [Cin, Cout, (in_lo + in_hi) * I, 2] -> [B, Cout, n, I, 2].
+// On the GPU the mixing runs inside the first pass' gather of the fixed column kernels (one
+// kernel, the mixed modes are never stored); otherwise fno_mix + c2c_axis.
+void check_mix_c2c(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t in_lo, int64_t in_hi) {
+  TORCH_CHECK(xm.dim() == 5 && xm.size(4) == 2, "amd_dft.fno_mix_c2c: xm must be [B, Cin, S, I, 2]");
+  TORCH_CHECK(xm.size(2) == in_lo + in_hi && in_lo >= 0 && in_hi >= 0 && in_lo + in_hi <= n && in_lo + in_hi >= 1,
+              "amd_dft.fno_mix_c2c: xm stores ", xm.size(2), " modes, expected in_lo + in_hi <= n");
+  TORCH_CHECK(w.dim() >= 3 && w.size(0) == xm.size(1) && w.size(-1) == 2 &&
+                  w.numel() == w.size(0) * w.size(1) * xm.size(2) * xm.size(3) * 2,
+              "amd_dft.fno_mix_c2c: w must be [Cin, Cout, S * I, 2]");
+}
+
+at::Tensor fno_mix_op(const at::Tensor& x, const at::Tensor& w) {
+  static auto op = c10::Dispatcher::singleton().findSchemaOrThrow("amd_dft::fno_mix", "").typed<at::Tensor(
+      const at::Tensor&, const at::Tensor&)>();
+  return op.call(x, w);
+}
+
+at::Tensor fno_mix_c2c_unfused(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t in_lo, int64_t in_hi,
+                               double scale, bool cuda) {
+  const int64_t B = xm.size(0), Cin = xm.size(1), S = xm.size(2), I = xm.size(3), Cout = w.size(1);
+  at::Tensor ym = fno_mix_op(xm.reshape({B, Cin, S * I, 2}), w.reshape({Cin, Cout, S * I, 2})).reshape({B, Cout, S, I, 2});
+  return cuda ? c2c_axis_cuda(ym, 2, n, in_lo, in_hi, n, 0, true, scale) : c2c_axis_cpu(ym, 2, n, in_lo, in_hi, n, 0, true, scale);
+}
+
+at::Tensor fno_mix_c2c_cuda(const at::Tensor& xm_, const at::Tensor& w_, int64_t n, int64_t in_lo, int64_t in_hi,
+                            double scale) {
+  const c10::DeviceGuard guard(xm_.device());
+  check_mix_c2c(xm_, w_, n, in_lo, in_hi);
+  at::Tensor xm = xm_.to(at::kFloat).contiguous();
+  at::Tensor w = w_.to(at::kFloat).contiguous();
+  const int64_t B = xm.size(0), Cin = xm.size(1), S = xm.size(2), I = xm.size(3), Cout = w.size(1);
+  at::Tensor out = alloc_complex({B, Cout, n, I}, xm.options(), at::kFloat);
+  if (out.numel() == 0) return out;
+  if (Cin < (int64_t(1) << 15) && Cout < (int64_t(1) << 15)) {
+    const MixIO mix{w.data_ptr<float>(), static_cast<int>(Cin), static_cast<int>(Cout)};
+    if (run_pass(Kind::C2C, xm, out, {B, Cout, S, I}, {B, Cout, n, I}, 2, n, static_cast<int>(in_lo),
+                 static_cast<int>(in_hi), static_cast<int>(n), 0, static_cast<float>(scale), true, nullptr, nullptr,
+                 nullptr, &mix))
+      return checked(out, "fno_mix_c2c");
+  }
+  // no fixed column kernel for this length / layout: the two native kernels
+  return checked(fno_mix_c2c_unfused(xm, w, n, in_lo, in_hi, scale, true), "fno_mix_c2c");
+}
+
+at::Tensor fno_mix_c2c_cpu(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t in_lo, int64_t in_hi,
+                           double scale) {
+  check_mix_c2c(xm, w, n, in_lo, in_hi);
+  return fno_mix_c2c_unfused(xm.to(at::kFloat).contiguous(), w.to(at::kFloat).contiguous(), n, in_lo, in_hi, scale, false);
+}
+
+at::Tensor fno_mix_c2c_meta(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t, int64_t, double) {
+  return at::empty({xm.size(0), w.size(1), n, xm.size(3), 2}, xm.options().dtype(at::kFloat));
+}
+
 at::Tensor c2c_axis_meta(const at::Tensor& x, int64_t dim, int64_t n, int64_t in_lo, int64_t in_hi, int64_t out_lo,
                          int64_t out_hi, bool, double) {
   std::vector<int64_t> s(x.sizes().begin(), x.sizes().end());
@@ -981,6 +1051,7 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("c2c_axis(Tensor x, int dim, int n, int in_lo, int in_hi, int out_lo, int out_hi, bool inverse=False, "
         "float scale=1.0) -> Tensor");
   m.def("dftw_r2c(Tensor x, int m, float scale=1.0) -> Tensor");
+  m.def("fno_mix_c2c(Tensor xm, Tensor w, int n, int in_lo, int in_hi, float scale=1.0) -> Tensor");
   m.def("r2c_ln(Tensor x, int dim, float scale, int keep, Tensor stats, Tensor gamma, Tensor beta, Tensor? pre=None, "
         "ScalarType? out_dtype=None) -> Tensor");
   m.def("c2r_ln_add(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
@@ -1001,6 +1072,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("c2r_add", AMD_DFT_TRACED("amd_dft::c2r_add", amd_dft::c2r_add_cuda));
   m.impl("c2c_axis", AMD_DFT_TRACED("amd_dft::c2c_axis", amd_dft::c2c_axis_cuda));
   m.impl("dftw_r2c", AMD_DFT_TRACED("amd_dft::dftw_r2c", amd_dft::dftw_r2c_cuda));
+  m.impl("fno_mix_c2c", AMD_DFT_TRACED("amd_dft::fno_mix_c2c", amd_dft::fno_mix_c2c_cuda));
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cuda));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cuda));
 }
@@ -1012,6 +1084,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("c2r_add", AMD_DFT_TRACED("amd_dft::c2r_add", amd_dft::c2r_add_cpu));
   m.impl("c2c_axis", AMD_DFT_TRACED("amd_dft::c2c_axis", amd_dft::c2c_axis_cpu));
   m.impl("dftw_r2c", AMD_DFT_TRACED("amd_dft::dftw_r2c", amd_dft::dftw_r2c_cpu));
+  m.impl("fno_mix_c2c", AMD_DFT_TRACED("amd_dft::fno_mix_c2c", amd_dft::fno_mix_c2c_cpu));
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cpu));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cpu));
 }
@@ -1023,6 +1096,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("c2r_add", &amd_dft::c2r_add_meta);
   m.impl("c2c_axis", &amd_dft::c2c_axis_meta);
   m.impl("dftw_r2c", &amd_dft::dftw_r2c_meta);
+  m.impl("fno_mix_c2c", &amd_dft::fno_mix_c2c_meta);
   m.impl("r2c_ln", &amd_dft::r2c_ln_meta);
   m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_meta);
 }

@@ -10,7 +10,11 @@
 // pixels of one channel (8/16-byte stores).  Per CH-pixel chunk starting at w0:
 //   spec:  A = G[k'][px]  (bf16 hi/lo fragments of s_k cos / -s_k sin, identical for every chunk,
 //          staged once per workgroup in LDS),  B = Y rotated by e^{2 pi i k w0/W} (fp32 in
-//          registers, split hi/lo per chunk) -- the same phase factorisation as dft_gemm.hip;
+//          registers, split hi/lo per chunk) -- the same phase factorisation as dft_gemm.hip.
+//          bf16 output: G hi and Y hi only (bf16 MFMA operands, fp32 accumulation, the precision
+//          of a bf16 nn.Linear); the Y lo plane would only refine an operand whose partner G is
+//          already rounded to bf16 (FNO_BF_YLO=1 restores it: 8 instead of 4 spectral MFMAs per
+//          pixel tile and channel tile);
 //   conv:  A = x[i][px] from a per-wave LDS tile of the channel-planar input, read transposed by
 //          ds_read_b64_tr_b16 (bf16; two reads give a lane its 8 channels of one pixel),
 //          B = Wc^T (hi/lo split once).
@@ -30,6 +34,9 @@
 
 #ifndef FNO_EPI_SWAP
 #define FNO_EPI_SWAP 1  // bf16 output: lane-transposed 16-byte stores (v_permlane16/32_swap), see the epilogue
+#endif
+#ifndef FNO_BF_YLO
+#define FNO_BF_YLO 0  // bf16 output: also the G_hi * Y_lo spectral products (see the header)
 #endif
 #ifndef FNO_EPI_STAGED
 // 1: output through a per-wave LDS tile in 64-byte row pieces; 0 (default): straight from the MFMA
@@ -143,6 +150,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   using GG = Geo<BF>;
   constexpr int PT = GG::PT, XP = GG::XP, ES = GG::ES, CH = GG::CH;
   constexpr bool PREC3 = !BF;  // fp32 output: also the G_lo * Y_hi term (twiddles exact to ~2^-17)
+  constexpr bool YLO = !BF || FNO_BF_YLO;  // the G_hi * Y_lo term
   constexpr int NG = PREC3 ? 2 : 1;
   __shared__ bf16x8 g0s[KS][PT][NG][64];
   __shared__ __attribute__((aligned(16))) char xs_raw[4][32 * XP * ES];
@@ -263,9 +271,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     Wl[ot] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
     bo[ot] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
   }
-  // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not)
-  for (int t = threadIdx.x; t < 4 * 32 * XP * ES / 16; t += 256)
-    reinterpret_cast<uint4*>(&xs_raw[0][0])[t] = make_uint4(0, 0, 0, 0);
+  // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not); rows < Cin
+  // are rewritten by every chunk before they are read
+  {
+    constexpr int RW = XP * ES / 16;  // 16-byte words per channel row
+    const int nz = (32 - Cin) * RW;   // per wave tile
+    for (int t = threadIdx.x; t < 4 * nz; t += 256) {
+      const int wq = t / nz, r = t - wq * nz;
+      reinterpret_cast<uint4*>(&xs_raw[wq][0])[Cin * RW + r] = make_uint4(0, 0, 0, 0);
+    }
+  }
   __syncthreads();
 
   if (u0 >= u1) return;  // no barriers below this point
@@ -289,7 +304,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
     }
     // ---- rotate + split the spectral operand for this chunk
-    bf16x8 Bh[CO][KS], Bl[CO][KS];
+    bf16x8 Bh[CO][KS], Bl[YLO ? CO : 1][YLO ? KS : 1];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       uint32_t hi[CO][4], lo[CO][4];
@@ -299,13 +314,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
         for (int ot = 0; ot < CO; ++ot) {
           const float2 v = Yv[ot][ks][q];
-          split_pk(v.x * r.x - v.y * r.y, v.x * r.y + v.y * r.x, hi[ot][q], lo[ot][q]);
+          const float re = v.x * r.x - v.y * r.y, im = v.x * r.y + v.y * r.x;
+          if constexpr (YLO) split_pk(re, im, hi[ot][q], lo[ot][q]);
+          else hi[ot][q] = pk_bf16(re, im);
         }
       }
 #pragma unroll
       for (int ot = 0; ot < CO; ++ot) {
         Bh[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(hi[ot][0], hi[ot][1], hi[ot][2], hi[ot][3]));
-        Bl[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(lo[ot][0], lo[ot][1], lo[ot][2], lo[ot][3]));
+        if constexpr (YLO) Bl[ot][ks] = __builtin_bit_cast(bf16x8, make_uint4(lo[ot][0], lo[ot][1], lo[ot][2], lo[ot][3]));
       }
     }
     // prefetch the next unit's x (unconditionally -- the last unit re-loads itself: behind a
@@ -354,7 +371,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
           for (int ot = 0; ot < CO; ++ot) {
             acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, Bh[ot][ks], acc[p4][ot], 0, 0, 0);
-            acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, Bl[ot][ks], acc[p4][ot], 0, 0, 0);
+            if constexpr (YLO) acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, Bl[ot][YLO ? ks : 0], acc[p4][ot], 0, 0, 0);
           }
           if constexpr (PREC3) {
             const bf16x8 gl = g0s[ks][pt][NG - 1][lane];

@@ -9,8 +9,10 @@ kernels per stage, and the full-resolution spectral output is never written to H
   1. pruned R2C over (H, W): along W a truncated DFT on MFMA (``csrc/spectral/dft_gemm.hip``,
      only the kept ``[0, m2)`` modes), then a pruned Stockham FFT along H keeping
      ``[0, m1) u [H-m1, H)``;
-  2. ``fno_mix``  -- the per-mode complex channel mixing on MFMA (``csrc/spectral/fno_mix.hip``);
-  3. pruned inverse FFT along H (``c2c_axis``), then ``fno_c2r_pw``: the inverse truncated DFT
+  2. ``fno_mix_c2c`` -- the per-mode complex channel mixing computed in the first-pass gather of
+     the pruned inverse FFT along H (the mixed modes are never stored; ``fno_mix`` on MFMA,
+     ``csrc/spectral/fno_mix.hip``, plus ``c2c_axis`` where no fixed column kernel covers H);
+  3. ``fno_c2r_pw``: the inverse truncated DFT
      along W on MFMA fused with the 1x1 convolution, bias and GELU
      (``csrc/spectral/fno_c2r_pw.hip``) -- reads x, writes y, nothing else.
 
@@ -111,8 +113,8 @@ class FNOBlock(nn.Module):
         return F.gelu(y) if self.activation else y
 
     def _forward_amd(self, x: torch.Tensor) -> torch.Tensor:
-        """pruned R2C (MFMA DFT-GEMM along W + pruned FFT along H) -> MFMA mode mixing ->
-        pruned inverse FFT along H -> fused [inverse DFT-GEMM along W + 1x1 conv + bias + GELU]."""
+        """pruned R2C (MFMA DFT-GEMM along W + pruned FFT along H) -> [mode mixing + pruned inverse
+        FFT along H] -> fused [inverse DFT-GEMM along W + 1x1 conv + bias + GELU]: four kernels."""
         sp = self.spectral
         B, C, H, W = x.shape
         sp._check(H, W)
@@ -120,9 +122,9 @@ class FNOBlock(nn.Module):
         ops = torch.ops.amd_dft
         xw = ops.dftw_r2c(x, m2, 1.0)  # [B, Cin, H, m2, 2]  truncated DFT along W on MFMA
         xm = ops.c2c_axis(xw, 2, H, H, 0, m1, m1, False, 1.0)  # [B, Cin, 2*m1, m2, 2]
-        ym = S.fno_spectral_mix(xm.reshape(B, C, 2 * m1 * m2, 2), sp._packed_weight())
-        ym = ym.reshape(B, sp.out_ch, 2 * m1, m2, 2)
-        yw = ops.c2c_axis(ym, 2, H, m1, m1, H, 0, True, 1.0 / (H * W))  # [B, Cout, H, m2, 2]
+        # mode mixing inside the inverse H transform's gather (one kernel; fno_mix + c2c_axis
+        # where no fixed column kernel covers H)
+        yw = ops.fno_mix_c2c(xm, sp._packed_weight(), H, m1, m1, 1.0 / (H * W))  # [B, Cout, H, m2, 2]
         return ops.fno_c2r_pw(yw, x, self.w.weight.reshape(self.w.out_channels, -1).float(), self.w.bias.float(),
                               self.activation)
 

@@ -231,3 +231,42 @@ def test_fno_c2r_pw_kernel_gpu(device):
             out = torch.ops.amd_dft.fno_c2r_pw(yw.to(device), x.to(device), wc.to(device), b.to(device), gelu)
             assert out.dtype == dt
             assert rel_l2(out.float(), ref) < tol, (B, Ci, Co, H, W, m, dt)
+
+
+def _mix_c2c_reference(xm, w, n, lo, hi, scale):
+    """fp64 torch composition: complex mode mixing, zero-padded unnormalised inverse FFT along dim 2."""
+    B, Ci, S_, I, _ = xm.shape
+    Co = w.shape[1]
+    xc = torch.view_as_complex(xm.double().contiguous())
+    wc = torch.view_as_complex(w.double().reshape(Ci, Co, S_, I, 2).contiguous())
+    ym = torch.einsum("bisc,iosc->bosc", xc, wc)
+    full = torch.zeros(B, Co, n, I, dtype=torch.complex128)
+    full[:, :, :lo] = ym[:, :, :lo]
+    if hi:
+        full[:, :, n - hi:] = ym[:, :, lo:]
+    return torch.view_as_real(torch.fft.ifft(full, dim=2, norm="forward") * scale)
+
+
+@pytest.mark.parametrize("shape", [(1, 4, 5, 20, 3, 3, 6), (2, 3, 2, 16, 4, 2, 3)])
+def test_fno_mix_c2c_cpu(shape):
+    """Mode mixing + pruned inverse C2C in one op (CPU: fno_mix + c2c_axis) vs the fp64 composition."""
+    B, Ci, Co, n, lo, hi, I = shape
+    torch.manual_seed(21)
+    xm = torch.randn(B, Ci, lo + hi, I, 2)
+    w = torch.randn(Ci, Co, (lo + hi) * I, 2)
+    out = torch.ops.amd_dft.fno_mix_c2c(xm, w, n, lo, hi, 0.25)
+    assert out.shape == (B, Co, n, I, 2)
+    assert rel_l2(out, _mix_c2c_reference(xm, w, n, lo, hi, 0.25)) < 1e-6
+
+
+@pytest.mark.gpu
+def test_fno_mix_c2c_gpu(device):
+    """Fused mixing gather of the fixed 720-point column kernel (FNO config 3 shapes) and the
+    unfused fallback (a length with no fixed column kernel), vs the fp64 composition."""
+    torch.manual_seed(22)
+    for (B, Ci, Co, n, lo, hi, I) in [(1, 20, 20, 720, 32, 32, 32), (2, 7, 13, 720, 12, 12, 9), (1, 5, 6, 50, 4, 4, 7)]:
+        xm = torch.randn(B, Ci, lo + hi, I, 2)
+        w = torch.randn(Ci, Co, (lo + hi) * I, 2)
+        ref = _mix_c2c_reference(xm, w, n, lo, hi, 1.0 / n)
+        out = torch.ops.amd_dft.fno_mix_c2c(xm.to(device), w.to(device), n, lo, hi, 1.0 / n)
+        assert rel_l2(out.cpu(), ref) < 2e-6, (B, Ci, Co, n, lo, hi, I)

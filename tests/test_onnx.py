@@ -187,7 +187,7 @@ def test_export_fast_fno_model_amd_nodes():
     doms = {n.domain for n in model.graph.node}
     assert "com.amd.dft" in doms
     ops = {n.op_type for n in model.graph.node if n.domain == "com.amd.dft"}
-    assert {"dftw_r2c", "c2c_axis", "fno_mix", "fno_c2r_pw", "fno_pointwise"} <= ops
+    assert {"dftw_r2c", "c2c_axis", "fno_mix_c2c", "fno_c2r_pw", "fno_pointwise"} <= ops
     (y,) = OnnxGraph(data, device="cpu").run(x)
     assert torch.allclose(y, ref, atol=1e-5)
 
