@@ -80,6 +80,13 @@ __device__ __forceinline__ void diag_guard() {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+#ifndef AFNO_TW64
+#define AFNO_TW64 0  // diagnostic builds only: pass-1 twiddles read as one 64-bit LDS load each (the form the
+                     // -O3 vectorizer produces: ds_read2_b64 / ds_read_b64 instead of ds_read2_b32)
+#endif
+#ifndef AFNO_EPI64
+#define AFNO_EPI64 0  // diagnostic builds only: GEMM-1 epilogue 8-byte pieces stored as one 64-bit LDS store
+#endif
 #ifndef AFNO_ABLATE
 #define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs,
                        // 4 = x3 GEMM B fragments of k-step 0 reused (no weight loads after the first)
@@ -181,7 +188,12 @@ __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __
         const int k = j % Ns;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
+          if constexpr (AFNO_TW64) {
+            const uint64_t t = *reinterpret_cast<const uint64_t*>(tw + (r - 1) * Ns + k);
+            v[q][r] = c_mul(v[q][r], __builtin_bit_cast(float2, t));
+          } else {
+            v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
+          }
         }
       }
       Dft<R>::run(v[q]);
@@ -349,6 +361,14 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
 #pragma unroll
       for (int mi = 0; mi < S::MT; ++mi) {
         const int m = mi * 16 + (lane & 15);
+        if constexpr (AFNO_EPI64) {
+          const uint2 u = make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
+                                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
+                                     static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][2] + bias.z, 0.f))) |
+                                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][3] + bias.w, 0.f))) << 16));
+          *reinterpret_cast<uint64_t*>(A + m * AP + n0) = (static_cast<uint64_t>(u.y) << 32) | u.x;
+          continue;
+        }
         *reinterpret_cast<uint2*>(A + m * AP + n0) =
             make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
                            (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
@@ -486,6 +506,16 @@ __device__ __forceinline__ void put_split2(uint16_t* Ahi, uint16_t* Alo, int idx
 __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx, float a, float b, float c, float d) {
   const uint16_t ha = f2bf16(a), hb = f2bf16(b), hc = f2bf16(c), hd = f2bf16(d);
   const auto up = [](uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); };
+  if constexpr (AFNO_EPI64) {
+    const uint64_t h = (static_cast<uint64_t>(static_cast<uint32_t>(hc) | (static_cast<uint32_t>(hd) << 16)) << 32) |
+                       (static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16));
+    const uint64_t l = (static_cast<uint64_t>(static_cast<uint32_t>(f2bf16(c - up(hc))) |
+                                              (static_cast<uint32_t>(f2bf16(d - up(hd))) << 16)) << 32) |
+                       (static_cast<uint32_t>(f2bf16(a - up(ha))) | (static_cast<uint32_t>(f2bf16(b - up(hb))) << 16));
+    *reinterpret_cast<uint64_t*>(Ahi + idx) = h;
+    *reinterpret_cast<uint64_t*>(Alo + idx) = l;
+    return;
+  }
   *reinterpret_cast<uint2*>(Ahi + idx) = make_uint2(static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16),
                                                     static_cast<uint32_t>(hc) | (static_cast<uint32_t>(hd) << 16));
   *reinterpret_cast<uint2*>(Alo + idx) =

@@ -7,8 +7,8 @@
 // have to be re-read for every row tile (W x 2m complex, 368 KB for 1440 x 32 -- more L2
 // traffic than x itself), so it is factored instead:
 //   k = KB*s + k',   e^{-2 pi i n k/W} = e^{-2 pi i n KB s/W} * e^{-2 pi i n k'/W}
-// The KB x 16G block B0[k'][n] (bf16 hi/lo split, so the twiddles are exact to ~2^-17 for fp32
-// input; bf16 input uses the hi plane only, see DFTW_BF_TWLO) lives in registers for the whole kernel; each KB-block of x contributes  ph_s[n] * (x_s . B0)  with
+// The KB x 16G block B0[k'][n] (bf16 hi/lo split, so the twiddles are exact to ~2^-17) lives
+// in registers for the whole kernel; each KB-block of x contributes  ph_s[n] * (x_s . B0)  with
 // one complex scale of the MFMA accumulator per block and mode.
 //
 //   x:   [R, W] bf16 or fp32 rows (contiguous)     out: [R, m] complex fp32 (re, im)
@@ -36,13 +36,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNKS = kDftGemmKB / 32;  // 32-deep MFMA k-steps per block
-#ifndef DFTW_BF_TWLO
-// bf16 input: the twiddles' lo plane as well (products a * (b_hi + b_lo), ~2^-17 twiddles).  Off:
-// bf16 MFMA operands on both sides, fp32 accumulation -- the input is bf16 already, and the
-// forward transform then costs 2 instead of 4 MFMAs per k-step and mode tile
-// (FNO block: profiles/fno_r3_hionly.txt)
-#define DFTW_BF_TWLO 0
-#endif
 
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
@@ -78,8 +71,7 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          if (!BF || DFTW_BF_TWLO || h == 0) bfr[kk][g][c][h] = b0[(((kk * G + g) * 2 + c) * 2 + h) * 64 + lane];
+        for (int h = 0; h < 2; ++h) bfr[kk][g][c][h] = b0[(((kk * G + g) * 2 + c) * 2 + h) * 64 + lane];
   f32x4 are[G], aim[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) are[g] = aim[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -134,14 +126,13 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
 #pragma unroll
           for (int t = 0; t < NR; ++t) buf[j][kk][t] = Raw{};
         if constexpr (BF) {
-          // bf16 input: bf16 twiddles (hi plane only; DFTW_BF_TWLO=1 adds the lo plane)
           const bf16x8 a = __builtin_bit_cast(bf16x8, buf[j][kk][0]);
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][0][0], tr[g], 0, 0, 0);
-            if (DFTW_BF_TWLO) tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][0][1], tr[g], 0, 0, 0);
+            tr[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][0][1], tr[g], 0, 0, 0);
             ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][0], ti[g], 0, 0, 0);
-            if (DFTW_BF_TWLO) ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][1], ti[g], 0, 0, 0);
+            ti[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[kk][g][1][1], ti[g], 0, 0, 0);
           }
         } else {
           const f32x4 f0 = __builtin_bit_cast(f32x4, buf[j][kk][0]), f1 = __builtin_bit_cast(f32x4, buf[j][kk][NR - 1]);

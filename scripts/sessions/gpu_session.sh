@@ -3,7 +3,7 @@
 # placement A/B, the FFT latency and the headline bench.  Every GPU step has its own time limit;
 # the session stops at the first abnormal exit (timeout, signal, fault).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # step <tag> <seconds> <cmd...>

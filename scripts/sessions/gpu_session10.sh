@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 10 (round 3): full GPU tier, smoke, headline bench, kernel table of the final state.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 11 (round 3): bf16 AFNO kernel with the transposed GEMM-1 epilogue.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 12 (round 3): FNO layer tail phase clocks.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 timeout -k 10 300 hipcc -O3 --offload-arch=gfx950 -munsafe-fp-atomics -fno-slp-vectorize -DFNO_STAMPS -Icsrc \
   bench/fno_stamps.hip -o /tmp/fno_stamps || exit 1

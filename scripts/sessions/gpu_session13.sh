@@ -3,7 +3,7 @@
 # clocks, and the FNO block A/B/C: + lane-transposed 16-byte bf16 stores (in-tree), without them
 # (build_diag/fnonoswap), the previous build (build_diag/fnoprev).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

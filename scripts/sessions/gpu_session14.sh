@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 14 (round 3, re-entry): full GPU tier + smoke + bench on the in-tree build, and the FNO block bench.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 15 (round 3): per-kernel tables of the FNO block (config 3) and of rfft2/irfft2 720x1440 (config 2).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fno -o fno -- \

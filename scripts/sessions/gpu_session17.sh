@@ -2,7 +2,7 @@
 # GPU session 18 (round 3): FNO block, batched mixing-gather loads and bf16 dftw on hi-only twiddles (after session 17:
 # mixing fused into the inverse H transform, bf16 c2r_pw on hi-only spectra) -- tests, bench, kernel table.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 step() {

@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU session 19 (round 3): (1) FNO block after the mixing-gather load batching and bf16 dftw on hi-only
-# twiddles; (2) rfft2/irfft2 720x1440 A/B of the FFT radix plans: default (1440: 10,12,12 at 144 threads;
+# GPU session 19 (round 3): (1) FNO block after the mixing-gather load batching (bf16 dftw on hi-only twiddles
+# was tried and reverted: the standalone bf16 DFT op lost its ~1e-6 accuracy); (2) rfft2/irfft2 720x1440 A/B of the FFT radix plans: default (1440: 10,12,12 at 144 threads;
 # 720 cols: 8,9,10 at 90 x 4) vs more threads per FFT (1440: 5,6,6,8 at 288; 720 cols: 4,4,5,9 at 180 x 4).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 step() {

@@ -2,7 +2,7 @@
 # GPU session 2 (round 3): in-step marginal cost of every fp32 block stage (no profiler), the
 # AFNO -O3 bisection, and the FFT after the column-layout change.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

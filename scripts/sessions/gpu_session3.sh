@@ -2,7 +2,7 @@
 # GPU session 3 (round 3): FNO staged-epilogue A/B, AFNO vectorizer-on build with device LDS checks,
 # GEMM per-call time under sustained load, IPC push interference.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

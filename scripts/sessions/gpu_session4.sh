@@ -3,7 +3,7 @@
 # GPU test tier, fp32 headline with the fc2-fused LayerNorm statistics (A/B against the ln_stats pass),
 # and a kernel-time profile of the replayed step.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

@@ -2,7 +2,7 @@
 # GPU session 5 (round 3): AFNO x3 phase clocks and the transposed-GEMM1 epilogue A/B, then the
 # from-source CI (compile on the box + both tiers).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 for t in 1 0; do

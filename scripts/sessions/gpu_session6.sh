@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 6 (round 3): AFNO H-filter with LDS twiddles (phase clocks + timing), spectral GPU tests, bench.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

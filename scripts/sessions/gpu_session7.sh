@@ -2,7 +2,7 @@
 # GPU session 7 (round 3): last block's fc2 writing the head operand as split pairs; x3 GEMM bench with full
 # fp32 operands (non-zero lo halves) vs the old zero-lo harness.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {

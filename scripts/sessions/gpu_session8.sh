@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU session 8 (round 3): persistent AFNO x3 kernel with the next tile's input DMA'd into LDS.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {
