@@ -191,9 +191,9 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
       if (x.ok0 && s >= 0) {
         const int32_t off = x.cc * a.Si_in + s * a.Sn_in;
         const int32_t sx = static_cast<int32_t>(a.So_in), sw = static_cast<int32_t>(a.So_in) * a.mix_cout;
-        // batches of 10 channels: all 20 loads of a batch in flight before the first FMA
+        // batches of 20 channels: all 40 loads of a batch in flight before the first FMA
         // (clamped channel index, masked product) -- one L2 round trip per batch
-        constexpr int U = 10;
+        constexpr int U = 20;
         for (int i0 = 0; i0 < a.mix_cin; i0 += U) {
           float2 xv[U], wv[U];
 #pragma unroll
@@ -536,7 +536,14 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
 }
 
 // ------------------------------------------------------------------ config table
+// The first entry of a length fixes its plan's radix order (fixed_radices; MI_DFT_FFT_RADICES picks
+// another configured order for A/B runs).  1440 rows: (5, 6, 6, 8) at 288 threads -- one butterfly
+// of 5..8 points per thread per pass, ~4.5 waves per transform -- beat (10, 12, 12) at 144 threads
+// (10-12 points per thread, ~2.3 waves) on rfft2 720x1440: 12.27-12.32 vs 12.70-12.78 us, irfft2
+// unchanged (12.14-12.23 vs 12.13-12.14); 180-thread (4, 4, 5, 9) 720-point columns lost
+// (irfft2 12.36-12.42): profiles/fft_plans_r3.txt.
 #define AMD_DFT_FIXED_CONFIGS(X)          \
+  X(1440, false, 288, 1, 5, 6, 6, 8)      \
   X(1440, false, 144, 1, 10, 12, 12)      \
   X(720, false, 90, 2, 8, 9, 10)          \
   X(1024, false, 128, 1, 8, 8, 16)        \
@@ -545,8 +552,6 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(256, false, 16, 4, 16, 16)            \
   X(720, true, 90, 4, 8, 9, 10)           \
   X(720, true, 90, 2, 8, 9, 10)           \
-  X(1440, false, 288, 1, 5, 6, 6, 8)      \
-  X(720, true, 180, 4, 4, 4, 5, 9)        \
   X(720, true, 45, 8, 8, 9, 10)           \
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \

@@ -46,6 +46,7 @@
 // are discarded) and 2BS / 16 column tiles over the 4 waves.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -82,7 +83,12 @@ __device__ __forceinline__ void diag_guard() {
 }
 #ifndef AFNO_TW64
 #define AFNO_TW64 0  // diagnostic builds only: pass-1 twiddles read as one 64-bit LDS load each (the form the
-                     // -O3 vectorizer produces: ds_read2_b64 / ds_read_b64 instead of ds_read2_b32)
+                     // -O3 vectorizer produces: ds_read2_b64 / ds_read_b64 instead of ds_read2_b32);
+                     // bit 0: forward FFT_H pass 1, bit 1: inverse FFT_H pass 1
+#endif
+#ifndef AFNO_TWCHECK
+#define AFNO_TWCHECK 0  // diagnostic builds only (with AFNO_TW64): every 64-bit twiddle read is re-read as two
+                        // volatile 32-bit loads; a mismatch poisons the butterfly with NaN
 #endif
 #ifndef AFNO_EPI64
 #define AFNO_EPI64 0  // diagnostic builds only: GEMM-1 epilogue 8-byte pieces stored as one 64-bit LDS store
@@ -174,7 +180,7 @@ struct HPass {
   static constexpr int Q = (NB + kNT - 1) / kNT;
 };
 
-template <int R, int L, int NP, int Ns, int Q>
+template <int R, int L, int NP, int Ns, int Q, int SITE = 0>
 __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
   using P = HPass<R, L, NP>;
   static_assert(P::Q == Q, "pass geometry");
@@ -188,9 +194,15 @@ __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __
         const int k = j % Ns;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          if constexpr (AFNO_TW64) {
+          if constexpr ((AFNO_TW64 & SITE) != 0) {
             const uint64_t t = *reinterpret_cast<const uint64_t*>(tw + (r - 1) * Ns + k);
-            v[q][r] = c_mul(v[q][r], __builtin_bit_cast(float2, t));
+            float2 tf = __builtin_bit_cast(float2, t);
+            if constexpr (AFNO_TWCHECK) {
+              const volatile float* f = reinterpret_cast<const volatile float*>(tw + (r - 1) * Ns + k);
+              const float a = f[0], b = f[1];
+              if (a != tf.x || b != tf.y) tf = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+            }
+            v[q][r] = c_mul(v[q][r], tf);
           } else {
             v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
           }
@@ -326,7 +338,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q, 1>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -450,7 +462,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q, 2>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -659,7 +671,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
     __syncthreads();
     AFNO_STAMP(3, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q, 1>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -776,7 +788,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q, 2>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -839,6 +851,13 @@ const AfnoInstance* find_instance(int H, int bs) {
 }
 
 void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a, void* stream) {
+  // MI_DFT_AFNO_LDS_EXTRA=<bytes>: diagnostic -- allocate that much dynamic LDS beyond what the
+  // kernel addresses (scripts/diag/afno_race_diag.py bisection)
+  static const int64_t extra = [] {
+    const char* e = std::getenv("MI_DFT_AFNO_LDS_EXTRA");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+  }();
+  lds += extra;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(lds));
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));
