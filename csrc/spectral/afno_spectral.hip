@@ -10,22 +10,30 @@
 // grid, and is faster than the -O1 build used before (bf16 452 vs 477 us, bf16x3 842 vs
 // 881 us at [32, 90, 46, 768]; scripts/diag/afno_race_diag.py, afno_poison_diag.py,
 // profiles/afno_o1_fix_r2.txt).
-// Round-3 bisection (profiles/afno_o3_bisect_r3.txt): 32 wait states after every MFMA k-step
-// group or after each GEMM (AFNO_DIAG=1/2) do NOT cure the vectorizer-on build, so it is no
-// MFMA read/write hazard; a static dataflow check of the compiled code
-// (scripts/diag/barrier_lds_check.py) finds no s_barrier reachable with LDS operations in
-// flight, in either build; the fp32 W-transforms (afno_wfft.hip) use the same 16-byte
-// ds_read/write_b128 staging at 3 workgroups per CU and are exact, and in the bf16 kernel the
-// vectorizer changes no LDS or global access at all -- only the kernel-argument scalar loads
-// (merged into s_load_dwordx4/x8, one moved into a conditional block) and the schedule.  The
-// cause is therefore a code-generation difference outside the memory operations, not a data
-// race in this source.  Two further leads were tested and refuted: an MI_DFT_DEVICE_CHECKS build
-// with the vectorizer on (every 16-byte fp32 staging access checked for alignment and bounds)
-// reproduces the errors without a single failed check, and the vectorizer-on code with every
-// v_swap_b32 (the one instruction it adds that no exact kernel here contains) rewritten as a
-// three-XOR swap still fails (scripts/diag/afno_swap_xor.sh).  The vectorizer stays off for this
-// file, the determinism screen (tests/test_determinism_gpu.py) runs every kernel family at
-// co-resident grids, and MI_DFT_DEVICE_CHECKS builds check every 16-byte staging access.
+// Root cause, as far as the instruction level (profiles/afno_o3_bisect_r3.txt, round 3): not a data
+// race in this source and not the memory operations.  Vectorizer-OFF builds that reproduce one of
+// its changes at a time isolate the trigger: the pass-1 twiddle multiply (forward or inverse FFT_H,
+// either alone) issued as `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` -- the high half (imaginary part)
+// of the LDS-loaded twiddle pair broadcast by op_sel -- instead of the shipped form (the imaginary
+// part first copied into its own pair, op_sel_hi:[1,0]).  With that consumer the kernels fail
+// whether the pair is loaded by ds_read_b64 (the vectorizer's form) or ds_read2_b32 (the shipped
+// load), with a full s_waitcnt lgkmcnt(0) and 16 further wait states before the multiply, and with
+// extra LDS allocated behind the table; with the same 64-bit load consumed by unpacked fp32 FMAs,
+// or by the packed form after a re-read check that proves the loaded values right, they are exact.
+// The GEMM-1 epilogue's 64-bit LDS writes (the vectorizer's other change) are harmless.  The
+// instruction alone is correct: a minimal kernel (scripts/diag/opsel_lds_repro.hip) issuing it on
+// LDS-loaded pairs at 1-4+ co-resident workgroups per CU gives 0 mismatches in 2.6e10 products,
+// and afno_wfft.hip issues it 88 times on global-loaded pairs and is exact.  What the kernel context
+// adds is not identified; the failure is therefore treated as a code-generation hazard of this
+// packed-FP32 form in these kernels (outside the source's semantics: no reordering of any memory
+// access is involved), and scripts/diag/opsel_lds_check.py flags the pattern in compiled code.
+// Earlier rounds had ruled out MFMA hazards (32 wait states after every MFMA group, AFNO_DIAG),
+// barriers with LDS operations in flight (scripts/diag/barrier_lds_check.py), misaligned or
+// out-of-bounds 16-byte LDS accesses (MI_DFT_DEVICE_CHECKS) and v_swap_b32.  The vectorizer stays
+// off for this file (no such instruction is emitted), the determinism screen
+// (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids, and
+// tests/test_codegen.py checks that the shipped flags emit no op_sel:[0,1]
+// packed multiply of an LDS-loaded pair.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
@@ -87,8 +95,12 @@ __device__ __forceinline__ void diag_guard() {
                      // bit 0: forward FFT_H pass 1, bit 1: inverse FFT_H pass 1
 #endif
 #ifndef AFNO_TWCHECK
-#define AFNO_TWCHECK 0  // diagnostic builds only (with AFNO_TW64): every 64-bit twiddle read is re-read as two
-                        // volatile 32-bit loads; a mismatch poisons the butterfly with NaN
+#define AFNO_TWCHECK 0  // diagnostic builds only (with AFNO_TW64): 1 = every 64-bit twiddle read is re-read as
+                        // two volatile 32-bit loads, a mismatch poisons the butterfly with NaN; 2 = s_waitcnt
+                        // lgkmcnt(0) right after each read; 3 = unpacked (scalar fp32) twiddle multiply; 4 / 5 =
+                        // the read as inline-asm ds_read_b64 + full wait, with the unpacked / packed multiply;
+                        // 6 = as 5 plus 16 wait states (2 x s_nop 7) between the wait and the packed multiply;
+                        // 7 = as 5 with the pair read by ds_read2_b32
 #endif
 #ifndef AFNO_EPI64
 #define AFNO_EPI64 0  // diagnostic builds only: GEMM-1 epilogue 8-byte pieces stored as one 64-bit LDS store
@@ -195,14 +207,37 @@ __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __
 #pragma unroll
         for (int r = 1; r < R; ++r) {
           if constexpr ((AFNO_TW64 & SITE) != 0) {
-            const uint64_t t = *reinterpret_cast<const uint64_t*>(tw + (r - 1) * Ns + k);
+            uint64_t t;
+            if constexpr (AFNO_TWCHECK >= 4) {  // the 64-bit read as inline asm, fully waited
+              typedef __attribute__((address_space(3))) const float2 lds_f2;
+              const uint32_t addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_f2*)(tw + (r - 1) * Ns + k)));
+              if constexpr (AFNO_TWCHECK == 7)  // the pair as two 32-bit LDS reads (ds_read2_b32), same consumer
+                asm volatile("ds_read2_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(addr) : "memory");
+              else if constexpr (AFNO_TWCHECK == 6)  // + 16 wait states before the first consumer
+                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7" : "=v"(t) : "v"(addr) : "memory");
+              else
+                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(addr) : "memory");
+            } else {
+              t = *reinterpret_cast<const uint64_t*>(tw + (r - 1) * Ns + k);
+            }
             float2 tf = __builtin_bit_cast(float2, t);
-            if constexpr (AFNO_TWCHECK) {
+            if constexpr (AFNO_TWCHECK == 1) {
               const volatile float* f = reinterpret_cast<const volatile float*>(tw + (r - 1) * Ns + k);
               const float a = f[0], b = f[1];
               if (a != tf.x || b != tf.y) tf = make_float2(__builtin_nanf(""), __builtin_nanf(""));
             }
-            v[q][r] = c_mul(v[q][r], tf);
+            if constexpr (AFNO_TWCHECK == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (AFNO_TWCHECK == 3 || AFNO_TWCHECK == 4) {  // scalar (unpacked) fp32 twiddle multiply
+              const float r0 = v[q][r].re[0], r1 = v[q][r].re[1], i0 = v[q][r].im[0], i1 = v[q][r].im[1];
+              const float a0 = fmaf(r0, tf.x, -i0 * tf.y), b0 = fmaf(r0, tf.y, i0 * tf.x);
+              const float a1 = fmaf(r1, tf.x, -i1 * tf.y), b1 = fmaf(r1, tf.y, i1 * tf.x);
+              v[q][r].re[0] = a0;
+              v[q][r].re[1] = a1;
+              v[q][r].im[0] = b0;
+              v[q][r].im[1] = b1;
+            } else {
+              v[q][r] = c_mul(v[q][r], tf);
+            }
           } else {
             v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
           }

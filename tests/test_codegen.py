@@ -1,0 +1,39 @@
+"""Code-generation guard for the AFNO spectral kernels (CPU tier: hipcc cross-compiles gfx950 here).
+
+The -O3 load/store vectorizer made both AFNO kernels nondeterministically wrong at co-resident grids; the round-3
+bisection (profiles/afno_o3_bisect_r3.txt) pinned the trigger to the pass-1 twiddle multiply issued as
+`v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` on an LDS-loaded twiddle pair.  This test compiles afno_spectral.hip with the
+shipped per-file flags and checks the device code contains no such instruction (scripts/diag/opsel_lds_check.py),
+and that the vectorizer-on build does (so the scanner still sees the pattern it guards against)."""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts", "diag"))
+HIPCC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+
+
+def _compile(tmp_path, extra):
+    from tensorrt_dft_plugins_amd import _build
+
+    src = os.path.join(ROOT, "csrc", "spectral", "afno_spectral.hip")
+    out = tmp_path / "afno.s"
+    cmd = [HIPCC, "-S", "--cuda-device-only", "-std=c++17", "-O3", "-x", "hip", f"--offload-arch={_build.ARCH}",
+           "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "csrc")]
+    cmd += _build._file_flags(src) + extra + [src, "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    return str(out)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC) and shutil.which("hipcc") is None, reason="hipcc not available")
+def test_afno_kernels_emit_no_opsel_high_lds_packed_multiply(tmp_path):
+    import opsel_lds_check as chk
+
+    shipped = chk.scan(_compile(tmp_path, []))
+    assert shipped and sum(t for _, t in shipped.values()) == 0 and sum(l for l, _ in shipped.values()) == 0, shipped
+    vec_on = chk.scan(_compile(tmp_path, ["-mllvm", "-amdgpu-load-store-vectorizer=1"]))
+    assert sum(l for l, _ in vec_on.values()) > 0, "scanner no longer sees the pattern in the vectorizer-on build"
