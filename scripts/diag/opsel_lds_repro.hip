@@ -23,11 +23,18 @@
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-template <int MODE, bool SEQ>
-__global__ void __launch_bounds__(256) repro(const float2* __restrict__ gtab, unsigned* __restrict__ bad, int lds_bytes,
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// CO: 512-thread workgroups whose waves 0-3 run a dependent MFMA chain for the whole kernel while waves 4-7 (one per
+// SIMD beside an MFMA wave) run the packed-multiply check -- the co-execution the AFNO kernels see when a co-resident
+// workgroup is in its GEMM phase
+template <int MODE, bool SEQ, bool CO, int FORM = 0>
+__global__ void __launch_bounds__(512) repro(const float2* __restrict__ gtab, unsigned* __restrict__ bad, int lds_bytes,
                                              int iters) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
+  const int ct = CO ? tid - 256 : tid;  // checker thread index
   const int ntab = 81;
   float2* tab = reinterpret_cast<float2*>(smem + lds_bytes - ntab * 8);  // the table at the top, like the AFNO twl
   if (tid < ntab) tab[tid] = gtab[tid];
@@ -36,6 +43,22 @@ __global__ void __launch_bounds__(256) repro(const float2* __restrict__ gtab, un
   const int nbusy = (lds_bytes - ntab * 8) / 16;
   for (int i = tid; i < nbusy; i += 256) busy[i] = make_float4(i, -i, 0.5f * i, 1.f);
   __syncthreads();
+  if constexpr (CO) {
+    if (tid < 256) {  // MFMA waves
+      bf16x8 x, y;
+      for (int j = 0; j < 8; ++j) {
+        x[j] = static_cast<__bf16>(0.001f * (tid + j));
+        y[j] = static_cast<__bf16>(0.002f * (tid - j));
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int it = 0; it < iters * 24; ++it) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, x, acc, 0, 0, 0);
+      }
+      if (acc[0] == 12345.f) atomicAdd(bad, 1u << 30);  // keep the chain live
+      return;
+    }
+  }
   unsigned mism = 0;
   f2v a = {1.0f + 0.001f * tid, -2.0f + 0.003f * tid};
   f2v b = {0.5f - 0.002f * tid, 1.5f + 0.001f * tid};
@@ -55,7 +78,27 @@ __global__ void __launch_bounds__(256) repro(const float2* __restrict__ gtab, un
           asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(addr) : "memory");
       }
       f2v p;
-      if constexpr (SEQ) {
+      if constexpr (FORM != 0) {
+        // single packed product next to the MFMA waves, in one of four forms (expected a * t.y for both lanes):
+        //  1: v_pk_mul op_sel:[0,1]            (src1 high half -> both lanes; the failing AFNO form)
+        //  2: v_pk_mul op_sel_hi:[1,0] on (t.y, t.y) copied by v_mov   (the shipped AFNO form)
+        //  3: v_pk_mul op_sel:[1,0] op_sel_hi:[1,1] with the operands swapped (src0 high half -> both lanes)
+        //  4: v_pk_fma op_sel:[0,1,0] with a zero addend   (src1 high half, FMA instead of MUL)
+        if constexpr (FORM == 1) {
+          asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1]" : "=v"(p) : "v"(a), "v"(t));
+        } else if constexpr (FORM == 2) {
+          f2v ty;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(ty.x) : "v"(t.y));
+          ty.y = 0.f;
+          asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(p) : "v"(a), "v"(ty));
+        } else if constexpr (FORM == 3) {
+          asm volatile("v_pk_mul_f32 %0, %2, %1 op_sel:[1,0]" : "=v"(p) : "v"(a), "v"(t));
+        } else {
+          const f2v z = {0.f, 0.f};
+          asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0]" : "=v"(p) : "v"(a), "v"(t), "v"(z));
+        }
+        mism += (p.x != a.x * t.y || p.y != a.y * t.y) ? 1u : 0u;
+      } else if constexpr (SEQ) {
         // the AFNO twiddle multiply exactly as the failing builds issue it: two op_sel:[0,1] products, then the two
         // packed FMAs that consume them (3 and 3 instructions later, no wait states in between)
         f2v q1, q2, re, im;
@@ -102,11 +145,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bad, sizeof(unsigned)));
   CK(hipMemcpy(gt, h.data(), 81 * sizeof(float2), hipMemcpyHostToDevice));
   CK(hipMemset(bad, 0, sizeof(unsigned)));
-  const bool seq = argc > 5 && std::atoi(argv[5]) != 0;
-  auto k = seq ? (mode == 1 ? repro<1, true> : (mode == 2 ? repro<2, true> : repro<0, true>))
-               : (mode == 1 ? repro<1, false> : (mode == 2 ? repro<2, false> : repro<0, false>));
+  const int seqa = argc > 5 ? std::atoi(argv[5]) : 0;  // 0: single product, 1: full sequence, 2: + MFMA co-runner waves
+  const bool seq = seqa != 0;
+  // seq 11..14: MFMA co-runner waves + single product in form 1..4 (global-loaded table)
+  auto k = seqa == 11 ? repro<1, false, true, 1> : seqa == 12 ? repro<1, false, true, 2>
+         : seqa == 13 ? repro<1, false, true, 3> : seqa == 14 ? repro<1, false, true, 4>
+         : seqa == 2 ? (mode == 1 ? repro<1, true, true> : (mode == 2 ? repro<2, true, true> : repro<0, true, true>))
+           : seq ? (mode == 1 ? repro<1, true, false> : (mode == 2 ? repro<2, true, false> : repro<0, true, false>))
+                 : (mode == 1 ? repro<1, false, false> : (mode == 2 ? repro<2, false, false> : repro<0, false, false>));
+  const int nthr = seqa >= 2 ? 512 : 256;
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(k, dim3(nwg), dim3(256), lds, 0, gt, bad, lds, iters);
+  for (int rep = 0; rep < 5; ++rep) hipLaunchKernelGGL(k, dim3(nwg), dim3(nthr), lds, 0, gt, bad, lds, iters);
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   unsigned nb = 0;
