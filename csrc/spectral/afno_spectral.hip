@@ -10,30 +10,24 @@
 // grid, and is faster than the -O1 build used before (bf16 452 vs 477 us, bf16x3 842 vs
 // 881 us at [32, 90, 46, 768]; scripts/diag/afno_race_diag.py, afno_poison_diag.py,
 // profiles/afno_o1_fix_r2.txt).
-// Root cause, as far as the instruction level (profiles/afno_o3_bisect_r3.txt, round 3): not a data
-// race in this source and not the memory operations.  Vectorizer-OFF builds that reproduce one of
-// its changes at a time isolate the trigger: the pass-1 twiddle multiply (forward or inverse FFT_H,
-// either alone) issued as `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` -- the high half (imaginary part)
-// of the LDS-loaded twiddle pair broadcast by op_sel -- instead of the shipped form (the imaginary
-// part first copied into its own pair, op_sel_hi:[1,0]).  With that consumer the kernels fail
-// whether the pair is loaded by ds_read_b64 (the vectorizer's form) or ds_read2_b32 (the shipped
-// load), with a full s_waitcnt lgkmcnt(0) and 16 further wait states before the multiply, and with
-// extra LDS allocated behind the table; with the same 64-bit load consumed by unpacked fp32 FMAs,
-// or by the packed form after a re-read check that proves the loaded values right, they are exact.
-// The GEMM-1 epilogue's 64-bit LDS writes (the vectorizer's other change) are harmless.  The
-// instruction alone is correct: a minimal kernel (scripts/diag/opsel_lds_repro.hip) issuing it on
-// LDS-loaded pairs at 1-4+ co-resident workgroups per CU gives 0 mismatches in 2.6e10 products,
-// and afno_wfft.hip issues it 88 times on global-loaded pairs and is exact.  What the kernel context
-// adds is not identified; the failure is therefore treated as a code-generation hazard of this
-// packed-FP32 form in these kernels (outside the source's semantics: no reordering of any memory
-// access is involved), and scripts/diag/opsel_lds_check.py flags the pattern in compiled code.
-// Earlier rounds had ruled out MFMA hazards (32 wait states after every MFMA group, AFNO_DIAG),
-// barriers with LDS operations in flight (scripts/diag/barrier_lds_check.py), misaligned or
-// out-of-bounds 16-byte LDS accesses (MI_DFT_DEVICE_CHECKS) and v_swap_b32.  The vectorizer stays
-// off for this file (no such instruction is emitted), the determinism screen
-// (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids, and
-// tests/test_codegen.py checks that the shipped flags emit no op_sel:[0,1]
-// packed multiply of an LDS-loaded pair.
+// Root cause (round 3, profiles/afno_o3_bisect_r3.txt): a gfx950 packed-FP32 fault, not a race in
+// this source.  With the vectorizer on, the pass-1 twiddle multiply is issued as
+// `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` (the high half of the twiddle pair broadcast through
+// src1's op_sel).  Packed-FP32 instructions that select the high half of src1 through op_sel
+// (v_pk_mul_f32 and v_pk_fma_f32 alike) return wrong products while another wave on the same SIMD
+// is executing MFMAs: scripts/diag/opsel_lds_repro.hip, a minimal kernel whose waves 0-3 run an MFMA
+// chain while waves 4-7 check packed products against unpacked ones, sees 7.7 % of those products
+// wrong (0 without the MFMA waves; 0 with op_sel on src0, or with the operand first copied to its
+// own pair, which is what the vectorizer-off build emits).  In this file the MFMA co-runner is the
+// co-resident workgroup's GEMM phase -- hence 'only when two or more workgroups share a CU'.  The
+// vectorizer-off bisection builds agree: the single change 'twiddle consumed through op_sel:[0,1]'
+// fails with either LDS load form, after a full s_waitcnt plus 16 wait states, with extra LDS
+// behind the table; the GEMM-1 epilogue's 64-bit LDS writes are harmless; unpacked FMAs on the
+// same loaded values are exact.  Guards: this file builds with the vectorizer off (no such
+// instruction), tests/test_codegen.py asserts that for this file and that no kernel of the built
+// library contains both an MFMA and a src1-high packed-FP32 op (scripts/diag/scan_so.py; the AFNO
+// W-transforms, the only kernels with the packed form, contain no MFMA), and the determinism
+// screen (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs

@@ -4,7 +4,8 @@ The -O3 load/store vectorizer made both AFNO kernels nondeterministically wrong 
 bisection (profiles/afno_o3_bisect_r3.txt) pinned the trigger to the pass-1 twiddle multiply issued as
 `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` on an LDS-loaded twiddle pair.  This test compiles afno_spectral.hip with the
 shipped per-file flags and checks the device code contains no such instruction (scripts/diag/opsel_lds_check.py),
-and that the vectorizer-on build does (so the scanner still sees the pattern it guards against)."""
+and that the vectorizer-on build does (so the scanner still sees the pattern it guards against); and scans every
+kernel of the built library for the MFMA + src1-high packed-FP32 combination (scripts/diag/scan_so.py)."""
 import os
 import shutil
 import subprocess
@@ -37,3 +38,20 @@ def test_afno_kernels_emit_no_opsel_high_lds_packed_multiply(tmp_path):
     assert shipped and sum(t for _, t in shipped.values()) == 0 and sum(l for l, _ in shipped.values()) == 0, shipped
     vec_on = chk.scan(_compile(tmp_path, ["-mllvm", "-amdgpu-load-store-vectorizer=1"]))
     assert sum(l for l, _ in vec_on.values()) > 0, "scanner no longer sees the pattern in the vectorizer-on build"
+
+
+SO = os.path.join(ROOT, "tensorrt_dft_plugins_amd", "_C.so")
+
+
+@pytest.mark.skipif(not os.path.exists(SO), reason="library not built")
+def test_no_kernel_mixes_mfma_with_src1_high_packed_fp32():
+    """Every gfx950 kernel in the shipped library: none contains both an MFMA and a packed-FP32 instruction that
+    takes the high half of src1 via op_sel -- on MI355X the latter returns wrong results while another wave on the
+    same SIMD runs MFMAs (scripts/diag/opsel_lds_repro.hip: 7.7 % of products; src0 op_sel and no op_sel are
+    unaffected).  The kernels that do contain the packed form (AFNO W-transforms) contain no MFMA."""
+    import scan_so
+
+    r = scan_so.scan(SO)
+    assert len(r) > 100 and sum(1 for v in r.values() if v[0]) > 10, "disassembly found too few kernels"
+    both = {k: v for k, v in r.items() if v[0] and v[1]}
+    assert not both, both
