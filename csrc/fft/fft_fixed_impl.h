@@ -552,9 +552,6 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(256, false, 16, 4, 16, 16)            \
   X(720, true, 90, 4, 8, 9, 10)           \
   X(720, true, 90, 2, 8, 9, 10)           \
-  X(720, true, 90, 4, 10, 9, 8)           \
-  X(720, true, 90, 4, 9, 10, 8)           \
-  X(1440, false, 288, 1, 8, 6, 6, 5)      \
   X(720, true, 45, 8, 8, 9, 10)           \
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \
