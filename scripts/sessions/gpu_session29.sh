@@ -21,3 +21,7 @@ t=open('gpurun_out/s29_${t}_$rep.log').read(); j=json.loads(t[t.index('{'):t.rin
 print('$t rep $rep rfft2 %.2f irfft2 %.2f'%(j['amd_rfft2']['graph']['median_us'], j['amd_irfft2']['graph']['median_us']))"
   done
 done
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s29_smoke.log 2>&1 || { tail -5 gpurun_out/s29_smoke.log; exit 1; }
+tail -1 gpurun_out/s29_smoke.log
+timeout -k 10 600 python -u bench.py > gpurun_out/s29_bench.log 2>&1 || { tail -5 gpurun_out/s29_bench.log; exit 1; }
+tail -1 gpurun_out/s29_bench.log
