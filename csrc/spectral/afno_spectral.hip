@@ -1,33 +1,27 @@
-// amd_dft-build-flags: -O3 -mllvm -amdgpu-load-store-vectorizer=0
 // Fused AFNO spectral filter along H (FourCastNet AFNO2D, K5 in SURVEY §2.5).
 //
-// Built at -O3 WITHOUT the AMDGPU load/store vectorizer.  With it (hipcc, ROCm 7.2, -O2/-O3)
-// both kernels of this file return slightly wrong values (bf16x3: rel-L2 ~6e-3 instead of
-// 6.2e-6, i.e. the lo-plane products of some tiles lost), differently from launch to launch,
-// but only when two or more workgroups share a CU; every element is still written.  Forcing
-// every s_waitcnt to 0 or an s_nop before every instruction does not cure it; disabling the
-// vectorizer -- which merges the split-plane LDS writes into ds_write_b128 -- does, at every
-// grid, and is faster than the -O1 build used before (bf16 452 vs 477 us, bf16x3 842 vs
-// 881 us at [32, 90, 46, 768]; scripts/diag/afno_race_diag.py, afno_poison_diag.py,
-// profiles/afno_o1_fix_r2.txt).
-// Root cause (round 3, profiles/afno_o3_bisect_r3.txt): a gfx950 packed-FP32 fault, not a race in
-// this source.  With the vectorizer on, the pass-1 twiddle multiply is issued as
-// `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` (the high half of the twiddle pair broadcast through
-// src1's op_sel).  Packed-FP32 instructions that select the high half of src1 through op_sel
-// (v_pk_mul_f32 and v_pk_fma_f32 alike) return wrong products while another wave on the same SIMD
-// is executing MFMAs: scripts/diag/opsel_lds_repro.hip, a minimal kernel whose waves 0-3 run an MFMA
-// chain while waves 4-7 check packed products against unpacked ones, sees 7.7 % of those products
-// wrong (0 without the MFMA waves; 0 with op_sel on src0, or with the operand first copied to its
-// own pair, which is what the vectorizer-off build emits).  In this file the MFMA co-runner is the
-// co-resident workgroup's GEMM phase -- hence 'only when two or more workgroups share a CU'.  The
-// vectorizer-off bisection builds agree: the single change 'twiddle consumed through op_sel:[0,1]'
-// fails with either LDS load form, after a full s_waitcnt plus 16 wait states, with extra LDS
-// behind the table; the GEMM-1 epilogue's 64-bit LDS writes are harmless; unpacked FMAs on the
-// same loaded values are exact.  Guards: this file builds with the vectorizer off (no such
-// instruction), tests/test_codegen.py asserts that for this file and that no kernel of the built
-// library contains both an MFMA and a src1-high packed-FP32 op (scripts/diag/scan_so.py; the AFNO
-// W-transforms, the only kernels with the packed form, contain no MFMA), and the determinism
-// screen (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids.
+// History (profiles/afno_o1_fix_r2.txt, profiles/afno_o3_bisect_r3.txt): with the AMDGPU load/store
+// vectorizer on, both kernels of this file used to return slightly wrong values (bf16x3 rel-L2 ~6e-3
+// instead of 6.2e-6), differently from launch to launch, only when two or more workgroups shared a
+// CU; rounds 2-3 built the file with the vectorizer off.
+// Root cause (round 3): a gfx950 packed-FP32 fault, not a race in this source.  With the vectorizer
+// on, the pass-1 twiddle multiply was issued as `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` -- the high
+// half of the twiddle pair broadcast through src1's op_sel.  Packed-FP32 ops that select src1's high
+// half through op_sel (v_pk_mul_f32 and v_pk_fma_f32 alike) return wrong products while another wave
+// on the same SIMD executes MFMAs: scripts/diag/opsel_lds_repro.hip, a minimal kernel whose waves 0-3
+// run an MFMA chain while waves 4-7 check packed products against unpacked ones, sees 7.7 % of the
+// products wrong (0 without the MFMA waves; 0 with op_sel on src0, or with the operand first copied
+// to its own register).  Here the MFMA co-runner was the co-resident workgroup's GEMM phase -- hence
+// 'only when two or more workgroups share a CU'.  The vectorizer-off bisection builds agree (the
+// single change 'twiddle consumed through op_sel:[0,1]' fails with either LDS load form, after a full
+// s_waitcnt plus 16 wait states; unpacked FMAs on the same loaded values are exact).
+// Fix, at the source: radix.h's c_mul(cpair, float2) routes the twiddle's imaginary part through its
+// own register, so no kernel issues the form (0 of 893 kernels); with it the vectorizer-on build is
+// exact and deterministic at every grid of the race screen and 4 % faster for bf16x3 (754 vs 786 us
+// at [32, 90, 46, 768]), so this file builds with the default flags again.  Guards:
+// tests/test_codegen.py (CPU tier) fails if any kernel of the built library issues the form
+// (scripts/diag/scan_so.py) and checks this file with the vectorizer on; the determinism screen
+// (tests/test_determinism_gpu.py) runs every kernel family at co-resident grids.
 //
 // One workgroup owns one (batch b, W-mode kw, channel block k) tile: X[h][c], h < H,
 // c < BS (block size), complex, produced by the W-direction R2C pass.  In one launch it runs
