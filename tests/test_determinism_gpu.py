@@ -1,7 +1,8 @@
 """Large-grid determinism + accuracy screen of every native kernel family (scripts/diag/determinism.py):
 workgroups co-resident on the CUs, each op run 3x, bit-identical outputs that match the CPU
-(ATen fp32) implementation.  Guards against cross-wave races and the co-resident-workgroup corruption that the AMDGPU
-load/store vectorizer caused in the AFNO spectral kernels (csrc/spectral/afno_spectral.hip header)."""
+(ATen fp32) implementation.  Guards against cross-wave races and co-residency faults such as the gfx950 packed-FP32
+op_sel fault beside MFMA waves that once corrupted the AFNO spectral kernels (csrc/spectral/afno_spectral.hip header;
+the static guard is tests/test_codegen.py)."""
 import os
 import runpy
 
