@@ -79,7 +79,7 @@ check("linear bf16 fc1+gelu", lambda: ops.linear(xg.to(dev).bfloat16(), wg.to(de
       torch.nn.functional.gelu(xg @ wg.t() + bg), 1e-2)
 check("linear3 fc1+gelu", lambda: ops.linear3(ops.split_bf16(xg.to(dev)), ops.split_bf16(wg.to(dev)), bg.to(dev), 1, None, False),
       torch.nn.functional.gelu(xg @ wg.t() + bg), 2e-5)
-# FNO block (fno_mix, dftw_r2c, c2c_axis, fno_c2r_pw), batch 4, 720x1440
+# FNO block (dftw_r2c, c2c_axis, fno_mix_c2c, fno_c2r_pw), batch 4, 720x1440
 blk_t = FNOBlock(20, 32, 32, backend="torch").eval()
 blk_a = FNOBlock(20, 32, 32, backend="amd").to(dev).eval()
 blk_a.load_state_dict(blk_t.state_dict())
