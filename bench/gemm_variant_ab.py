@@ -3,7 +3,7 @@ launches: bit-exactness of the outputs (both variants run the same MFMA sequence
 they must agree exactly) and timing (bench/bench_gemm.py --x3 in a child per variant, since the
 variant is read once per process).
 
-Usage: python bench/gemm_variant_ab.py [--rows 518400] [--rounds 3] [--variants 8w+direct,8w,2wg]  (kernel[:stagger cycles][+direct])
+Usage: python bench/gemm_variant_ab.py [--rows 518400] [--rounds 3] [--variants 8w+direct,8w,2wg]  (kernel[+direct])
 """
 import argparse
 import os
@@ -40,12 +40,10 @@ print("saved", sys.argv[1], flush=True)
 
 
 def variant_env(v: str) -> dict:
-    """"8w", "8w+direct" (epilogue stored straight from the MFMA layout), "8w:50" (odd CUs start
-    50 % of a tile late), "2wg", "2wg:60000" (second-resident workgroups start 60000 cycles late)."""
+    """"8w", "8w+direct" (epilogue stored straight from the MFMA layout), "2wg" (an experimental
+    build with bench/experimental/gemm2wg.hip linked in)."""
     kern, _, epi = v.partition("+")
-    kern, _, stagger = kern.partition(":")
-    key = "MI_DFT_GEMM2WG_STAGGER" if kern == "2wg" else "MI_DFT_GEMM_STAGGER"
-    return {"MI_DFT_GEMM_KERNEL": kern, key: stagger or "0", "MI_DFT_GEMM_EPI": epi or "staged"}
+    return {"MI_DFT_GEMM_KERNEL": kern, "MI_DFT_GEMM_EPI": epi or "staged"}
 
 
 def main(argv=None):

@@ -2,6 +2,7 @@
 // selection (kernels: fft_fixed_impl.h, instantiated in fft_fixed_{c2c,r2c,c2r}.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -32,8 +33,11 @@ const std::vector<FixedCfg>& fixed_configs() { return table(); }
 // MI_DFT_FFT_RADICES="L:r,r,...;L:..." picks another configured order for L (A/B runs; read
 // when the plan of L is first built).
 std::vector<int32_t> fixed_radices(int32_t L) {
-  if (const char* e = std::getenv("MI_DFT_FFT_RADICES")) {
-    const std::string spec(e);
+  static const std::string spec = [] {
+    const char* e = std::getenv("MI_DFT_FFT_RADICES");
+    return std::string(e ? e : "");
+  }();
+  if (!spec.empty()) {
     size_t pos = 0;
     while (pos < spec.size()) {
       size_t end = spec.find(';', pos);
@@ -60,19 +64,35 @@ std::vector<int32_t> fixed_radices(int32_t L) {
 
 namespace {
 
+// Process-wide A/B knobs of the fixed kernels, read once (never per launch).  None of them can
+// change a result: they pick between correct kernels / tile orders.
+//   MI_DFT_FIXED=0         the generic pass kernels instead of the specialised ones
+//   MI_DFT_FIXED_CFG=TP,T  force one configured (threads per signal, signals per tile) pair
+//   MI_DFT_FFT_XCD=0|1     force the XCD-aware column-tile order off / on
+struct FixedKnobs {
+  bool enabled = true;
+  int force_tp = 0, force_t = 0;
+  int xcd = -1;  // -1: automatic
+};
+const FixedKnobs& knobs() {
+  static const FixedKnobs k = [] {
+    FixedKnobs r;
+    if (const char* fe = std::getenv("MI_DFT_FIXED")) r.enabled = std::atoi(fe) != 0;
+    if (const char* fc = std::getenv("MI_DFT_FIXED_CFG")) std::sscanf(fc, "%d,%d", &r.force_tp, &r.force_t);
+    if (const char* xe = std::getenv("MI_DFT_FFT_XCD")) r.xcd = std::atoi(xe) != 0 ? 1 : 0;
+    return r;
+  }();
+  return k;
+}
+
 // Picks the configuration for d and fills its kernel arguments; false if none applies.
 bool prepare_fixed(const PassDesc& d, int& best_out, FixedArgs& a, int64_t& nblocks_out) {
-  // MI_DFT_FIXED=0 disables the specialised kernels (A/B tests); MI_DFT_FIXED_CFG="TP,T"
-  // forces one configuration.
-  const char* fe = std::getenv("MI_DFT_FIXED");
-  if (fe && std::atoi(fe) == 0) return false;
-  if (d.tw_count == 0 && d.npass > 1) return false;  // ablation builds
+  const FixedKnobs& kn = knobs();
+  if (!kn.enabled) return false;
   const bool cols = d.Si_in < d.Sn_in || d.Si_out < d.Sn_out;
   const bool paired = d.kind != Kind::C2C;
   const int64_t nsig = paired ? (d.I + 1) / 2 : d.I;
-  std::vector<int32_t> rad(d.radix, d.radix + d.npass);
-  int force_tp = 0, force_t = 0;
-  if (const char* fc = std::getenv("MI_DFT_FIXED_CFG")) std::sscanf(fc, "%d,%d", &force_tp, &force_t);
+  int force_tp = kn.force_tp, force_t = kn.force_t;
   const auto& cfgs = fixed_configs();
   if (force_tp) {  // the override only applies where such a configuration exists
     bool any = false;
@@ -84,7 +104,7 @@ bool prepare_fixed(const PassDesc& d, int& best_out, FixedArgs& a, int64_t& nblo
   for (int i = 0; i < static_cast<int>(cfgs.size()); ++i) {
     const FixedCfg& c = cfgs[i];
     if (c.L != d.L || c.cols != cols) continue;
-    if (std::vector<int32_t>(c.radix, c.radix + c.npass) != rad) continue;
+    if (c.npass != d.npass || !std::equal(c.radix, c.radix + c.npass, d.radix)) continue;
     if (force_tp && (c.TP != force_tp || c.T != force_t)) continue;
     const int64_t wgs = d.O * ((nsig + c.T - 1) / c.T);
     const int64_t waves = wgs * ((c.TP * c.T + 63) / 64);
@@ -167,10 +187,8 @@ bool prepare_fixed(const PassDesc& d, int& best_out, FixedArgs& a, int64_t& nblo
     const int eb = a.bf16_in ? 2 : 4;
     const int64_t row_bytes = static_cast<int64_t>(cfg.T) * 2 * eb;  // complex or paired-real elements
     bool on = cfg.cols && row_bytes < 128 && nblocks >= 16;
-    if (const char* xe = std::getenv("MI_DFT_FFT_XCD")) on = std::atoi(xe) != 0;
+    if (kn.xcd >= 0) on = kn.xcd != 0;
     a.xcd_nb = on ? static_cast<int32_t>(nblocks) : 0;
-    const char* ab = std::getenv("MI_DFT_FFT_ABLATE");
-    a.ablate = ab ? std::atoi(ab) : 0;
   }
   best_out = best;
   nblocks_out = nblocks;

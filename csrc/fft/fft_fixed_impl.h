@@ -29,7 +29,6 @@ struct FixedArgs {
   int32_t I, Si_in, Si_out, Sn_in, Sn_out;  // per-element offsets fit 32 bits (host-checked)
   int32_t in_lo, in_hi, out_lo, out_hi, tiles_per_outer;
   int32_t xcd_nb;    // > 0: XCD-aware remap of the nb = xcd_nb blocks (see xcd_block)
-  int32_t ablate;    // timing ablations (MI_DFT_FFT_ABLATE, wrong results): 2 = no twiddles, 4 = no butterflies
   float scale;
   int32_t inverse, vec_in, vec_out, bf16_in, bf16_out;
   const void* add1;  // C2R epilogue: out = scale * irfft + add1 (+ add2); same layout/dtype as out
@@ -252,7 +251,6 @@ __device__ __forceinline__ float2 gather(const Ctx& x, int n) {
   return z;
 }
 
-// Last-pass element store (C2C / C2R), with output pruning and the fused scale.
 // Last-pass element store (C2C / C2R), with output pruning, the fused scale and (C2R) the
 // pre-loaded addend pair `ad` (add1 + add2 at this element, zero when NADD == 0).
 template <Kind K, int L, bool BF, bool PR, bool PV>
@@ -324,7 +322,6 @@ template <class F, int TP, int P>
 __device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, TP, P>::Q][PassGeom<F, TP, P>::TWR]) {
   using G = PassGeom<F, TP, P>;
   if constexpr (G::Ns > 1) {
-    if (x.a.ablate & 2) return;
 #pragma unroll
     for (int q = 0; q < G::Q; ++q) {
       const int j = x.tp + q * TP;
@@ -394,12 +391,10 @@ struct Step {
       const int j = x.tp + q * TP;
       if (G::EXACT || j < LR) {
         if constexpr (Ns > 1) {
-          if (!(x.a.ablate & 2)) {
 #pragma unroll
-            for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[q][r - 1]);
-          }
+          for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[q][r - 1]);
         }
-        if (!(x.a.ablate & 4)) Dft<R>::run(v[q]);
+        Dft<R>::run(v[q]);
       }
     }
     // ---- scatter

@@ -35,7 +35,9 @@
 // and fragment reads as the bf16 kernel (its k-step 0 / 1 fragments become the hi / lo
 // fragments) feed 24 MFMAs per phase instead of 16 -- 2x the bf16 loads for 3x the MFMAs.
 // Outputs: fp32 (OUT 1) or a split pair row in the same layout (OUT 2), ready to be the
-// next GEMM's operand.
+// next GEMM's operand.  The LayerNorm fold works in split mode too (fc1 of the fp32 block reads
+// the raw residual stream's split pairs written by the AFNO C2R epilogue; c1 is summed from the
+// split weight pairs, so x W'^T - mean c1 cancels the mean exactly up to the split's 2^-17).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -318,13 +320,6 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         const int ii = rem / p.gw, jj = rem - ii * p.gw;
         gb[r][i] = (b * p.gC * (p.gh * 8) + ii * 8) * rowlen + jj * 8;
       }
-  }
-  // optional first-round stagger: odd CUs of each XCD (blockIdx / 8 odd, first dispatch round)
-  // start p.stagger shader cycles late, so that the CUs' epilogue store bursts interleave with
-  // other CUs' main loops instead of all hitting HBM together
-  if (p.stagger > 0 && b < 256 && ((b >> 3) & 1)) {
-    const long long s0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - s0 < p.stagger) __builtin_amdgcn_s_sleep(8);
   }
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
   stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
@@ -637,6 +632,11 @@ void launch_res(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 // split (bf16x3) path: fp32 output (+ fp32 residual) or split-pair output (no residual)
 template <int ACT, bool BIAS>
 void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if (p.ln_stats) {  // fc1 of the fp32 block: LayerNorm folded in (raw residual-stream pairs), split-pair output
+    if (p.out != 2 || p.residual) throw std::runtime_error("amd_dft: gemm: a split LayerNorm fold writes split pairs, no residual");
+    launch_one<ACT, BIAS, false, true, 0, true, 2>(p, st, grid);
+    return;
+  }
   if (p.out == 2) {
     if (p.residual) {  // last fp32 block: x + h W2^T straight to the head GEMM's split-pair operand
       if constexpr (ACT == 0 && !BIAS) {
@@ -688,20 +688,9 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
   if (p_.out < 0 || p_.out > 2 || (p_.out != 0) != (p_.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
-  if (p_.split && p_.ln_stats) throw std::runtime_error("amd_dft: gemm: no LayerNorm fold in split mode");
   if (p_.split && !split_k_ok(p_.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
   GemmLaunch p = p_;
   p.direct_epi = gemm_direct_epi();
-  {
-    // MI_DFT_GEMM_STAGGER: first-round start delay of odd CUs in percent of an estimated tile
-    // (~3300 shader cycles per K-tile + ~15k epilogue)
-    static const int pct = [] {
-      const char* e = std::getenv("MI_DFT_GEMM_STAGGER");
-      return e ? std::atoi(e) : 0;
-    }();
-    const int kt = p.split ? p.K / 32 : p.K / kBK;
-    p.stagger = pct > 0 ? static_cast<int>((static_cast<int64_t>(kt) * 3300 + 15000) * pct / 100) : 0;
-  }
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   const dim3 grid(static_cast<uint32_t>(nwg));
   hipStream_t st = static_cast<hipStream_t>(stream);

@@ -136,12 +136,6 @@ bool run_pass(Kind kind, const at::Tensor& in, const at::Tensor& out, const std:
   TORCH_CHECK(choose_tiling(d), "amd_dft: transform length ", L, " exceeds the LDS-resident limit (",
               max_lds_length(), ")");
   finalize_vec_flags(d, static_cast<int>(in.element_size()), static_cast<int>(out.element_size()));
-  // Timing-only ablations (results are WRONG): MI_DFT_ABLATE=nopass|notw|io
-  if (const char* ab = std::getenv("MI_DFT_ABLATE")) {
-    const std::string a(ab);
-    if (a == "nopass" || a == "io") d.npass = 0;
-    if (a == "notw" || a == "io") d.tw_count = 0;
-  }
   void* stream = c10::hip::getCurrentHIPStream(in.device().index()).stream();
   if (ln) {
     d.ln_stats = ln->stats;
@@ -698,6 +692,13 @@ void check_ln_args(const at::Tensor& x, int64_t dim, const at::Tensor& stats, co
               ": stats must hold (mean, rstd) per token");
 }
 
+// MI_DFT_NO_AFNO_W=1 (A/B, read once): LayerNorm-fused AFNO W-transforms on the generic fixed
+// Stockham kernels instead of afno_wfft.hip (same results)
+bool afno_w_enabled() {
+  static const bool on = std::getenv("MI_DFT_NO_AFNO_W") == nullptr;
+  return on;
+}
+
 at::Tensor r2c_cpu(const at::Tensor& x, at::IntArrayRef dim, double scale, at::IntArrayRef keep,
                    std::optional<at::ScalarType> out_dtype);
 at::Tensor c2r_cpu(const at::Tensor& x, at::IntArrayRef dim, at::IntArrayRef out_size, double scale,
@@ -728,7 +729,7 @@ at::Tensor r2c_ln_cuda(const at::Tensor& x_, int64_t dim, double scale, int64_t 
           pre_.has_value() ? pre.data_ptr<float>() : nullptr};
   const int64_t C = x.size(-1);
   const bool w_f32 = x.scalar_type() == at::kFloat && odt == at::kFloat;
-  if (((x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16) || w_f32) && !std::getenv("MI_DFT_NO_AFNO_W") &&
+  if (((x.scalar_type() == at::kBFloat16 && odt == at::kBFloat16) || w_f32) && afno_w_enabled() &&
       afno_w_supported(static_cast<int>(s.n), static_cast<int>(C), static_cast<int>(s.lo)) &&
       x.numel() / (s.n * C) < (int64_t(1) << 31)) {
     AfnoWLaunch p;  // 16-byte-lane two-pass kernel (afno_wfft.hip)
@@ -797,7 +798,7 @@ at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double 
   const bool w_f32 = X.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat;
   if (w_f32 && X.numel() > 0) {
     const int64_t C = x.size(-1);
-    if (!std::getenv("MI_DFT_NO_AFNO_W") && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
+    if (afno_w_enabled() && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
         x.numel() / (n * C) < (int64_t(1) << 31)) {
       at::Tensor out = at::empty_like(x);
       AfnoWLaunch p;  // fp32 instantiation of the two-pass kernel (afno_wfft.hip)
@@ -829,7 +830,7 @@ at::Tensor c2r_ln_add_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double 
     LnIO ln{stats.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(),
             pre_.has_value() ? pre.data_ptr<float>() : nullptr};
     const int64_t C = x.size(-1);
-    if (!std::getenv("MI_DFT_NO_AFNO_W") &&
+    if (afno_w_enabled() &&
         afno_w_supported(static_cast<int>(s.n), static_cast<int>(C), static_cast<int>(km)) &&
         x.numel() / (s.n * C) < (int64_t(1) << 31)) {
       AfnoWLaunch p;  // 16-byte-lane two-pass kernel (afno_wfft.hip)
@@ -877,6 +878,95 @@ at::Tensor c2r_ln_add_cpu(const at::Tensor& X, int64_t dim, int64_t n, double sc
 at::Tensor c2r_ln_add_meta(const at::Tensor&, int64_t, int64_t, double, const at::Tensor& x, const at::Tensor&,
                            const at::Tensor&, const at::Tensor&, const std::optional<at::Tensor>&) {
   return at::empty_like(x);
+}
+
+// c2r_ln_add + the residual stream's bf16x3 split-pair rows and per-64-channel LayerNorm partials
+// (mean, M2), all from the one C2R epilogue (afno_wfft.hip SPLIT instantiation): the fp32 block's
+// fc1 then reads the pairs with LN2 folded in (linear3_ln) -- no LayerNorm / split pass.
+// Returns (out [..., W, C] fp32, pairs [tokens, 2C] bf16, part [tokens, C/64, 2] fp32).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> split_and_partials(const at::Tensor& y) {
+  const int64_t C = y.size(-1);
+  at::Tensor rows = y.reshape({-1, C}).to(at::kFloat);
+  at::Tensor hi = rows.to(at::kBFloat16);
+  at::Tensor lo = (rows - hi.to(at::kFloat)).to(at::kBFloat16);
+  const int64_t M = rows.size(0);
+  at::Tensor pairs = at::cat({hi.reshape({M, C / 32, 32}), lo.reshape({M, C / 32, 32})}, -1).reshape({M, 2 * C}).contiguous();
+  at::Tensor w = rows.reshape({M, C / 64, 64});
+  at::Tensor mean = w.mean(2);
+  at::Tensor m2 = (w - mean.unsqueeze(2)).pow(2).sum(2);
+  return {y, pairs, at::stack({mean, m2}, 2).contiguous()};
+}
+
+at::Tensor c2r_ln_add_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale, const at::Tensor& x,
+                          const at::Tensor& stats, const at::Tensor& g, const at::Tensor& b,
+                          const std::optional<at::Tensor>& pre);
+
+void check_split_out(const at::Tensor& X, const at::Tensor& x, const char* op) {
+  TORCH_CHECK(X.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "amd_dft.", op,
+              ": split-pair outputs come with the fp32 residual stream");
+  TORCH_CHECK(x.size(-1) % 64 == 0, "amd_dft.", op, ": C must be a multiple of 64");
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double scale,
+                                                                     const at::Tensor& x_, const at::Tensor& stats_,
+                                                                     const at::Tensor& g_, const at::Tensor& b_,
+                                                                     const std::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(X_.device());
+  check_ln_args(x_, dim, stats_, g_, b_, pre_, "c2r_ln_add_split");
+  check_split_out(X_, x_, "c2r_ln_add_split");
+  const int64_t axis = x_.dim() - 2;
+  TORCH_CHECK(X_.dim() == x_.dim() + 1 && X_.size(-1) == 2 && x_.size(axis) == n &&
+                  X_.sizes().slice(0, axis) == x_.sizes().slice(0, axis) && X_.size(axis + 1) == x_.size(-1) &&
+                  X_.size(axis) <= n / 2 + 1,
+              "amd_dft.c2r_ln_add_split: X must be [..., km, C, 2] with the leading dims and C of x and km <= n/2+1");
+  at::Tensor X = X_.contiguous(), x = x_.contiguous();
+  const int64_t km = X.size(axis), C = x.size(-1);
+  if (X.numel() > 0 && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
+      x.numel() / (n * C) < (int64_t(1) << 31)) {
+    at::Tensor stats = stats_.to(at::kFloat).contiguous(), g = g_.to(at::kFloat).contiguous(),
+               b = b_.to(at::kFloat).contiguous();
+    at::Tensor pre;
+    if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+    const int64_t M = x.numel() / C;
+    at::Tensor out = at::empty_like(x);
+    at::Tensor pairs = at::empty({M, 2 * C}, x.options().dtype(at::kBFloat16));
+    at::Tensor part = at::empty({M, C / 64, 2}, x.options());
+    AfnoWLaunch p;  // fp32 two-pass kernel with the split / statistics epilogue (afno_wfft.hip)
+    p.x = x.data_ptr();
+    p.stats = stats.data_ptr<float>();
+    p.gamma = g.data_ptr<float>();
+    p.beta = b.data_ptr<float>();
+    p.pre = pre_.has_value() ? pre.data_ptr<float>() : nullptr;
+    p.spec = X.data_ptr();
+    p.out = out.data_ptr();
+    p.pairs = reinterpret_cast<uint16_t*>(pairs.data_ptr());
+    p.part = part.data_ptr<float>();
+    p.O = static_cast<int>(M / n);
+    p.L = static_cast<int>(n);
+    p.C = static_cast<int>(C);
+    p.KM = static_cast<int>(km);
+    p.scale = static_cast<float>(scale);
+    p.f32 = 1;
+    launch_afno_w_c2r_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return {checked(out, "c2r_ln_add_split"), pairs, part};
+  }
+  fallback_note("c2r_ln_add_split", "no fused W-transform for this shape: c2r_ln_add + ATen split / statistics");
+  return split_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_));
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale,
+                                                                    const at::Tensor& x, const at::Tensor& stats,
+                                                                    const at::Tensor& g, const at::Tensor& b,
+                                                                    const std::optional<at::Tensor>& pre) {
+  check_split_out(X, x, "c2r_ln_add_split");
+  return split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre));
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_meta(const at::Tensor&, int64_t, int64_t, double,
+                                                                     const at::Tensor& x, const at::Tensor&, const at::Tensor&,
+                                                                     const at::Tensor&, const std::optional<at::Tensor>&) {
+  const int64_t C = x.size(-1), M = x.numel() / std::max<int64_t>(C, 1);
+  return {at::empty_like(x), at::empty({M, 2 * C}, x.options().dtype(at::kBFloat16)), at::empty({M, C / 64, 2}, x.options())};
 }
 
 // ------------------------------------------------------------------ CPU impls (torch.fft)
@@ -1056,6 +1146,8 @@ TORCH_LIBRARY(amd_dft, m) {
         "ScalarType? out_dtype=None) -> Tensor");
   m.def("c2r_ln_add(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
         "Tensor? pre=None) -> Tensor");
+  m.def("c2r_ln_add_split(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
+        "Tensor? pre=None) -> (Tensor, Tensor, Tensor)");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("plan_info(int n) -> str", &amd_dft::plan_info);
@@ -1075,6 +1167,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("fno_mix_c2c", AMD_DFT_TRACED("amd_dft::fno_mix_c2c", amd_dft::fno_mix_c2c_cuda));
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cuda));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cuda));
+  m.impl("c2r_ln_add_split", AMD_DFT_TRACED("amd_dft::c2r_ln_add_split", amd_dft::c2r_ln_add_split_cuda));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -1087,6 +1180,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("fno_mix_c2c", AMD_DFT_TRACED("amd_dft::fno_mix_c2c", amd_dft::fno_mix_c2c_cpu));
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cpu));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cpu));
+  m.impl("c2r_ln_add_split", AMD_DFT_TRACED("amd_dft::c2r_ln_add_split", amd_dft::c2r_ln_add_split_cpu));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -1099,6 +1193,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("fno_mix_c2c", &amd_dft::fno_mix_c2c_meta);
   m.impl("r2c_ln", &amd_dft::r2c_ln_meta);
   m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_meta);
+  m.impl("c2r_ln_add_split", &amd_dft::c2r_ln_add_split_meta);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {

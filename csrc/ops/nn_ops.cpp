@@ -492,6 +492,66 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_meta(const at::Tensor& xs, cons
   return {at::empty(os, xs.options().dtype(at::kFloat)), at::empty({M, ws.size(0) / 64, 2}, xs.options().dtype(at::kFloat))};
 }
 
+// fc1 of the fp32 FourCastNet block: y = split(act(LN(x) W^T + b)) from the split pairs of the RAW
+// residual stream x (the AFNO C2R epilogue writes them, c2r_ln_add_split), the LayerNorm folded into
+// the bf16x3 GEMM's epilogue exactly as linear_ln does for bf16: ws = split(W * gamma),
+// c1[n] = sum_k (hi + lo)(ws)[n, k] (from the split pairs the GEMM reads), bias = W beta + b,
+// stats [M, 2] = (mean, rstd) of x.  Output: split-pair rows (the next GEMM's operand).
+void check_linear3_ln(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
+                      const at::Tensor& stats, int64_t act) {
+  check_split_linear(xs, ws, bias, "linear3_ln");
+  TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear3_ln: act must be 0 (none) or 1 (gelu)");
+  TORCH_CHECK(xs.size(-1) == ws.size(1), "amd_dft.linear3_ln: xs [..., 2K], ws [N, 2K]");
+  const int64_t N = ws.size(0), M = xs.numel() / std::max<int64_t>(ws.size(1), 1);
+  TORCH_CHECK(c1.numel() == N, "amd_dft.linear3_ln: c1 must have N entries");
+  TORCH_CHECK(stats.numel() == 2 * M && stats.size(-1) == 2, "amd_dft.linear3_ln: stats must be [M, 2] (mean, rstd)");
+}
+
+at::Tensor linear3_ln_cpu(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
+                          const at::Tensor& stats, int64_t act) {
+  check_linear3_ln(xs, ws, c1, bias, stats, act);
+  at::Tensor y = linear_ln_ref(unsplit_rows(xs), unsplit_rows(ws), c1, bias, stats, act);
+  return split_ref(y, true);
+}
+
+at::Tensor linear3_ln_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const at::Tensor& c1_,
+                           const c10::optional<at::Tensor>& bias, const at::Tensor& stats_, int64_t act) {
+  const c10::DeviceGuard guard(xs_.device());
+  check_linear3_ln(xs_, ws_, c1_, bias, stats_, act);
+  const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_ln: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0 (got N=",
+              N, ", K=", K, ")");
+  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
+  at::Tensor c1 = c1_.to(at::kFloat).contiguous(), stats = stats_.to(at::kFloat).contiguous();
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = 2 * N;
+  at::Tensor y = at::empty(os, xs.options());
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(xs.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  p.bias = b.defined() ? b.data_ptr<float>() : nullptr;
+  p.y = y.data_ptr();
+  p.ln_stats = stats.data_ptr<float>();
+  p.ln_c1 = c1.data_ptr<float>();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.act = static_cast<int>(act);
+  p.split = 1;
+  p.out = 2;
+  if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
+  return y;
+}
+
+at::Tensor linear3_ln_meta(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor&, const c10::optional<at::Tensor>&,
+                           const at::Tensor&, int64_t) {
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = 2 * ws.size(0);
+  return at::empty(os, xs.options());
+}
+
 at::Tensor linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>&, int64_t,
                         const c10::optional<at::Tensor>&, bool split_out) {
   std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
@@ -615,6 +675,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
   m.def("linear3(Tensor xs, Tensor ws, Tensor? bias=None, int act=0, Tensor? residual=None, bool split_out=False) -> Tensor");
   m.def("linear3_stats(Tensor xs, Tensor ws, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
+  m.def("linear3_ln(Tensor xs, Tensor ws, Tensor c1, Tensor? bias, Tensor stats, int act=0) -> Tensor");
   m.def("patch_linear3(Tensor xs, Tensor ws, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
   m.def("linear_unpatch3(Tensor ts, Tensor ws, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
 }
@@ -628,6 +689,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cuda));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cuda));
+  m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cuda));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cuda));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cuda));
 }
@@ -641,6 +703,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cpu));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cpu));
+  m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cpu));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cpu));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cpu));
 }
@@ -654,6 +717,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("split_bf16", &amd_dft::split_bf16_meta);
   m.impl("linear3", &amd_dft::linear3_meta);
   m.impl("linear3_stats", &amd_dft::linear3_stats_meta);
+  m.impl("linear3_ln", &amd_dft::linear3_ln_meta);
   m.impl("patch_linear3", &amd_dft::patch_linear3_meta);
   m.impl("linear_unpatch3", &amd_dft::linear_unpatch3_meta);
 }

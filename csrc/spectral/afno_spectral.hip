@@ -67,37 +67,6 @@ constexpr int kNT = 256;  // threads
 #ifndef AFNO_BPF3
 #define AFNO_BPF3 2  // k-steps of B-fragment prefetch in the bf16x3 block-MLP GEMMs
 #endif
-#ifndef AFNO_DIAG
-#define AFNO_DIAG 0  // diagnostic builds only (scripts/diag/afno_o3_bisect.sh): 1 = 32 wait states after every
-                     // k-step's MFMA group (fragment registers reloaded while MFMAs may still read them),
-                     // 2 = 32 wait states after each GEMM, before its accumulators are read
-#endif
-__device__ __forceinline__ void diag_guard() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-#ifndef AFNO_TW64
-#define AFNO_TW64 0  // diagnostic builds only: pass-1 twiddles read as one 64-bit LDS load each (the form the
-                     // -O3 vectorizer produces: ds_read2_b64 / ds_read_b64 instead of ds_read2_b32);
-                     // bit 0: forward FFT_H pass 1, bit 1: inverse FFT_H pass 1
-#endif
-#ifndef AFNO_TWCHECK
-#define AFNO_TWCHECK 0  // diagnostic builds only (with AFNO_TW64): 1 = every 64-bit twiddle read is re-read as
-                        // two volatile 32-bit loads, a mismatch poisons the butterfly with NaN; 2 = s_waitcnt
-                        // lgkmcnt(0) right after each read; 3 = unpacked (scalar fp32) twiddle multiply; 4 / 5 =
-                        // the read as inline-asm ds_read_b64 + full wait, with the unpacked / packed multiply;
-                        // 6 = as 5 plus 16 wait states (2 x s_nop 7) between the wait and the packed multiply;
-                        // 7 = as 5 with the pair read by ds_read2_b32
-#endif
-#ifndef AFNO_EPI64
-#define AFNO_EPI64 0  // diagnostic builds only: GEMM-1 epilogue 8-byte pieces stored as one 64-bit LDS store
-#endif
-#ifndef AFNO_ABLATE
-#define AFNO_ABLATE 0  // timing-only builds (bench/afno_ablate.hip): 1 = no FFT butterflies, 2 = no GEMM MFMAs,
-                       // 4 = x3 GEMM B fragments of k-step 0 reused (no weight loads after the first)
-#endif
-
 #ifdef AFNO_STAMPS
 // phase clocks (bench/afno_stamps.hip): thread 0 of each workgroup records s_memtime after every
 // phase barrier of the bf16x3 kernel (slot 0 / 11: s_memrealtime at entry / exit, 12: s_memtime at exit; 16 per workgroup)
@@ -180,11 +149,10 @@ struct HPass {
   static constexpr int Q = (NB + kNT - 1) / kNT;
 };
 
-template <int R, int L, int NP, int Ns, int Q, int SITE = 0>
+template <int R, int L, int NP, int Ns, int Q>
 __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __restrict__ tw) {
   using P = HPass<R, L, NP>;
   static_assert(P::Q == Q, "pass geometry");
-  if constexpr (AFNO_ABLATE & 1) return;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int b = threadIdx.x + q * kNT;
@@ -193,43 +161,7 @@ __device__ __forceinline__ void h_twiddle_dft(cpair (&v)[Q][R], const float2* __
       if constexpr (Ns > 1) {
         const int k = j % Ns;
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-          if constexpr ((AFNO_TW64 & SITE) != 0) {
-            uint64_t t;
-            if constexpr (AFNO_TWCHECK >= 4) {  // the 64-bit read as inline asm, fully waited
-              typedef __attribute__((address_space(3))) const float2 lds_f2;
-              const uint32_t addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_f2*)(tw + (r - 1) * Ns + k)));
-              if constexpr (AFNO_TWCHECK == 7)  // the pair as two 32-bit LDS reads (ds_read2_b32), same consumer
-                asm volatile("ds_read2_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(addr) : "memory");
-              else if constexpr (AFNO_TWCHECK == 6)  // + 16 wait states before the first consumer
-                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7" : "=v"(t) : "v"(addr) : "memory");
-              else
-                asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(addr) : "memory");
-            } else {
-              t = *reinterpret_cast<const uint64_t*>(tw + (r - 1) * Ns + k);
-            }
-            float2 tf = __builtin_bit_cast(float2, t);
-            if constexpr (AFNO_TWCHECK == 1) {
-              const volatile float* f = reinterpret_cast<const volatile float*>(tw + (r - 1) * Ns + k);
-              const float a = f[0], b = f[1];
-              if (a != tf.x || b != tf.y) tf = make_float2(__builtin_nanf(""), __builtin_nanf(""));
-            }
-            if constexpr (AFNO_TWCHECK == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if constexpr (AFNO_TWCHECK == 3 || AFNO_TWCHECK == 4) {  // scalar (unpacked) fp32 twiddle multiply
-              const float r0 = v[q][r].re[0], r1 = v[q][r].re[1], i0 = v[q][r].im[0], i1 = v[q][r].im[1];
-              const float a0 = fmaf(r0, tf.x, -i0 * tf.y), b0 = fmaf(r0, tf.y, i0 * tf.x);
-              const float a1 = fmaf(r1, tf.x, -i1 * tf.y), b1 = fmaf(r1, tf.y, i1 * tf.x);
-              v[q][r].re[0] = a0;
-              v[q][r].re[1] = a1;
-              v[q][r].im[0] = b0;
-              v[q][r].im[1] = b1;
-            } else {
-              v[q][r] = c_mul(v[q][r], tf);
-            }
-          } else {
-            v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
-          }
-        }
+        for (int r = 1; r < R; ++r) v[q][r] = c_mul(v[q][r], tw[(r - 1) * Ns + k]);
       }
       Dft<R>::run(v[q]);
     }
@@ -291,13 +223,10 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
     for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
-        if constexpr (AFNO_ABLATE & 2) acc[mi][nj] += __builtin_bit_cast(f32x4, afr[mi]) + __builtin_bit_cast(f32x4, bq[ks % NQ][nj]);
-        else if constexpr (TR) acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks % NQ][nj], afr[mi], acc[mi][nj], 0, 0, 0);
+        if constexpr (TR) acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks % NQ][nj], afr[mi], acc[mi][nj], 0, 0, 0);
         else acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[mi], bq[ks % NQ][nj], acc[mi][nj], 0, 0, 0);
       }
-    if constexpr (AFNO_DIAG & 1) diag_guard();
   }
-  if constexpr (AFNO_DIAG & 2) diag_guard();
 }
 
 template <class S, bool BFI, bool BFO>
@@ -361,7 +290,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
       }
     }
     __syncthreads();
-    h_twiddle_dft<R1, L, NP, R0, P1::Q, 1>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -396,14 +325,6 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
 #pragma unroll
       for (int mi = 0; mi < S::MT; ++mi) {
         const int m = mi * 16 + (lane & 15);
-        if constexpr (AFNO_EPI64) {
-          const uint2 u = make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
-                                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
-                                     static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][2] + bias.z, 0.f))) |
-                                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][3] + bias.w, 0.f))) << 16));
-          *reinterpret_cast<uint64_t*>(A + m * AP + n0) = (static_cast<uint64_t>(u.y) << 32) | u.x;
-          continue;
-        }
         *reinterpret_cast<uint2*>(A + m * AP + n0) =
             make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
                            (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
@@ -485,7 +406,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(lds, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q, 2>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -541,16 +462,6 @@ __device__ __forceinline__ void put_split2(uint16_t* Ahi, uint16_t* Alo, int idx
 __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx, float a, float b, float c, float d) {
   const uint16_t ha = f2bf16(a), hb = f2bf16(b), hc = f2bf16(c), hd = f2bf16(d);
   const auto up = [](uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); };
-  if constexpr (AFNO_EPI64) {
-    const uint64_t h = (static_cast<uint64_t>(static_cast<uint32_t>(hc) | (static_cast<uint32_t>(hd) << 16)) << 32) |
-                       (static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16));
-    const uint64_t l = (static_cast<uint64_t>(static_cast<uint32_t>(f2bf16(c - up(hc))) |
-                                              (static_cast<uint32_t>(f2bf16(d - up(hd))) << 16)) << 32) |
-                       (static_cast<uint32_t>(f2bf16(a - up(ha))) | (static_cast<uint32_t>(f2bf16(b - up(hb))) << 16));
-    *reinterpret_cast<uint64_t*>(Ahi + idx) = h;
-    *reinterpret_cast<uint64_t*>(Alo + idx) = l;
-    return;
-  }
   *reinterpret_cast<uint2*>(Ahi + idx) = make_uint2(static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16),
                                                     static_cast<uint32_t>(hc) | (static_cast<uint32_t>(hd) << 16));
   *reinterpret_cast<uint2*>(Alo + idx) =
@@ -574,7 +485,8 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
   // B (weight) fragments stream from L2 AFNO_BPF3 k-steps ahead: with one k-step of lookahead
-  // the L2 latency is exposed every k-step (bench/afno_ablate.hip, AFNO_ABLATE=4: -164 us)
+  // the L2 latency is exposed every k-step (a timing-only build that reused the first k-step's
+  // fragments ran 164 us faster, round 2)
   constexpr int D0 = S::NTW >= 4 ? 1 : AFNO_BPF3;  // 4 column tiles per wave: no registers for 2
   constexpr int D = D0 < S::KS ? D0 : S::KS - 1, NQ = D + 1;
   bf16x8 bh[NQ][S::NTW], bl[NQ][S::NTW];
@@ -588,7 +500,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
     }
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
-    if (ks + D < S::KS && !(AFNO_ABLATE & 4)) {
+    if (ks + D < S::KS) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
         const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
@@ -605,11 +517,6 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(Al + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
-        if constexpr (AFNO_ABLATE & 2) {
-          acc[mi][nj] += __builtin_bit_cast(f32x4, al) + __builtin_bit_cast(f32x4, bh[ks % NQ][nj]) +
-                         __builtin_bit_cast(f32x4, ah) + __builtin_bit_cast(f32x4, bl[ks % NQ][nj]);
-          continue;
-        }
         if constexpr (TR) {
           acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[ks % NQ][nj], al, acc[mi][nj], 0, 0, 0);
           acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[ks % NQ][nj], ah, acc[mi][nj], 0, 0, 0);
@@ -621,9 +528,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
         }
       }
     }
-    if constexpr (AFNO_DIAG & 1) diag_guard();
   }
-  if constexpr (AFNO_DIAG & 2) diag_guard();
 }
 
 template <class S>
@@ -694,7 +599,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
     }
     __syncthreads();
     AFNO_STAMP(3, __builtin_amdgcn_s_memtime());
-    h_twiddle_dft<R1, L, NP, R0, P1::Q, 1>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -811,7 +716,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         for (int r = 0; r < R1; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P1::LR) * BS + 2 * tp);
       }
     }
-    h_twiddle_dft<R1, L, NP, R0, P1::Q, 2>(v, twl);
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
 #pragma unroll
     for (int q = 0; q < P1::Q; ++q) {
       const int bb = tid + q * kNT;
@@ -874,13 +779,6 @@ const AfnoInstance* find_instance(int H, int bs) {
 }
 
 void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a, void* stream) {
-  // MI_DFT_AFNO_LDS_EXTRA=<bytes>: diagnostic -- allocate that much dynamic LDS beyond what the
-  // kernel addresses (scripts/diag/afno_race_diag.py bisection)
-  static const int64_t extra = [] {
-    const char* e = std::getenv("MI_DFT_AFNO_LDS_EXTRA");
-    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
-  }();
-  lds += extra;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(lds));
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_spectral attr: ") + hipGetErrorString(e));

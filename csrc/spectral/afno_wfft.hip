@@ -82,6 +82,8 @@ struct WArgs {
   const float* pre;      // [C] or nullptr
   const void* spec;      // C2R input [O, KM, C, 2] bf16 / fp32
   void* out;             // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
+  uint16_t* pairs;       // C2R, SPLIT: [O * 180, 2C] bf16 split pairs of out
+  float* part;           // C2R, SPLIT: [O * 180, C / 64, 2] (mean, M2) of out per 64-channel slab
   int C, nslab;
   float scale;
 };
@@ -277,8 +279,23 @@ constexpr int c2r_load_kind(int n1) {
   return all ? 1 : (any ? 2 : 0);
 }
 
-template <int KM, bool F32>
+// sum over a 16-lane DPP row (every lane gets the total): quad swaps, then the 8- and 16-lane mirrors
+__device__ __forceinline__ float row_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));  // row_mirror
+  return x;
+}
+
+// SPLIT (fp32 block, round 4): the epilogue also writes the next GEMM's operand -- the bf16x3 split
+// pairs of y -- and the next LayerNorm's partial statistics of y over this workgroup's 64 channels
+// (the 16 lanes of one DPP row hold one position's 64 channels).  That removes the separate
+// LayerNorm -> split pass over the residual stream (one full read of it per block); LN2 is then
+// folded into fc1's epilogue (linear3_ln) from per-token stats merged by ln_stats_merge.
+template <int KM, bool F32, bool SPLIT = false>
 __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs a) {
+  static_assert(!SPLIT || F32, "split-pair outputs come with the fp32 instantiation");
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
   // bf16 (XLDS): fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its
   // LN statistics: 49.6 KB -> still 3 workgroups per CU, and the addends need no VGPRs.
@@ -424,6 +441,20 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
       y[2 * p + 1] = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
     }
     stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
+    if constexpr (SPLIT) {
+      const int n = k1 + kA * k2;
+      const int64_t t = static_cast<int64_t>(o) * kL + n;  // token
+      const uint32_t h01 = bfpack(y[0], y[1]), h23 = bfpack(y[2], y[3]);
+      const uint32_t l01 = bfpack(y[0] - __uint_as_float(h01 << 16), y[1] - __uint_as_float(h01 & 0xffff0000u));
+      const uint32_t l23 = bfpack(y[2] - __uint_as_float(h23 << 16), y[3] - __uint_as_float(h23 & 0xffff0000u));
+      uint16_t* pr = a.pairs + t * (2 * C) + (c0 >> 5) * 64 + (c0 & 31);  // k32-interleaved [hi(32) | lo(32)]
+      *reinterpret_cast<uint2*>(pr) = make_uint2(h01, h23);
+      *reinterpret_cast<uint2*>(pr + 32) = make_uint2(l01, l23);
+      const float mean = row_sum16((y[0] + y[1]) + (y[2] + y[3])) * (1.f / 64.f);
+      const float d0 = y[0] - mean, d1 = y[1] - mean, d2 = y[2] - mean, d3 = y[3] - mean;
+      const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+      if (g == 0) *reinterpret_cast<float2*>(a.part + (t * a.nslab + slab) * 2) = make_float2(mean, m2);
+    }
   }
 }
 
@@ -436,6 +467,8 @@ WArgs make_args(const AfnoWLaunch& p) {
   a.pre = p.pre;
   a.spec = p.spec;
   a.out = p.out;
+  a.pairs = p.pairs;
+  a.part = p.part;
   a.C = p.C;
   a.nslab = p.C / kSlab;
   a.scale = p.scale;
@@ -467,7 +500,10 @@ void launch_afno_w_c2r_ln(const AfnoWLaunch& p, void* stream) {
   check_launch(p, "afno_w_c2r_ln");
   const WArgs a = make_args(p);
   const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
-  if (p.f32) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  if ((p.pairs != nullptr) != (p.part != nullptr) || (p.pairs && !p.f32))
+    throw std::runtime_error("amd_dft: afno_w_c2r_ln: split pairs and partial statistics come together, fp32 only");
+  if (p.pairs) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  else if (p.f32) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   else hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, false>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_w_c2r_ln launch: ") + hipGetErrorString(e));

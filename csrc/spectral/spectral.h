@@ -78,6 +78,10 @@ struct AfnoWLaunch {
   int O = 0, L = 0, C = 0, KM = 0;
   float scale = 1.f;
   int f32 = 0;                    // fp32 residual stream, spectrum and output
+  // C2R, fp32 only: also the output's bf16x3 split-pair rows [O*L, 2C] (k32-interleaved, the
+  // next GEMM's operand) and its per-64-channel LayerNorm partials [O*L, C/64] (mean, M2)
+  uint16_t* pairs = nullptr;
+  float* part = nullptr;
 };
 bool afno_w_supported(int L, int C, int KM);
 void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4, GPU session 1: the fp32 block without the LayerNorm->split pass (c2r_ln_add_split + linear3_ln) --
+# its GPU tests, the headline bench and a per-kernel table; plus the FNO block baseline at batch 1 / 8.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+step() {
+  local tag=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$tag.log" 2>&1; local rc=$?
+  echo "== $tag rc=$rc"; grep -v amdgpu.ids "gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
+  if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
+}
+TAILN=4 step r4s01_tests 500 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_fp32_path.py -k "ln or split or full_depth or fp32_amd"
+TAILN=3 step r4s01_bench 400 python -u bench.py
+TAILN=6 step r4s01_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
+TAILN=6 step r4s01_fno_b8 300 python -u bench/bench_fno.py --amd-only --rounds 4 --batch 8
+PROF_TAG=_r4s01 timeout -k 10 700 bash scripts/prof_bench.sh > gpurun_out/r4s01_prof.txt 2>&1; echo "prof rc=$?"; head -16 gpurun_out/r4s01_prof.txt

@@ -306,20 +306,41 @@ def _ln_folded_fc(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
                          build)
 
 
+def _ln_folded_fc3(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
+    """fc(LN(x)) with the LayerNorm folded, bf16x3 operands: (split(W * gamma), c1, c2) with
+    c1[n] = sum_k (hi + lo)[n, k] of exactly the split pairs the GEMM reads (so the mean term
+    cancels the GEMM's own representation of W * gamma) and c2 = W beta + b, both summed in fp64.
+    Cached on the Linear module."""
+    def build():
+        w = fc.weight.double()
+        ws = split_bf16((w * ln.weight.double()[None, :]).float())
+        c1 = unsplit_bf16(ws).double().sum(1).float().contiguous()
+        c2 = w @ ln.bias.double()
+        if fc.bias is not None:
+            c2 = c2 + fc.bias.double()
+        return ws, c1, c2.float().contiguous()
+
+    return module_cached(fc, "ln_folded3", (fc.weight, ln.weight, ln.bias) + ((fc.bias,) if fc.bias is not None else ()),
+                         build)
+
+
 def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None,
                          split_out: bool = False):
     """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
 
-      stats = (mean, rstd) of x                  ln_stats (fp32 rows)
+      stats = (mean, rstd) of x                  ln_stats_merge of the previous fc2's partials
+                                                 (first block: ln_stats over x)
       X_w   = R2C_W(LN1(x))                      afno_wfft fp32 instantiation, fp32 spectrum
       Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral bf16x3 variant (fp32 staging)
-      x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32
-      yn    = split(LN2(x1))                     layer_norm_split: [hi | lo] bf16 pair rows
-      h     = split(GELU(yn W1^T + b1))          bf16x3 GEMM, erf GELU, split-pair epilogue
+      x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32, whose epilogue ALSO writes x1's
+                                                 bf16x3 split pairs and LN2's per-64-channel partials
+                                                 (c2r_ln_add_split: no LayerNorm / split pass)
+      st2   = (mean, rstd) of x1                 ln_stats_merge (8 B per token)
+      h     = split(GELU(LN2(x1) W1^T + b1))     bf16x3 GEMM on x1's pairs with LN2 folded into the
+                                                 epilogue (linear3_ln), erf GELU, split-pair output
       x1    = x1 + h W2^T                        bf16x3 GEMM, fp32 residual epilogue, which also
                                                  emits the next LN1's statistics of x1 + b2 as
-                                                 per-64-channel partials (no ln_stats pass over x1
-                                                 in the next block: ln_stats_merge, 50 MB)
+                                                 per-64-channel partials
 
     ``part``: those partials from the previous block (else ln_stats runs).  Returns
     (x1, LnCarry(fc2.bias, partials)); with ``split_out`` (last block) fc2 writes x1 as bf16x3
@@ -335,44 +356,23 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     ops = _ops()
     pre32 = None if pre is None else _f32(blk, "pre", pre)
     g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
-    dup = _DUP  # diagnostic (MI_DFT_DUP): run one stage twice to measure its in-step marginal cost
-    if part is not None and os.environ.get("MI_DFT_FC2_STATS", "1") != "0":
-        stats = ops.ln_stats_merge(part, n1.eps)
-    else:
-        stats = ops.ln_stats(xs, pre32, n1.eps)
-    if dup == "ln_stats":
-        stats = ops.ln_stats(xs, pre32, n1.eps)
+    stats = ops.ln_stats_merge(part, n1.eps) if part is not None else ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
-    if dup == "r2c":
-        xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    if dup == "spectral":
-        yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-    if dup == "c2r":
-        x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-    yn = ops.layer_norm_split(x1.reshape(-1, C), n2.weight, n2.bias, n2.eps, None)
-    if dup == "ln_split":
-        yn = ops.layer_norm_split(x1.reshape(-1, C), n2.weight, n2.bias, n2.eps, None)
-    w1s = module_cached(m, "fc1_split", (m.fc1.weight,), lambda: split_bf16(m.fc1.weight))
+    x1, x1s, part2 = ops.c2r_ln_add_split(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    # ln_stats_merge takes <= 64 chunks of 64 channels
+    st2 = ops.ln_stats_merge(part2, n2.eps) if C <= 64 * 64 else ops.ln_stats(x1, None, n2.eps)
+    w1s, c1, c2 = _ln_folded_fc3(m.fc1, n2)
+    hid = ops.linear3_ln(x1s, w1s, c1, c2, st2, 1)
     w2s = module_cached(m, "fc2_split", (m.fc2.weight,), lambda: split_bf16(m.fc2.weight))
-    b1 = _f32(m, "fc1_b", m.fc1.bias)
-    hid = ops.linear3(yn, w1s, b1, 1, None, True)
-    if dup == "fc1":
-        hid = ops.linear3(yn, w1s, b1, 1, None, True)
-    if split_out and os.environ.get("MI_DFT_HEAD_SPLIT", "1") != "0":
+    if split_out:
         return SplitRows(ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), True)), m.fc2.bias
     if C > 64 * 64:  # ln_stats_merge takes <= 64 chunks of 64 channels
         x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
         return x1, m.fc2.bias
     b2 = _f32(m, "fc2_b", m.fc2.bias)
     x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
-    if dup == "fc2":
-        x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
     return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
-
-
-_DUP = os.environ.get("MI_DFT_DUP", "")
 
 
 _MLP_HAND: Optional[bool] = None

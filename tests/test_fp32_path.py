@@ -86,6 +86,47 @@ def test_linear3_stats_cpu_semantics():
     assert yo.shape == (5, 768) and po.shape == (5, 12, 2)
 
 
+def _ln_fold_operands(w, b, g, be):
+    """(split(W * gamma), c1 from the split pairs, c2 = W beta + b): what _ln_folded_fc3 builds."""
+    ws = ops.split_bf16((w.double() * g.double()[None, :]).float(), True)
+    c1 = unsplit_bf16(ws).double().sum(1).float()
+    c2 = (w.double() @ be.double() + b.double()).float()
+    return ws, c1, c2
+
+
+def test_linear3_ln_cpu_semantics():
+    """fc1 with LN2 folded, bf16x3 operands from the raw residual stream: split(GELU(LN(x) W^T + b))."""
+    torch.manual_seed(11)
+    x, w, b = torch.randn(21, 128) * 2 + 0.7, torch.randn(256, 128) * 0.1, torch.randn(256) * 0.1
+    g, be = torch.randn(128) * 0.3 + 1, torch.randn(128) * 0.1
+    ws, c1, c2 = _ln_fold_operands(w, b, g, be)
+    st = _ln_stats_ref(x)
+    y = ops.linear3_ln(ops.split_bf16(x, True), ws, c1, c2, st, 1)
+    assert y.shape == (21, 512) and y.dtype == torch.bfloat16
+    ref = F.gelu(F.linear(F.layer_norm(x, (128,), g, be, 1e-6), w, b))
+    assert rel_l2(unsplit_bf16(y), ref) < 3e-5
+    assert ops.linear3_ln(torch.empty(5, 1536, device="meta", dtype=torch.bfloat16),
+                          torch.empty(3072, 1536, device="meta", dtype=torch.bfloat16), torch.empty(3072),
+                          None, torch.empty(5, 2), 1).shape == (5, 6144)
+
+
+def test_c2r_ln_add_split_cpu_semantics():
+    """c2r_ln_add + the output's split pairs + its per-64-channel LN partials (merged = ln_stats)."""
+    torch.manual_seed(12)
+    B, H, W, C = 1, 3, 180, 128
+    x = torch.randn(B, H, W, C)
+    g, be, pre = torch.randn(C) * 0.3 + 1, torch.randn(C) * 0.1, torch.randn(C) * 0.2
+    st = ops.ln_stats(x, pre, 1e-6)
+    X = torch.randn(B, H, 46, C, 2)
+    y, pairs, part = ops.c2r_ln_add_split(X, 2, W, 0.01, x, st, g, be, pre)
+    assert torch.equal(y, ops.c2r_ln_add(X, 2, W, 0.01, x, st, g, be, pre))
+    assert pairs.shape == (B * H * W, 2 * C) and part.shape == (B * H * W, C // 64, 2)
+    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C), True))
+    assert torch.allclose(ops.ln_stats_merge(part, 1e-6), _ln_stats_ref(y.reshape(-1, C)), rtol=1e-5, atol=1e-6)
+    with pytest.raises(RuntimeError, match="fp32"):
+        ops.c2r_ln_add_split(X.bfloat16(), 2, W, 0.01, x.bfloat16(), st, g, be, pre)
+
+
 def test_linear3_split_out_with_residual_cpu():
     torch.manual_seed(5)
     x, w, r = torch.randn(7, 128), torch.randn(256, 128) * 0.1, torch.randn(7, 256)
@@ -176,6 +217,53 @@ def test_linear3_stats_gpu(device, M, N, K, with_pre):
     ref = _ln_stats_ref(y.cpu(), pre)
     assert torch.allclose(st, ref, rtol=2e-5, atol=2e-6), (st - ref).abs().max()
     assert torch.allclose(st, ops.ln_stats(y, None if pre is None else pre.to(device), 1e-6).cpu(), rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,mean_scale", [(1000, 0.5), (777, 10.0), (300, 100.0)])
+def test_linear3_ln_gpu_vs_fp64(device, M, mean_scale):
+    """fc1 of the fp32 block: the LayerNorm folded into the bf16x3 GEMM's epilogue, from the raw
+    stream's split pairs.  Rows with a large common mean (|mean| / std = 10, 100) check the
+    mean cancellation rstd * (x W'^T - mean c1): c1 is summed from the same split pairs the GEMM
+    reads, so the error stays at the split's level instead of growing with |mean| / std."""
+    torch.manual_seed(M)
+    K, N = 768, 3072
+    x = torch.randn(M, K) + mean_scale * torch.randn(M, 1)
+    w, b = torch.randn(N, K) / K ** 0.5, torch.randn(N) * 0.1
+    g, be = torch.randn(K) * 0.3 + 1, torch.randn(K) * 0.1
+    ws, c1, c2 = _ln_fold_operands(w, b, g, be)
+    st = _ln_stats_ref(x)
+    ref = F.gelu(F.linear(F.layer_norm(x.double(), (K,), g.double(), be.double(), 1e-6), w.double(), b.double()))
+    d = lambda t: t.to(device)  # noqa: E731
+    y = ops.linear3_ln(ops.split_bf16(d(x), True), d(ws), d(c1), d(c2), d(st), 1)
+    assert y.shape == (M, 2 * N) and y.dtype == torch.bfloat16
+    err = rel_l2(unsplit_bf16(y.cpu()), ref)
+    print(f"linear3_ln |mean|/std ~ {mean_scale}: rel-L2 vs fp64 = {err:.2e}")
+    assert err < 2e-5 * max(1.0, mean_scale / 10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_pre", [False, True])
+def test_c2r_ln_add_split_gpu(device, with_pre):
+    """The AFNO C2R epilogue's extra outputs: split pairs of the fp32 output (bit-exact against
+    split_bf16 of the same output) and per-64-channel LN partials (DPP row sums) vs fp64."""
+    torch.manual_seed(13)
+    B, H, W, C = 2, 90, 180, 768
+    x = torch.randn(B, H, W, C) + 0.5
+    g, be = torch.randn(C) * 0.3 + 1, torch.randn(C) * 0.1
+    pre = torch.randn(C) * 0.2 if with_pre else None
+    st = ops.ln_stats(x, pre, 1e-6)
+    X = torch.randn(B, H, 46, C, 2)
+    d = lambda t: None if t is None else t.to(device)  # noqa: E731
+    S.fallback_reset()
+    y, pairs, part = ops.c2r_ln_add_split(d(X), 2, W, 1.0 / math.sqrt(H * W), d(x), d(st), d(g), d(be), d(pre))
+    assert S.fallback_counts() == {}
+    ref = ops.c2r_ln_add(X, 2, W, 1.0 / math.sqrt(H * W), x, st, g, be, pre)
+    assert rel_l2(y.cpu(), ref) < 2e-6
+    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C), True))
+    stg = ops.ln_stats_merge(part, 1e-6).cpu()
+    sref = _ln_stats_ref(y.cpu().reshape(-1, C))
+    assert torch.allclose(stg, sref, rtol=2e-5, atol=2e-6), (stg - sref).abs().max()
 
 
 @pytest.mark.gpu
