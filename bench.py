@@ -235,6 +235,25 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None):
     return info, runner
 
 
+def _ensure_library(rank: int, world: int, cuda: bool) -> dict:
+    """The benchmarked library must be built from exactly these sources: check the digest the
+    library carries (tensorrt_dft_plugins_amd/_build.py) and rebuild here if it does not match
+    (local rank 0 builds, the others wait).  Recorded in the JSON line."""
+    from tensorrt_dft_plugins_amd import _build
+
+    st = _build.library_status()
+    rebuilt = False
+    if not st["digest_ok"] and not os.environ.get("MI_DFT_LIB"):
+        if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+            log("native library does not match the sources: rebuilding from source")
+            _build.build(from_source=True)
+        rebuilt = True
+        if world > 1:
+            dist.barrier()
+        st = _build.library_status()
+    return {"source_digest_ok": st["digest_ok"], "rebuilt_here": rebuilt}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +287,7 @@ def main(argv=None) -> int:
     dev = torch.device("cuda", local % torch.cuda.device_count()) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(dev)
+    lib_note = _ensure_library(rank, world, cuda)
     tdp.load_plugins()
     gemm_table = None  # hipBLASLt solution tables: bench/experimental/gemm_tables.py (comparator only)
     from tensorrt_dft_plugins_amd.ops.spectral import mlp_on_hand_gemm
@@ -351,6 +371,7 @@ def main(argv=None) -> int:
                                  **({"rccl": rccl} if rccl else {})),
             },
             "model_tflops_per_s": round(tflops, 2),
+            "library": dict(lib_note, build_info=tdp.build_info()),
         }
         out.update(extra)
         line = json.dumps(out)

@@ -40,8 +40,9 @@ at::Tensor ipc_alloc(int64_t bytes, int64_t device) {
   void* p = nullptr;
   hip_ok(hipMalloc(&p, static_cast<size_t>(bytes)), "_ipc_alloc(hipMalloc)");
   auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
-  // freed only when the last tensor reference goes: IpcAllGather.close() drops it after a
-  // barrier, i.e. after every peer has closed its mapping and finished pushing into it
+  // freed only when the last tensor reference goes: IpcAllGather.close() drops it in its second
+  // teardown phase, after a barrier that every peer reaches only once it has unmapped this
+  // buffer (hipIpcCloseMemHandle) and released the events it opened -- never while mapped
   return at::from_blob(p, {bytes}, [](void* q) { (void)hipFree(q); }, opts);
 }
 

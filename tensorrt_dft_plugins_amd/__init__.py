@@ -7,7 +7,7 @@ PyTorch-ROCm custom ops, MFMA spectral-layer kernels, hipGraph engines and RCCL
 data-parallel inference.
 """
 from ._loader import (  # noqa: F401
-    NativeLibraryMissing, get_plugin_creator, is_loaded, load_plugins, native_library_path, plugin_names,
+    NativeLibraryMissing, build_info, get_plugin_creator, is_loaded, load_plugins, native_library_path, plugin_names,
     plugin_registry,
 )
 from .ops.dft import (  # noqa: F401

@@ -8,7 +8,15 @@ by ``hipcc --offload-arch=gfx950`` into objects under ``build/`` and linked into
 looks, like the reference's CMAKE_LIBRARY_OUTPUT_DIRECTORY).  No hipify step, no CUDA
 sources, no rocFFT/hipFFT/hipBLAS link.
 
-Usage: ``python -m tensorrt_dft_plugins_amd._build [--force] [-j N] [--out DIR]``
+Usage: ``python -m tensorrt_dft_plugins_amd._build [--force] [-j N] [--out DIR] [--from-source]``
+
+Provenance: every link embeds ``amd_dft_build_info()`` = the SHA-256 of the sources (all of
+csrc/, the target and the compile flags), the host and the time.  ``build()`` skips work only
+when the library's embedded digest equals the current sources' (not by file times, which a
+snapshot copy does not preserve reliably); ``library_status()`` reports it, and the GPU-tier
+conftest rebuilds the library from source on the GPU box before any test loads it
+(``from_source=True``: every object compiled there), so the GPU tier always runs a library
+compiled on that machine from exactly these sources.
 
 ``--out DIR`` builds a separate copy (objects under DIR/obj, library DIR/_C.so) without touching
 the in-tree one: scripts/ci_gpu.sh compiles every source on the GPU box this way and runs the
@@ -20,7 +28,9 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
+import socket
 import shutil
 import subprocess
 import sys
@@ -63,6 +73,62 @@ def sources():
     for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)):
         out.append((p, "/ops/" in p.replace(os.sep, "/")))
     return out
+
+
+# bump when the compile / link command lines below change (part of the source digest)
+_FLAGS_VERSION = "r4-1"
+_DIGEST_MARK = b"amd_dft_source_digest="
+
+
+def source_digest() -> str:
+    """SHA-256 over every file of csrc/ (path + content), the target arch and the flags version."""
+    h = hashlib.sha256()
+    h.update(f"{ARCH}|{_FLAGS_VERSION}|{os.environ.get('MI_DFT_HIPCC_EXTRA', '')}|"
+             f"{os.environ.get('MI_DFT_DEVICE_CHECKS', '0')}".encode())
+    files = []
+    for ext in ("hip", "cpp", "h"):
+        files += glob.glob(os.path.join(CSRC, "**", f"*.{ext}"), recursive=True)
+    for f in sorted(files):
+        h.update(os.path.relpath(f, CSRC).replace(os.sep, "/").encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def embedded_digest(lib: str) -> str | None:
+    """The source digest a built library carries (read from the file, without loading it)."""
+    try:
+        with open(lib, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(_DIGEST_MARK)
+    if i < 0:
+        return None
+    j = i + len(_DIGEST_MARK)
+    return data[j:j + 64].decode(errors="replace")
+
+
+def library_status(lib: str | None = None) -> dict:
+    """{"path", "exists", "digest_ok"}: does the library match the current sources?"""
+    lib = lib or os.environ.get("MI_DFT_LIB") or LIB
+    d = embedded_digest(lib)
+    return {"path": lib, "exists": os.path.exists(lib), "digest_ok": d is not None and d == source_digest()}
+
+
+def _build_info_obj(obj_dir: str, digest: str) -> str:
+    """A tiny translation unit carrying the provenance string, compiled fresh at every link."""
+    src = os.path.join(obj_dir, "build_info.cpp")
+    info = f"{_DIGEST_MARK.decode()}{digest} host={socket.gethostname()} time={time.strftime('%Y-%m-%dT%H:%M:%SZ', time.gmtime())}"
+    with open(src, "w") as f:
+        f.write('extern "C" const char* amd_dft_build_info() { return "' + info + '"; }\n')
+    obj = src[:-4] + ".o"
+    cmd = [_hipcc(), "-c", "-fPIC", "-x", "c++", "-o", obj, src]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    return obj
 
 
 def _headers_mtime() -> float:
@@ -119,17 +185,25 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False, ob
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True, asan: bool = False,
-          out: str | None = None) -> str:
+          out: str | None = None, from_source: bool = False) -> str:
     """Compile every HIP/C++ source for gfx950 and link ``_C.so``; returns its path.
     ``asan``: host C++ with AddressSanitizer into build/asan/_C.so (device objects shared).
-    ``out``: a separate build directory (objects in out/obj, library out/_C.so)."""
+    ``out``: a separate build directory (objects in out/obj, library out/_C.so).
+    ``from_source``: relink even when the library's digest matches, from objects compiled on
+    THIS host (objects from another host's build directory are not reused: a per-host object
+    directory), i.e. a full compile on a machine that has not built these sources yet."""
     if out and asan:
         raise ValueError("--out and --asan are exclusive")
     obj_dir = os.path.join(os.path.abspath(out), "obj") if out else None
+    if from_source and not out and not asan:
+        obj_dir = os.path.join(ROOT, "build", f"host-{socket.gethostname()}")
     os.makedirs(obj_dir or BUILD, exist_ok=True)
     if asan:
         os.makedirs(BUILD_ASAN, exist_ok=True)
     lib = os.path.join(os.path.abspath(out), "_C.so") if out else (LIB_ASAN if asan else LIB)
+    digest = source_digest()
+    if not (force or from_source) and embedded_digest(lib) == digest:
+        return lib  # up to date with exactly these sources
     tinc, tlib, abi = _torch_paths()
     hdr = _headers_mtime()
     srcs = sources()
@@ -138,7 +212,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
         obj = _obj_path(src, asan, obj_dir)
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
             todo.append((src, nt))
-    jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    jobs = jobs or max(1, min(int(os.environ.get("MAX_JOBS", "8") or 8), os.cpu_count() or 4, 16))
     t0 = time.time()
     if todo:
         if verbose:
@@ -151,7 +225,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
                 if verbose:
                     print("  built", os.path.relpath(futs[f], ROOT), flush=True)
     objs = [_obj_path(s, asan, obj_dir) for s, _ in srcs]
-    if todo or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+    if True:  # digest mismatch, --force or from_source: always relink (with a fresh provenance record)
+        objs = objs + [_build_info_obj(obj_dir or (BUILD_ASAN if asan else BUILD), digest)]
         tmp = lib + ".tmp"
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [
             "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
@@ -163,8 +238,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, lib)
         if verbose:
-            print(f"[amd_dft build] linked {os.path.relpath(lib, ROOT)} ({len(todo)} compiled, "
-                  f"{time.time() - t0:.0f} s)", flush=True)
+            print(f"[amd_dft build] linked {os.path.relpath(lib, ROOT)} ({len(todo)} compiled on "
+                  f"{socket.gethostname()}, {time.time() - t0:.0f} s, sources {digest[:12]})", flush=True)
     return lib
 
 
@@ -174,8 +249,9 @@ def main(argv=None):
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--asan", action="store_true", help="host AddressSanitizer build into build/asan/_C.so")
     ap.add_argument("--out", default=None, help="separate build directory (library at OUT/_C.so)")
+    ap.add_argument("--from-source", action="store_true", help="compile every object on this host and relink")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.j, asan=a.asan, out=a.out)
+    build(force=a.force, jobs=a.j, asan=a.asan, out=a.out, from_source=a.from_source)
 
 
 if __name__ == "__main__":

@@ -53,6 +53,17 @@ def is_loaded() -> bool:
     return _loaded
 
 
+def build_info() -> str:
+    """Provenance of the loaded library: ``amd_dft_source_digest=<sha256 of csrc/> host=<builder>
+    time=<UTC>`` (embedded at link time by ``_build``)."""
+    import ctypes
+
+    load_plugins()
+    fn = ctypes.CDLL(_LIB_PATH).amd_dft_build_info
+    fn.restype = ctypes.c_char_p
+    return fn().decode()
+
+
 def plugin_registry() -> list[dict]:
     """Registered plugin creators: name, version, namespace, ONNX domain and attribute fields.
 

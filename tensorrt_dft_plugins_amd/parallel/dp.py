@@ -122,7 +122,12 @@ class DataParallelInference:
         return self.cap.inputs[0]
 
     def step(self) -> torch.Tensor:
-        """Enqueue one step; returns the (eventually) gathered output buffer of this step."""
+        """Enqueue one step; returns the gathered output buffer of this step.
+
+        The buffer is complete only in stream order: read it after ``drain()`` (GPU: the current
+        stream then waits for the gather; CPU: the gather has finished) -- on the CPU/IPC path the
+        pushes run asynchronously on a worker thread, exactly as on the GPU.  It stays valid until
+        the step two calls later reuses its slot."""
         i = self.k % len(self.cap.outputs)
         self.k += 1
         if self.gather and self.works[i] is not None:

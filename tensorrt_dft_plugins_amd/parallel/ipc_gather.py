@@ -53,9 +53,10 @@ class HipIpcTransport:
         self.device = device
         self.dev = device.index if device.index is not None else torch.cuda.current_device()
         self.ops = torch.ops.amd_dft
-        self._opened: List[int] = []
-        self._events: List[int] = []
-        self._bufs: List[torch.Tensor] = []
+        self._opened: List[int] = []         # peers' buffers mapped into this process
+        self._opened_events: List[int] = []  # peers' events opened in this process
+        self._events: List[int] = []         # this rank's own (exported) events
+        self._bufs: List[torch.Tensor] = []  # this rank's own (exported) buffers
 
     def alloc(self, nbytes: int):
         buf = self.ops._ipc_alloc(nbytes, self.dev)
@@ -75,7 +76,11 @@ class HipIpcTransport:
         return ev, self.ops._ipc_event_handle(ev)
 
     def open_event(self, handle, local_ev, is_self: bool):
-        return local_ev if is_self else self.ops._ipc_event_open(handle, self.dev)
+        if is_self:
+            return local_ev
+        ev = self.ops._ipc_event_open(handle, self.dev)
+        self._opened_events.append(ev)
+        return ev
 
     def push(self, src: torch.Tensor, dst_ptrs: Sequence[int], offset: int) -> None:
         self.ops._ipc_push(src.contiguous(), list(dst_ptrs), offset)
@@ -92,15 +97,27 @@ class HipIpcTransport:
     def synchronize(self) -> None:
         torch.cuda.current_stream(self.device).synchronize()
 
-    def close(self) -> None:
-        """Caller guarantees (barrier) that no peer still pushes into, or reads, these buffers."""
+    def close_imports(self) -> None:
+        """Teardown step 1: unmap every peer buffer and release every peer event this process
+        opened.  Caller guarantees (barrier) that no rank still pushes or waits."""
         torch.cuda.synchronize(self.device)
         for p in self._opened:
             self.ops._ipc_close_mem(p)
+        for ev in self._opened_events:
+            self.ops._ipc_event_destroy(ev)
+        self._opened, self._opened_events = [], []
+
+    def close_own(self) -> None:
+        """Teardown step 2, after a second barrier (every peer has run close_imports, so nobody
+        maps these any more): destroy this rank's exported events and free its buffers."""
         for ev in self._events:
             self.ops._ipc_event_destroy(ev)
-        self._opened, self._events = [], []
+        self._events = []
         self._bufs = []  # the last references: hipFree through the from_blob deleter
+
+    def close(self) -> None:
+        self.close_imports()
+        self.close_own()
 
 
 class _HostStream:
@@ -221,15 +238,21 @@ class ShmTransport:
     def synchronize(self) -> None:
         self.stream.synchronize()
 
-    def close(self) -> None:
+    def close_imports(self) -> None:
         self.stream.synchronize()
         self.stream.stop()
+
+    def close_own(self) -> None:
         for f in self._files:
             try:
                 os.unlink(f)
             except OSError:
                 pass
         self._files = []
+
+    def close(self) -> None:
+        self.close_imports()
+        self.close_own()
 
 
 class IpcAllGather:
@@ -303,11 +326,17 @@ class IpcAllGather:
         self.transport.synchronize()
 
     def close(self) -> None:
-        """Collective: drain this rank's stream, wait until every rank has drained (no push into
-        or read of any buffer is still in flight anywhere), then release handles and buffers."""
+        """Collective, two phases: drain this rank's stream and barrier (no push into or read of
+        any buffer is in flight anywhere); every rank unmaps its peers' buffers and releases the
+        peer events it opened; barrier again (nobody maps anything exported any more); only then
+        does each rank destroy its own events and free its own buffers."""
         if self._closed:
             return
         self.transport.synchronize()
         dist.barrier(group=self.host_group)
-        self.transport.close()
+        self.transport.close_imports()
+        self.peers, self.peer_events, self.peer_rel = [], [], []
+        dist.barrier(group=self.host_group)
+        self.full, self.events, self.rel = [], [], []
+        self.transport.close_own()
         self._closed = True

@@ -48,7 +48,9 @@ def test_afno_kernels_emit_no_src1_high_packed_fp32(tmp_path):
     assert sum(l for l, _ in chk.scan(str(out)).values()) > 0, "scanner no longer sees the form in the reproducer"
 
 
-SO = os.path.join(ROOT, "tensorrt_dft_plugins_amd", "_C.so")
+# the library under test: MI_DFT_LIB when set (CI builds elsewhere and points both tiers at it), else the in-tree
+# one -- the same rule tensorrt_dft_plugins_amd/_loader.py uses, so the scan inspects the binary the tests load
+SO = os.environ.get("MI_DFT_LIB") or os.path.join(ROOT, "tensorrt_dft_plugins_amd", "_C.so")
 
 
 @pytest.mark.skipif(not os.path.exists(SO), reason="library not built")
