@@ -1,5 +1,6 @@
-"""Distributed tier (CPU, Gloo, world_size 2): batch-DP inference with overlapped all-gather
-equals the single-process result; bench.py harness under torch.distributed.run."""
+"""Distributed tier (CPU, Gloo, world sizes 2, 3 and 8): batch-DP inference with overlapped all-gather
+equals the single-process result; bench.py harness under torch.distributed.run (including the
+driver's 8-process launch line)."""
 import os
 import socket
 import subprocess
@@ -91,9 +92,16 @@ def test_dp_allgather_gloo_world2(backend):
 
 @pytest.mark.parametrize("backend", ["rccl", "ipc"])
 def test_dp_allgather_gloo_world3(backend):
-    """An odd world size: every rank's slot offset and every peer push list differ from world 2
-    (rehearses the 8-GPU node's rank arithmetic on the CPU)."""
+    """An odd world size: every rank's slot offset and every peer push list differ from world 2."""
     _run_dp("cpu", backend, world=3)
+
+
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_dp_allgather_gloo_world8(backend):
+    """The 8-GPU node's rank count, rehearsed on the CPU: 8 processes, every rank pushes into 7
+    peers' buffers at 8 different slot offsets (ipc) or joins an 8-way all_gather (rccl path on
+    Gloo), and every rank's gathered output equals the concatenation of the 8 local results."""
+    _run_dp("cpu", backend, world=8)
 
 
 def _slow_consumer_worker(rank, world, port, q, release):
@@ -149,7 +157,7 @@ def _run_slow_consumer(world, release):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_ipc_gather_slow_consumer_slot_reuse(world):
     """Write-after-read across processes: every rank reads step k's gathered slot after it has
     enqueued step k + 1 (the overlap the double buffer is for); the last rank's stream lags (each
@@ -176,12 +184,16 @@ def test_dp_allgather_gloo_world2_on_one_gpu(backend):
     _run_dp("cuda", backend)
 
 
-@pytest.mark.parametrize("extra,scaling,gather_dtype", [([], "weak", None),
-                                                        (["--global-batch", "4", "--gather-dtype", "bf16"], "strong", "bf16")])
-def test_bench_harness_torchrun_gloo(extra, scaling, gather_dtype):
+@pytest.mark.parametrize("nproc,extra,scaling,gather_dtype", [
+    (2, [], "weak", None),
+    (2, ["--global-batch", "4", "--gather-dtype", "bf16"], "strong", "bf16"),
+    (8, [], "weak", None),                                  # the driver's N = 8 launch line, on Gloo
+    (8, ["--global-batch", "32", "--gather", "ipc"], "strong", None),  # SURVEY 5.8 sizing: 4 per rank
+])
+def test_bench_harness_torchrun_gloo(nproc, extra, scaling, gather_dtype):
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--tiny", "--gpus", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--tiny", "--gpus", str(nproc),
            "--steps", "2", "--warmup", "1"] + extra
     # a CPU-tier test: hide any GPU (on the GPU box two ranks would otherwise pick RCCL on one device)
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", MI_DFT_DIST_BACKEND="gloo")
@@ -192,10 +204,14 @@ def test_bench_harness_torchrun_gloo(extra, scaling, gather_dtype):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == scaling and d["config"]["parallelism"] == "dp2"
+    assert d["n_gpus"] == nproc and d["scaling"] == scaling and d["config"]["parallelism"] == f"dp{nproc}"
     assert d["value"] > 0 and d["higher_is_better"] is True
+    assert d["config"]["output_allgather"] is True
     if scaling == "strong":
-        assert d["config"]["global_batch"] == 4 and d["config"]["per_gpu_batch"] == 2
+        g = int(extra[extra.index("--global-batch") + 1])
+        assert d["config"]["global_batch"] == g and d["config"]["per_gpu_batch"] == g // nproc
+    if "--gather" in extra:
+        assert d["config"]["gather_backend"] == extra[extra.index("--gather") + 1]
     if gather_dtype:
         assert d["config"]["gather_dtype"] == gather_dtype
 
