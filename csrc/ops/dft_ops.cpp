@@ -615,28 +615,44 @@ void check_mix_c2c(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t
               "amd_dft.fno_mix_c2c: w must be [Cin, Cout, S * I, 2]");
 }
 
-at::Tensor fno_mix_op(const at::Tensor& x, const at::Tensor& w) {
+at::Tensor fno_mix_op(const at::Tensor& x, const at::Tensor& w, int64_t path) {
   static auto op = c10::Dispatcher::singleton().findSchemaOrThrow("amd_dft::fno_mix", "").typed<at::Tensor(
-      const at::Tensor&, const at::Tensor&)>();
-  return op.call(x, w);
+      const at::Tensor&, const at::Tensor&, int64_t)>();
+  return op.call(x, w, path);
 }
 
 at::Tensor fno_mix_c2c_unfused(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t in_lo, int64_t in_hi,
-                               double scale, bool cuda) {
+                               double scale, bool cuda, int64_t mix_path = 0) {
   const int64_t B = xm.size(0), Cin = xm.size(1), S = xm.size(2), I = xm.size(3), Cout = w.size(1);
-  at::Tensor ym = fno_mix_op(xm.reshape({B, Cin, S * I, 2}), w.reshape({Cin, Cout, S * I, 2})).reshape({B, Cout, S, I, 2});
+  at::Tensor ym = fno_mix_op(xm.reshape({B, Cin, S * I, 2}), w.reshape({Cin, Cout, S * I, 2}), mix_path)
+                      .reshape({B, Cout, S, I, 2});
   return cuda ? c2c_axis_cuda(ym, 2, n, in_lo, in_hi, n, 0, true, scale) : c2c_axis_cpu(ym, 2, n, in_lo, in_hi, n, 0, true, scale);
 }
 
+// Batch size from which the default mixing path is the batched MFMA GEMM (fno_mix.hip, the per-mode
+// weights read once per 8-mode tile for the whole batch) + the pruned inverse C2C, instead of the
+// mixing gather inside the inverse transform (which re-reads every mode's weights once per sample):
+// bench/bench_fno.py --mix-path, profiles/fno_batched_mix_r4.txt.
+constexpr int64_t kFnoMixMfmaMinBatch = 8;
+
+// path: 0 = auto (by batch size, above), 1 = mixing gather inside the inverse H transform,
+//       2 = batched MFMA mixing + pruned inverse C2C (two kernels)
 at::Tensor fno_mix_c2c_cuda(const at::Tensor& xm_, const at::Tensor& w_, int64_t n, int64_t in_lo, int64_t in_hi,
-                            double scale) {
+                            double scale, int64_t path) {
   const c10::DeviceGuard guard(xm_.device());
   check_mix_c2c(xm_, w_, n, in_lo, in_hi);
+  TORCH_CHECK(path >= 0 && path <= 2, "amd_dft.fno_mix_c2c: path must be 0 (auto), 1 (gather) or 2 (mfma)");
   at::Tensor xm = xm_.to(at::kFloat).contiguous();
   at::Tensor w = w_.to(at::kFloat).contiguous();
   const int64_t B = xm.size(0), Cin = xm.size(1), S = xm.size(2), I = xm.size(3), Cout = w.size(1);
   at::Tensor out = alloc_complex({B, Cout, n, I}, xm.options(), at::kFloat);
   if (out.numel() == 0) return out;
+  // the MFMA kernel's LDS tile: 8 modes x (batch x 2Cin + 2Cin x 2Cout + batch x 2Cout) fp32, padded
+  const int64_t Kp = (2 * Cin + 3) & ~3, Bp = (B + 15) & ~15, Np = (2 * Cout + 15) & ~15;
+  const bool fits = 4 * 8 * (Bp * Kp + Kp * Np + Bp * Np) <= 160 * 1024;
+  const bool mfma = path == 2 || (path == 0 && B >= kFnoMixMfmaMinBatch);
+  if (mfma && fits)
+    return checked(fno_mix_c2c_unfused(xm, w, n, in_lo, in_hi, scale, true, 2), "fno_mix_c2c");
   if (Cin < (int64_t(1) << 15) && Cout < (int64_t(1) << 15)) {
     const MixIO mix{w.data_ptr<float>(), static_cast<int>(Cin), static_cast<int>(Cout)};
     if (run_pass(Kind::C2C, xm, out, {B, Cout, S, I}, {B, Cout, n, I}, 2, n, static_cast<int>(in_lo),
@@ -649,12 +665,12 @@ at::Tensor fno_mix_c2c_cuda(const at::Tensor& xm_, const at::Tensor& w_, int64_t
 }
 
 at::Tensor fno_mix_c2c_cpu(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t in_lo, int64_t in_hi,
-                           double scale) {
+                           double scale, int64_t /*path*/) {
   check_mix_c2c(xm, w, n, in_lo, in_hi);
   return fno_mix_c2c_unfused(xm.to(at::kFloat).contiguous(), w.to(at::kFloat).contiguous(), n, in_lo, in_hi, scale, false);
 }
 
-at::Tensor fno_mix_c2c_meta(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t, int64_t, double) {
+at::Tensor fno_mix_c2c_meta(const at::Tensor& xm, const at::Tensor& w, int64_t n, int64_t, int64_t, double, int64_t) {
   return at::empty({xm.size(0), w.size(1), n, xm.size(3), 2}, xm.options().dtype(at::kFloat));
 }
 
@@ -1141,7 +1157,7 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("c2c_axis(Tensor x, int dim, int n, int in_lo, int in_hi, int out_lo, int out_hi, bool inverse=False, "
         "float scale=1.0) -> Tensor");
   m.def("dftw_r2c(Tensor x, int m, float scale=1.0) -> Tensor");
-  m.def("fno_mix_c2c(Tensor xm, Tensor w, int n, int in_lo, int in_hi, float scale=1.0) -> Tensor");
+  m.def("fno_mix_c2c(Tensor xm, Tensor w, int n, int in_lo, int in_hi, float scale=1.0, int path=0) -> Tensor");
   m.def("r2c_ln(Tensor x, int dim, float scale, int keep, Tensor stats, Tensor gamma, Tensor beta, Tensor? pre=None, "
         "ScalarType? out_dtype=None) -> Tensor");
   m.def("c2r_ln_add(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "

@@ -110,7 +110,7 @@ bool afno_spectral_ok(int64_t H, int64_t block_size) {
 
 // ------------------------------------------------------------------ FNO mode mixing
 // x [B, Cin, M, 2] fp32, w [Cin, Cout, M, 2] fp32 -> y [B, Cout, M, 2] fp32
-at::Tensor fno_mix_cpu(const at::Tensor& x, const at::Tensor& w) {
+at::Tensor fno_mix_cpu(const at::Tensor& x, const at::Tensor& w, int64_t /*path*/) {
   TORCH_CHECK(x.dim() == 4 && x.size(3) == 2 && w.dim() == 4 && w.size(3) == 2 && w.size(0) == x.size(1) &&
                   w.size(2) == x.size(2),
               "fno_mix: x [B, Cin, M, 2], w [Cin, Cout, M, 2]");
@@ -124,7 +124,8 @@ bool fno_mix_fits(int64_t B, int64_t Cin, int64_t Cout) {
   return 4 * 8 * (Bp * Kp + Kp * Np + Bp * Np) <= 160 * 1024;
 }
 
-at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
+// path: 0 = auto (scalar split-K stream for B <= 8, the MFMA kernel above), 2 = the MFMA kernel at any B
+at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_, int64_t path) {
   const c10::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.dim() == 4 && x_.size(3) == 2 && w_.dim() == 4 && w_.size(3) == 2 && w_.size(0) == x_.size(1) &&
                   w_.size(2) == x_.size(2),
@@ -132,7 +133,7 @@ at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
   const int64_t B = x_.size(0), Cin = x_.size(1), M = x_.size(2), Cout = w_.size(1);
   if (!fno_mix_fits(B, Cin, Cout)) {  // ATen on the device tensors
     fallback_note("fno_mix", "operand tiles exceed the 160 KB LDS");
-    return fno_mix_cpu(x_, w_);
+    return fno_mix_cpu(x_, w_, path);
   }
   at::Tensor x = x_.to(at::kFloat).contiguous(), w = w_.to(at::kFloat).contiguous();
   at::Tensor y = at::empty({B, Cout, M, 2}, x.options());
@@ -144,11 +145,12 @@ at::Tensor fno_mix_cuda(const at::Tensor& x_, const at::Tensor& w_) {
   p.Cin = static_cast<int>(Cin);
   p.Cout = static_cast<int>(Cout);
   p.M = static_cast<int>(M);
+  p.mfma = path == 2 ? 1 : 0;
   launch_fno_mix(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
   return checked(y, "fno_mix");
 }
 
-at::Tensor fno_mix_meta(const at::Tensor& x, const at::Tensor& w) {
+at::Tensor fno_mix_meta(const at::Tensor& x, const at::Tensor& w, int64_t) {
   return at::empty({x.size(0), w.size(1), x.size(2), 2}, x.options().dtype(at::kFloat));
 }
 
@@ -493,7 +495,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
   m.def("ln_stats_merge(Tensor part, float eps=1e-6) -> Tensor");
   m.def("layer_norm_split(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? pre=None) -> Tensor");
-  m.def("fno_mix(Tensor x, Tensor w) -> Tensor");
+  m.def("fno_mix(Tensor x, Tensor w, int path=0) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
   m.def("fno_c2r_pw(Tensor yw, Tensor x, Tensor wc, Tensor? bias=None, bool gelu=True) -> Tensor");
 }

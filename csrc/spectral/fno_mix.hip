@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) fno_mix_small_kernel(const float2* __rest
 
 void launch_fno_mix(const FnoMixLaunch& p, void* stream) {
   if (p.B <= 0 || p.M <= 0) return;
-  if (p.B <= 8) {
+  if (p.B <= 8 && !p.mfma) {
     const int64_t n = static_cast<int64_t>(p.Cout) * p.M;
     const dim3 grid(static_cast<uint32_t>((n + 63) / 64));
     hipStream_t st = static_cast<hipStream_t>(stream);

@@ -33,6 +33,7 @@ struct FnoMixLaunch {
   const float* w;   // [Cin, Cout, M, 2] fp32
   float* y;         // [B, Cout, M, 2] fp32
   int B, Cin, Cout, M;
+  int mfma = 0;     // 1: the batched MFMA kernel even for B <= 8 (weights read once per mode tile)
 };
 void launch_fno_mix(const FnoMixLaunch& p, void* stream);
 

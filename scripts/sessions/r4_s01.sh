@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, GPU session 1: the fp32 block without the LayerNorm->split pass (c2r_ln_add_split + linear3_ln) --
-# its GPU tests, the headline bench and a per-kernel table; plus the FNO block baseline at batch 1 / 8.
+# its GPU tests (library compiled from source on the box by the GPU-tier conftest), the headline bench and a
+# per-kernel table; the FNO block baseline and the batched MFMA mixing path at batch 1 / 8 / 32.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
@@ -11,8 +12,8 @@ step() {
   echo "== $tag rc=$rc"; grep -v amdgpu.ids "gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
   if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
 }
-TAILN=4 step r4s01_tests 500 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_fp32_path.py -k "ln or split or full_depth or fp32_amd"
+TAILN=6 step r4s01_tests 700 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_fp32_path.py tests/test_fno.py -k "ln or split or full_depth or fp32_amd or mix"
 TAILN=3 step r4s01_bench 400 python -u bench.py
+TAILN=8 step r4s01_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
 TAILN=6 step r4s01_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
-TAILN=6 step r4s01_fno_b8 300 python -u bench/bench_fno.py --amd-only --rounds 4 --batch 8
 PROF_TAG=_r4s01 timeout -k 10 700 bash scripts/prof_bench.sh > gpurun_out/r4s01_prof.txt 2>&1; echo "prof rc=$?"; head -16 gpurun_out/r4s01_prof.txt

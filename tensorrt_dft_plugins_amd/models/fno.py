@@ -105,6 +105,9 @@ class FNOBlock(nn.Module):
         self.w = nn.Conv2d(width, width, 1)
         self.activation = activation
         self.backend = backend
+        # mode-mixing path of the amd backend: 0 = by batch size (the native op's rule), 1 = inside
+        # the inverse H transform's gather, 2 = batched MFMA GEMM (weights read once per batch)
+        self.mix_path = 0
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.backend == "amd":
@@ -114,7 +117,9 @@ class FNOBlock(nn.Module):
 
     def _forward_amd(self, x: torch.Tensor) -> torch.Tensor:
         """pruned R2C (MFMA DFT-GEMM along W + pruned FFT along H) -> [mode mixing + pruned inverse
-        FFT along H] -> fused [inverse DFT-GEMM along W + 1x1 conv + bias + GELU]: four kernels."""
+        FFT along H] -> fused [inverse DFT-GEMM along W + 1x1 conv + bias + GELU]: four kernels.
+        From batch 8 the mixing runs as batched per-mode GEMMs on MFMA (fno_mix.hip: every mode's
+        weights read once for the whole batch) followed by the pruned inverse transform: five."""
         sp = self.spectral
         B, C, H, W = x.shape
         sp._check(H, W)
@@ -124,7 +129,7 @@ class FNOBlock(nn.Module):
         xm = ops.c2c_axis(xw, 2, H, H, 0, m1, m1, False, 1.0)  # [B, Cin, 2*m1, m2, 2]
         # mode mixing inside the inverse H transform's gather (one kernel; fno_mix + c2c_axis
         # where no fixed column kernel covers H)
-        yw = ops.fno_mix_c2c(xm, sp._packed_weight(), H, m1, m1, 1.0 / (H * W))  # [B, Cout, H, m2, 2]
+        yw = ops.fno_mix_c2c(xm, sp._packed_weight(), H, m1, m1, 1.0 / (H * W), self.mix_path)  # [B, Cout, H, m2, 2]
         return ops.fno_c2r_pw(yw, x, self.w.weight.reshape(self.w.out_channels, -1).float(), self.w.bias.float(),
                               self.activation)
 

@@ -270,3 +270,38 @@ def test_fno_mix_c2c_gpu(device):
         ref = _mix_c2c_reference(xm, w, n, lo, hi, 1.0 / n)
         out = torch.ops.amd_dft.fno_mix_c2c(xm.to(device), w.to(device), n, lo, hi, 1.0 / n)
         assert rel_l2(out.cpu(), ref) < 2e-6, (B, Ci, Co, n, lo, hi, I)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", [1, 2])
+def test_fno_mix_c2c_paths_gpu(device, path):
+    """Both mixing paths of fno_mix_c2c at a batched FNO shape (B = 8): the gather inside the inverse
+    H transform (1) and the batched MFMA GEMM + pruned inverse C2C (2), vs the fp64 composition."""
+    torch.manual_seed(23)
+    B, Ci, Co, n, lo, hi, I = 8, 20, 20, 720, 32, 32, 32
+    xm = torch.randn(B, Ci, lo + hi, I, 2)
+    w = torch.randn(Ci, Co, (lo + hi) * I, 2)
+    ref = _mix_c2c_reference(xm, w, n, lo, hi, 1.0 / n)
+    out = torch.ops.amd_dft.fno_mix_c2c(xm.to(device), w.to(device), n, lo, hi, 1.0 / n, path)
+    assert rel_l2(out.cpu(), ref) < 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix_path", [1, 2])
+def test_fno_block_batched_mfma_mix_gpu(device, mix_path):
+    """The FNO block at batch 8 with the mode mixing on the batched MFMA kernel (2) and in the
+    gather (1) against the plain-PyTorch SpectralConv2d reference (spectral_conv2d_reference + conv
+    + GELU); no ATen fallback on either path."""
+    from tensorrt_dft_plugins_amd.ops import spectral as S
+
+    torch.manual_seed(24)
+    blk = _block(20, 32, 32).to(device)
+    x = torch.randn(8, 20, 720, 1440, device=device)
+    with torch.no_grad():
+        ref = blk(x)
+        blk.backend = blk.spectral.backend = "amd"
+        blk.mix_path = mix_path
+        S.fallback_reset()
+        out = blk(x)
+    assert S.fallback_counts() == {}
+    assert rel_l2(out, ref) < 1e-4
