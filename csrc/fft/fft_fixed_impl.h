@@ -15,6 +15,16 @@
 
 #include <hip/hip_runtime.h>
 
+// Twiddle source of passes 1..P-1:
+//   0: the plan's global table (L1/L2 resident), each thread's twiddles of pass p + 1 prefetched
+//      into registers while pass p runs;
+//   1: the whole table staged into LDS by the workgroup at kernel start (coalesced 8-byte loads
+//      issued together with pass 0's global loads), each pass reading its twiddles from LDS after
+//      its barrier (no prefetch registers).
+#ifndef AMD_DFT_TW_LDS
+#define AMD_DFT_TW_LDS 0
+#endif
+
 #include "fft_fixed.h"
 #include "radix.h"
 
@@ -153,6 +163,7 @@ struct Ctx {
   bool ok0, ok1;    // c < I (C2C) / 2c < I, 2c+1 < I (paired)
   int t, tp;
   float2* lds;
+  float2* twl;  // AMD_DFT_TW_LDS: the plan's twiddle table staged in LDS (filled during pass 0)
   // NADD == 3 (LayerNorm IO): stats of this outer row, per-channel params of the signal pair
   const float2* st;
   float2 g, be, pre;
@@ -328,7 +339,10 @@ __device__ __forceinline__ void load_tw(const Ctx& x, float2 (&tw)[PassGeom<F, T
       if (G::EXACT || j < G::LR) {
         const int k = j % G::Ns;
 #pragma unroll
-        for (int r = 1; r < G::R; ++r) tw[q][r - 1] = x.a.tw[F::goff(P) + (r - 1) * G::Ns + k];
+        for (int r = 1; r < G::R; ++r) {
+          if constexpr (AMD_DFT_TW_LDS) tw[q][r - 1] = x.twl[F::goff(P) + (r - 1) * G::Ns + k];
+          else tw[q][r - 1] = x.a.tw[F::goff(P) + (r - 1) * G::Ns + k];
+        }
       }
     }
   }
@@ -343,6 +357,16 @@ struct Step {
 
   __device__ __forceinline__ static void run(const Ctx& x, float2 (&tw)[G::Q][G::TWR]) {
     constexpr int R = G::R, LR = G::LR, Q = G::Q, Ns = G::Ns;
+    if constexpr (AMD_DFT_TW_LDS) {  // twiddles read from LDS inside body, after its barrier
+      body(x, tw);
+      AMD_DFT_STAMP(x.a, 3 + P, static_cast<long long>(__builtin_amdgcn_s_memtime()));
+      if constexpr (!LAST) {
+        using GN = PassGeom<F, TP, P + 1>;
+        float2 twn[GN::Q][GN::TWR];
+        Step<K, COLS, TP, T, F, P + 1, BFI, BFO, PR, NADD, PV>::run(x, twn);
+      }
+      return;
+    }
     // prefetch next pass' twiddles
     if constexpr (!LAST) {
       using GN = PassGeom<F, TP, P + 1>;
@@ -384,7 +408,13 @@ struct Step {
         }
       }
     }
+    if constexpr (AMD_DFT_TW_LDS && P == 0 && F::goff(F::N) > 0) {
+      // stage the twiddle table behind pass 0's gather loads (one memory round trip for both);
+      // pass 0's closing barrier publishes it to passes 1..P-1
+      for (int i = static_cast<int>(threadIdx.x); i < F::goff(F::N); i += TP * T) x.twl[i] = x.a.tw[i];
+    }
     if constexpr (P > 0) __syncthreads();  // all reads of the shared buffer done
+    if constexpr (AMD_DFT_TW_LDS) load_tw<F, TP, P>(x, tw);  // staged table, visible since pass 0's barrier
     // ---- twiddle + butterfly
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -436,7 +466,8 @@ __device__ __forceinline__ int32_t xcd_block(int32_t b, int32_t nb) {
 }
 
 template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>
-__device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int tid, bool active, float2* lds) {
+__device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int tid, bool active, float2* lds,
+                                           float2* twl = nullptr) {
   constexpr int L = F::L;
   Ctx x;
   x.a = a;
@@ -481,6 +512,7 @@ __device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int 
     x.pre = a.ln_pre ? *reinterpret_cast<const float2*>(a.ln_pre + ch) : make_float2(0.f, 0.f);
   }
   x.lds = lds;
+  x.twl = twl;
   AMD_DFT_STAMP(a, 0, static_cast<long long>(__builtin_amdgcn_s_memrealtime()));
   AMD_DFT_STAMP(a, 1, static_cast<long long>(__builtin_amdgcn_s_memtime()));
   using G0 = PassGeom<F, TP, 0>;
@@ -527,7 +559,13 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   __shared__ __attribute__((aligned(16))) float2 lds[tile_lds<COLS, T, F::L>()];
   const int32_t bid = a.xcd_nb > 0 ? xcd_block(static_cast<int32_t>(blockIdx.x), a.xcd_nb)
                                    : static_cast<int32_t>(blockIdx.x);
-  fixed_tile<K, COLS, TP, T, F, BFI, BFO, PR, NADD, PV>(a, bid, static_cast<int>(threadIdx.x), true, lds);
+  if constexpr (AMD_DFT_TW_LDS) {
+    constexpr int TWN = F::goff(F::N) > 0 ? F::goff(F::N) : 1;
+    __shared__ float2 twl[TWN];  // filled by pass 0 after its gather loads are issued
+    fixed_tile<K, COLS, TP, T, F, BFI, BFO, PR, NADD, PV>(a, bid, static_cast<int>(threadIdx.x), true, lds, twl);
+  } else {
+    fixed_tile<K, COLS, TP, T, F, BFI, BFO, PR, NADD, PV>(a, bid, static_cast<int>(threadIdx.x), true, lds);
+  }
 }
 
 // ------------------------------------------------------------------ config table

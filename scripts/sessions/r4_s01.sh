@@ -17,3 +17,11 @@ TAILN=3 step r4s01_bench 400 python -u bench.py
 TAILN=8 step r4s01_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
 TAILN=6 step r4s01_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
 PROF_TAG=_r4s01 timeout -k 10 700 bash scripts/prof_bench.sh > gpurun_out/r4s01_prof.txt 2>&1; echo "prof rc=$?"; head -16 gpurun_out/r4s01_prof.txt
+# rfft2 / irfft2 720x1440: LDS-staged twiddles (variants/twlds = -DAMD_DFT_TW_LDS=1) vs the L1-table prefetch, ABAB
+for r in 1 2; do
+  step r4s01_fft_def_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_def_$r.json
+
+  python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_def_$r.json'));print('default', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
+  MI_DFT_LIB=$PWD/variants/twlds/_C.so step r4s01_fft_tw_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_tw_$r.json
+  python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_tw_$r.json'));print('twlds  ', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
+done
