@@ -98,7 +98,10 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
   // past nblk are clamped loads with zeroed data): a conditional consumer lets the compiler
   // sink each load down to its use, which serialises the batch into one round trip per block.
   // PF divides the per-wave block count of the 1440-wide FNO rows (8 at NW = 3, 6 at NW = 4).
-  constexpr int PF = G >= 4 ? 2 : BF ? (NW == 3 ? 4 : 6) : 3;
+#ifndef DFTW_PF_BF3
+#define DFTW_PF_BF3 4  // bf16 blocks per batch at NW = 3 (8 = a wave's whole share of a 1440 row in one batch)
+#endif
+  constexpr int PF = G >= 4 ? 2 : BF ? (NW == 3 ? DFTW_PF_BF3 : 6) : 3;
   // The first batch is requested before the phase table is copied and the workgroup synchronises,
   // so the table's and the samples' global round trips overlap instead of following each other.
   Raw buf[PF][kNKS][NR];

@@ -25,3 +25,8 @@ for r in 1 2; do
   MI_DFT_LIB=$PWD/variants/twlds/_C.so step r4s01_fft_tw_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_tw_$r.json
   python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_tw_$r.json'));print('twlds  ', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
 done
+# FNO block: dftw_r2c with a wave's whole 1440-row share in one load batch (variants/dftwpf8) vs default, ABAB
+for r in 1 2; do
+  TAILN=2 step r4s01_fno_def_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5
+  MI_DFT_LIB=$PWD/variants/dftwpf8/_C.so TAILN=2 step r4s01_fno_pf8_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5
+done
