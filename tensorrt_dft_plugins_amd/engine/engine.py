@@ -191,9 +191,16 @@ class Engine:
 
     __call__ = infer
 
-    def execute_v2(self, bindings: Sequence[Union[int, torch.Tensor]]) -> bool:
-        """TensorRT-style synchronous execute: ``bindings`` = input then output device pointers
-        (ints) or tensors, in binding order (reference: test_dft.py:112-114)."""
+    @property
+    def binding_tensors(self) -> List[torch.Tensor]:
+        """The engine's own binding buffers (inputs then outputs; the captured graph reads and
+        writes exactly these).  Passing their pointers to ``execute_v2`` runs with zero copies."""
+        return list(self.static_inputs) + list(self.static_outputs)
+
+    def binding_ptrs(self) -> List[int]:
+        return [t.data_ptr() for t in self.binding_tensors]
+
+    def _views(self, bindings: Sequence[Union[int, torch.Tensor]]) -> List[torch.Tensor]:
         n_in, n_out = len(self.static_inputs), len(self.static_outputs)
         if len(bindings) != n_in + n_out:
             raise ValueError(f"expected {n_in + n_out} bindings, got {len(bindings)}")
@@ -201,17 +208,36 @@ class Engine:
         for b, t in zip(bindings, self.static_inputs + self.static_outputs):
             if isinstance(b, torch.Tensor):
                 views.append(b)
+            elif int(b) == t.data_ptr():
+                views.append(t)  # the engine's own buffer: no wrapper, no copy
             elif self.device.type == "cuda":
                 views.append(torch.ops.amd_dft.wrap_device_ptr(int(b), list(t.shape), t.dtype, self.device.index or 0))
             else:
                 views.append(torch.ops.amd_dft.wrap_host_ptr(int(b), list(t.shape), t.dtype))
+        return views
+
+    def execute_async_v2(self, bindings: Sequence[Union[int, torch.Tensor]]) -> bool:
+        """TensorRT-style asynchronous execute on the current stream: ``bindings`` = input then
+        output device pointers (ints) or tensors in binding order.  Bindings that ARE the engine's
+        buffers (``binding_ptrs()``) are used in place; others are copied in / out on the stream
+        (the captured graph is bound to its own buffers).  Returns without waiting."""
+        views = self._views(bindings)
+        n_in = len(self.static_inputs)
         for si, v in zip(self.static_inputs, views[:n_in]):
-            si.copy_(v)
+            if v.data_ptr() != si.data_ptr():
+                si.copy_(v)
         self.enqueue()
         for so, v in zip(self.static_outputs, views[n_in:]):
-            v.copy_(so)
+            if v.data_ptr() != so.data_ptr():
+                v.copy_(so)
+        return True
+
+    def execute_v2(self, bindings: Sequence[Union[int, torch.Tensor]]) -> bool:
+        """TensorRT-style synchronous execute (reference: test_dft.py:112-114): as
+        ``execute_async_v2``, then waits for the stream (the reference's call is blocking)."""
+        self.execute_async_v2(bindings)
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            torch.cuda.current_stream(self.device).synchronize()
         return True
 
     # ------------------------------------------------------------------ (de)serialisation

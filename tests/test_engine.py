@@ -54,6 +54,22 @@ def test_engine_execute_v2_host_pointers_cpu():
     assert torch.allclose(y, torch.view_as_real(torch.fft.rfft2(x)), atol=1e-5)
 
 
+def test_engine_execute_v2_own_bindings_zero_copy_cpu():
+    """Bindings that are the engine's own buffers run in place (TensorRT-style preallocated
+    bindings); execute_async_v2 returns without waiting."""
+    x = torch.randn(1, 1, 4, 8)
+    eng = Engine.build(Rfft2Model(), (x,), device="cpu")
+    xin, yout = eng.binding_tensors
+    xin.copy_(x)
+    ptr_out = yout.data_ptr()
+    assert eng.execute_v2(eng.binding_ptrs())
+    assert yout.data_ptr() == ptr_out
+    assert torch.allclose(yout, torch.view_as_real(torch.fft.rfft2(x)), atol=1e-5)
+    y2 = torch.empty_like(yout)
+    assert eng.execute_async_v2([xin.data_ptr(), y2.data_ptr()])  # mixed: own input, foreign output
+    assert torch.allclose(y2, yout)
+
+
 def test_engine_rejects_bad_file():
     with pytest.raises(ValueError, match="magic"):
         Engine.deserialize(b"not an engine")
@@ -95,6 +111,10 @@ def test_engine_hipgraph_gpu(device, tmp_path):
     y = torch.empty(2, 4, 720, 1440, device=device)
     eng2.execute_v2([xg.data_ptr(), y.data_ptr()])
     assert torch.allclose(y.cpu(), 0.25 * x, atol=1e-5)
+    # zero-copy: the engine's own bindings, graph replay straight on them
+    eng2.binding_tensors[0].copy_(xg * 2)
+    eng2.execute_v2(eng2.binding_ptrs())
+    assert torch.allclose(eng2.binding_tensors[1].cpu(), 0.5 * x, atol=1e-5)
     st = eng2.benchmark(iterations=20, warmup=2)
     assert st["latency_median_ms"] > 0
 
