@@ -434,23 +434,29 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       for (int h = 0; h < 2; ++h) {
         const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
         RT rr[RES ? NIT : 1];
-        if constexpr (RES) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16 features per lane
-#pragma unroll
-          for (int it = 0; it < NIT; ++it) {
-            int rt = min(tbase + it * RPI + rsub, M - 1);
-            if constexpr (MODE == 1) {
-              if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
-            }
-            if constexpr (OUT == 2) {
-              const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
-              const float* rp = static_cast<const float*>(p.residual) + o;
-              rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
-            } else {
-              const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
-              if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
-              else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
-            }
+        // residual rows are prefetched PD passes ahead of their use: all NIT before the half is
+        // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
+        // for OUT 2 (8 fp32 per pass: the whole half would hold 128 VGPRs beside the accumulators)
+        // -- each of those spilled when the whole half was prefetched
+        constexpr int PD = OUT == 2 ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
+        auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
+          int rt = min(tbase + it * RPI + rsub, M - 1);
+          if constexpr (MODE == 1) {
+            if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
           }
+          if constexpr (OUT == 2) {
+            const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
+            const float* rp = static_cast<const float*>(p.residual) + o;
+            rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
+          } else {
+            const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
+            if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
+            else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+          }
+        };
+        if constexpr (RES) {
+#pragma unroll
+          for (int it = 0; it < PD; ++it) load_rr(it);
         }
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
@@ -469,6 +475,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
+          if constexpr (RES && PD < NIT) {
+            if (it + PD < NIT) load_rr(it + PD);
+          }
           const int row = it * RPI + rsub, t = tbase + row;
           const char* rp = reg + row * 256;
           if constexpr (OUT == 1) {

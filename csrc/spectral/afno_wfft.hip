@@ -293,8 +293,14 @@ __device__ __forceinline__ float row_sum16(float x) {
 // (the 16 lanes of one DPP row hold one position's 64 channels).  That removes the separate
 // LayerNorm -> split pass over the residual stream (one full read of it per block); LN2 is then
 // folded into fc1's epilogue (linear3_ln) from per-token stats merged by ln_stats_merge.
+// Register budget (workgroups per CU): the fp32 instantiation holds the 15-point DFT (60 VGPRs) and
+// its 15 positions' addends (90) across the DFT; with the split / statistics epilogue that needs
+// ~256 VGPRs, i.e. 2 workgroups per CU (at 3 it spilled ~400 bytes per lane).
+#ifndef AFNO_C2R_SPLIT_OCC
+#define AFNO_C2R_SPLIT_OCC 2
+#endif
 template <int KM, bool F32, bool SPLIT = false>
-__global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs a) {
+__global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(!SPLIT || F32, "split-pair outputs come with the fp32 instantiation");
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
   // bf16 (XLDS): fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its
@@ -423,6 +429,8 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
   void* ob = F32 ? static_cast<void*>(static_cast<float*>(a.out) + obase)
                  : static_cast<void*>(static_cast<uint16_t*>(a.out) + obase);
   const float sc = a.scale;
+  uint16_t* const pbase = SPLIT ? a.pairs + static_cast<int64_t>(o) * kL * (2 * C) : nullptr;
+  float* const sbase_part = SPLIT ? a.part + (static_cast<int64_t>(o) * kL * a.nslab + slab) * 2 : nullptr;
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
     float xp[kCh], h[kCh];
@@ -442,19 +450,22 @@ __global__ void __launch_bounds__(kThreads, 3) afno_w_c2r_ln_kernel(const WArgs 
     }
     stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
     if constexpr (SPLIT) {
+      // workgroup-uniform bases (o's first token) + 32-bit lane offsets: position n = k1 + 12 k2
       const int n = k1 + kA * k2;
-      const int64_t t = static_cast<int64_t>(o) * kL + n;  // token
       const uint32_t h01 = bfpack(y[0], y[1]), h23 = bfpack(y[2], y[3]);
       const uint32_t l01 = bfpack(y[0] - __uint_as_float(h01 << 16), y[1] - __uint_as_float(h01 & 0xffff0000u));
       const uint32_t l23 = bfpack(y[2] - __uint_as_float(h23 << 16), y[3] - __uint_as_float(h23 & 0xffff0000u));
-      uint16_t* pr = a.pairs + t * (2 * C) + (c0 >> 5) * 64 + (c0 & 31);  // k32-interleaved [hi(32) | lo(32)]
+      uint16_t* pr = pbase + (n * (2 * C) + (c0 >> 5) * 64 + (c0 & 31));  // k32-interleaved [hi(32) | lo(32)]
       *reinterpret_cast<uint2*>(pr) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(pr + 32) = make_uint2(l01, l23);
       const float mean = row_sum16((y[0] + y[1]) + (y[2] + y[3])) * (1.f / 64.f);
       const float d0 = y[0] - mean, d1 = y[1] - mean, d2 = y[2] - mean, d3 = y[3] - mean;
       const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
-      if (g == 0) *reinterpret_cast<float2*>(a.part + (t * a.nslab + slab) * 2) = make_float2(mean, m2);
+      if (g == 0) *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) = make_float2(mean, m2);
     }
+    // one output position at a time: interleaving the positions' epilogues (the scheduler's
+    // choice) keeps several positions' temporaries live and spills the fp32 instantiations
+    if constexpr (F32) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
