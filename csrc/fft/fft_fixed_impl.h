@@ -574,7 +574,8 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
 // of 5..8 points per thread per pass, ~4.5 waves per transform -- beat (10, 12, 12) at 144 threads
 // (10-12 points per thread, ~2.3 waves) on rfft2 720x1440: 12.27-12.32 vs 12.70-12.78 us, irfft2
 // unchanged (12.14-12.23 vs 12.13-12.14); 180-thread (4, 4, 5, 9) 720-point columns lost
-// (irfft2 12.36-12.42): profiles/fft_plans_r3.txt.
+// (irfft2 12.36-12.42): profiles/fft_plans_r3.txt.  720 = (24, 30): two passes (one LDS round trip
+// fewer) at 30 threads per transform, A/B via MI_DFT_FFT_RADICES="720:24,30" (round 4).
 #define AMD_DFT_FIXED_CONFIGS(X)          \
   X(1440, false, 288, 1, 5, 6, 6, 8)      \
   X(1440, false, 144, 1, 10, 12, 12)      \
@@ -583,12 +584,15 @@ __global__ void __launch_bounds__(TP * T) fft_fixed_kernel(const FixedArgs a) {
   X(2048, false, 256, 1, 8, 16, 16)       \
   X(512, false, 64, 2, 8, 8, 8)           \
   X(256, false, 16, 4, 16, 16)            \
+  X(720, false, 30, 2, 24, 30)            \
   X(720, true, 90, 4, 8, 9, 10)           \
   X(720, true, 90, 2, 8, 9, 10)           \
   X(720, true, 45, 8, 8, 9, 10)           \
   X(720, true, 45, 4, 8, 9, 10)           \
   X(720, true, 90, 8, 8, 9, 10)           \
   X(720, true, 45, 16, 8, 9, 10)          \
+  X(720, true, 30, 4, 24, 30)             \
+  X(720, true, 30, 8, 24, 30)             \
   X(90, true, 10, 16, 9, 10)              \
   X(180, true, 15, 16, 12, 15)            \
   X(180, true, 15, 32, 12, 15)

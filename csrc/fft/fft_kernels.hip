@@ -261,6 +261,8 @@ __global__ void __launch_bounds__(256) fft_pass_kernel(const PassDesc d) {
       case 13: stockham_pass<13>(src, dst, tw, L, logT, Ns, d.ns_div[p]); break;
       case 15: stockham_pass<15>(src, dst, tw, L, logT, Ns, d.ns_div[p]); break;
       case 16: stockham_pass<16>(src, dst, tw, L, logT, Ns, d.ns_div[p]); break;
+      case 24: stockham_pass<24>(src, dst, tw, L, logT, Ns, d.ns_div[p]); break;
+      case 30: stockham_pass<30>(src, dst, tw, L, logT, Ns, d.ns_div[p]); break;
       default:
         stockham_pass_generic(src, dst, tw, tw_s + d.rootoff[p], R, L, logT, Ns, d.ns_div[p]);
         break;

@@ -76,8 +76,14 @@ Best search(int32_t L, std::map<int32_t, Best>& memo) {
 
 }  // namespace
 
+// radices with a compile-time butterfly that only a fixed-kernel configuration's radix order
+// selects (AMD_DFT_FIXED_CONFIGS): no root table in the plan, never chosen by search()
+const int kFixedOnly[] = {24, 30};
+
 bool radix_is_specialised(int r) {
   for (int s : kSpecialised)
+    if (s == r) return true;
+  for (int s : kFixedOnly)
     if (s == r) return true;
   return false;
 }

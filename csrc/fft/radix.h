@@ -211,5 +211,8 @@ template <> struct Dft<10> : DftComp<2, 5> {};
 template <> struct Dft<12> : DftComp<4, 3> {};
 template <> struct Dft<15> : DftComp<3, 5> {};
 template <> struct Dft<16> : DftComp<4, 4> {};
+// fixed-kernel-only radices (two-pass 720 = 24 x 30; never picked by the generic planner's search)
+template <> struct Dft<24> : DftComp<8, 3> {};
+template <> struct Dft<30> : DftComp<10, 3> {};
 
 }  // namespace amd_dft

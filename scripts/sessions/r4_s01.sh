@@ -30,3 +30,11 @@ for r in 1 2; do
   TAILN=2 step r4s01_fno_def_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5
   MI_DFT_LIB=$PWD/variants/dftwpf8/_C.so TAILN=2 step r4s01_fno_pf8_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5
 done
+# 720 = (24, 30) two-pass column / row plan vs (8, 9, 10): correctness, then rfft2 / irfft2 ABAB
+MI_DFT_FFT_RADICES="720:24,30" TAILN=2 step r4s01_tests_2430 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_dft_gpu.py
+for r in 1 2; do
+  step r4s01_fft_d2_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_d2_$r.json
+  python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_d2_$r.json'));print('8,9,10 ', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
+  MI_DFT_FFT_RADICES="720:24,30" step r4s01_fft_2430_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_2430_$r.json
+  python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_2430_$r.json'));print('24,30  ', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
+done
