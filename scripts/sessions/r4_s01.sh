@@ -38,3 +38,6 @@ for r in 1 2; do
   MI_DFT_FFT_RADICES="720:24,30" step r4s01_fft_2430_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_2430_$r.json
   python3 -c "import json;d=json.load(open('gpurun_out/r4s01_fft_2430_$r.json'));print('24,30  ', {k:round(d[k]['graph']['median_us'],2) for k in ('amd_rfft2','amd_irfft2')})"
 done
+# phase clocks of the fused FNO tail (fno_c2r_pw) and the rfft2 fixed passes (timing-only builds, variants/bin)
+TAILN=30 step r4s01_fno_stamps 120 ./variants/bin/fno_stamps
+TAILN=30 step r4s01_fft_stamps 120 ./variants/bin/fft_stamps
