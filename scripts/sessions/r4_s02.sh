@@ -1,7 +1,6 @@
 #!/bin/bash
-# Round 4, GPU session 2: the fp32 block without the LayerNorm->split pass (c2r_ln_add_split + linear3_ln) --
-# its GPU tests (library compiled from source on the box by the GPU-tier conftest), the headline bench and a
-# per-kernel table; the FNO block baseline and the batched MFMA mixing path at batch 1 / 8 / 32.
+# Round 4, GPU session 2: A/B runs (LDS-staged FFT twiddles, the dftw load-batch depth, the 720 = 24 x 30 plan)
+# and phase clocks of the FNO tail and the rfft2 passes.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
