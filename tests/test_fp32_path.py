@@ -444,3 +444,37 @@ def test_fp32_block_gate_checks_real_mlp_width():
     assert not S._mlp_gemm_ok(Mlp(320, 1280), split=False)
     assert S._mlp_gemm_ok(Mlp(256, 1280), split=False)
     assert not S._mlp_gemm_ok(Mlp(256, 1056), split=True)  # fc2 K = 1056: 32-tiles ok, fc1 out 1056 % 256 != 0
+
+
+def test_fused_fp32_block_composition_and_export_cpu(monkeypatch):
+    """The fp32 fused block (c2r_ln_add_split -> ln_stats_merge -> linear3_ln -> linear3_stats) forced onto
+    the CPU op implementations: equals the torch model, and exports / re-imports through ONNX (the
+    three-output c2r_ln_add_split node included) -- the engine bench.py times is built this way on the GPU."""
+    from tensorrt_dft_plugins_amd.onnx import exporter as ex
+    from tensorrt_dft_plugins_amd.onnx import proto as P
+    from tensorrt_dft_plugins_amd.onnx.runner import OnnxGraph
+
+    torch.manual_seed(14)
+    cfg = AFNOConfig(img_size=(16, 32), in_chans=3, out_chans=3, embed_dim=256, depth=2, num_blocks=4, patch_size=8)
+    m = AFNONet(cfg, backend="torch").eval()
+    x = torch.randn(1, 3, 16, 32)
+    with torch.no_grad():
+        ref = m(x)
+    calls = []
+    orig = S.afno_block_fused_f32
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(S, "afno_block_fused_f32", spy)
+    monkeypatch.setattr(S, "_ln_fused_ok", lambda blk, t: t.dtype == torch.float32)
+    with torch.no_grad():
+        out = m.set_backend("amd")(x)
+    assert len(calls) == cfg.depth
+    assert rel_l2(out, ref) < 1e-5
+    data = ex.export(m, x)
+    ops_in_graph = {n.op_type for n in P.load_model(data).graph.node if n.domain == "com.amd.dft"}
+    assert {"c2r_ln_add_split", "linear3_ln", "ln_stats_merge", "linear3_stats"} <= ops_in_graph
+    (y,) = OnnxGraph(data, device="cpu").run(x)
+    assert rel_l2(y, ref) < 1e-5
