@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr int RPI = 64 / LPR;  // channel rows per wave instruction
   const int st_ch = lane / LPR, st_px = (lane % LPR) * 8;  // staging role of this lane
   float2 Yv[CO][KS][4];
-  int64_t cur_row = -1;
+  int cur_b = -1, cur_h = -1;  // (b, h) of the spectrum row held in Yv
   // byte offsets (not pointers: a pointer carried around the loop loses its global address
   // space and the stores become flat stores, which every later LDS wait would also drain)
   int64_t yrow[CO];  // &y[b][16 ot + l15][h][4 lq] - y  (clamped to a valid channel)
@@ -201,11 +201,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   using Raw = u32x4;  // 16 bytes = 8 bf16 or 4 fp32 (a native vector: HIP's uint4 struct copies went to scratch)
   constexpr int NR = BF ? 1 : 2;
   Raw xr[NQ][NR];
-  auto load_x = [&](int64_t uu) {
-    const int64_t rr = uu / nch;
-    const int cw = static_cast<int>(uu - rr * nch) * CH + st_px;
-    const int64_t bb = rr / H, hh = rr - bb * H;
-    const char* src = static_cast<const char*>(x) + (((bb * Cin + st_ch) * H + hh) * W + cw) * ES;
+  // Unit u = (b * H + h) * nch + c, kept as (c, h, b) counters advanced once per unit: the
+  // divisions by the runtime nch / H (64-bit: ~150 instructions each with branches) stay out of
+  // the loop
+  struct UPos {
+    int c, h, b;
+  };
+  auto advance = [&](UPos& q) {
+    if (++q.c == nch) {
+      q.c = 0;
+      if (++q.h == H) {
+        q.h = 0;
+        ++q.b;
+      }
+    }
+  };
+  auto load_x = [&](const UPos& q) {
+    const int cw = q.c * CH + st_px;
+    const char* src = static_cast<const char*>(x) +
+                      (((static_cast<int64_t>(q.b) * Cin + st_ch) * H + q.h) * W + cw) * ES;
     // Unconditional loads (clamped address when out of range): pixels >= W only reach outputs
     // that are never stored and channels >= Cin are never staged, so no zeroing is needed --
     // a select on the loaded value here would make the compiler wait for the load right away
@@ -219,9 +233,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   // the spectrum operand of one (b, h) row and its output row offsets
-  auto load_row = [&](int64_t row) {
-    cur_row = row;
-    const int64_t b = row / H, h = row - b * H;
+  auto load_row = [&](const UPos& q) {
+    cur_b = q.b;
+    cur_h = q.h;
+    const int64_t b = q.b, h = q.h;
 #pragma unroll
     for (int ot = 0; ot < CO; ++ot)
 #pragma unroll
@@ -240,9 +255,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // this wave's first x chunk and spectrum row are requested before the table setup below, so the
   // three global round trips overlap instead of following each other (the setup was ~17 % of a
   // wave's time, profiles/fno_phases_r3.txt)
+  UPos cur;
+  {
+    const int64_t row = u0 / nch;  // once per wave
+    cur.c = static_cast<int>(u0 - row * nch);
+    cur.b = static_cast<int>(row / H);
+    cur.h = static_cast<int>(row - static_cast<int64_t>(cur.b) * H);
+  }
   if (u0 < u1) {
-    load_x(u0);
-    load_row(u0 / nch);
+    load_x(cur);
+    load_row(cur);
   }
 
 
@@ -287,9 +309,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   FNO_T(0);
 
   for (int64_t u = u0; u < u1; ++u) {
-    const int64_t row = u / nch;
-    const int c = static_cast<int>(u - row * nch);
-    if (row != cur_row) load_row(row);
+    const int c = cur.c;
+    if (cur.h != cur_h || cur.b != cur_b) load_row(cur);
+    UPos nxt = cur;
+    advance(nxt);
     FNO_T(1);
     const int w0 = c * CH;
     // ---- x chunk (channels x pixels) into this wave's LDS tile
@@ -327,7 +350,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     // prefetch the next unit's x (unconditionally -- the last unit re-loads itself: behind a
     // branch, the waits after the join would be merged conservatively to vmcnt(0) and drain it)
-    load_x(u + 1 < u1 ? u + 1 : u);
+    load_x(u + 1 < u1 ? nxt : cur);
     wave_lds_fence();
     FNO_T(2);
     // ---- MFMA, 4 pixel tiles at a time: conv + spectral into bias-initialised accumulators
@@ -485,6 +508,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
       FNO_T(4);
     }
+    cur = nxt;
   }
 #ifdef FNO_STAMPS
   if (lane == 0) {
