@@ -17,3 +17,4 @@ TAILN=3 step r4s01_bench 400 python -u bench.py
 TAILN=8 step r4s01_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
 TAILN=6 step r4s01_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
 PROF_TAG=_r4s01 timeout -k 10 700 bash scripts/prof_bench.sh > gpurun_out/r4s01_prof.txt 2>&1; echo "prof rc=$?"; head -16 gpurun_out/r4s01_prof.txt
+python3 scripts/trace_window.py gpurun_out/prof_bench_r4s01 > gpurun_out/r4s01_window.txt 2>&1; head -30 gpurun_out/r4s01_window.txt
