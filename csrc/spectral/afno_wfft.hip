@@ -299,6 +299,9 @@ __device__ __forceinline__ float row_sum16(float x) {
 #ifndef AFNO_C2R_SPLIT_OCC
 #define AFNO_C2R_SPLIT_OCC 2
 #endif
+#ifndef AFNO_C2R_JIT
+#define AFNO_C2R_JIT 0  // fp32: addends loaded 3 positions ahead inside the epilogue (A/B; see below)
+#endif
 template <int KM, bool F32, bool SPLIT = false>
 __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(!SPLIT || F32, "split-pair outputs come with the fp32 instantiation");
@@ -412,12 +415,18 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
   const int lo = k1 * C + kCh * g;  // 32-bit lane offset from the workgroup-uniform base
   float xr[XLDS ? 1 : kB][kCh];
   float2 sv[XLDS ? 1 : kB];
+  // register addends: all 15 positions' loads issued before the DFT (latency hidden under it), or
+  // (AFNO_C2R_JIT) only the first JD, the rest JD positions ahead inside the epilogue (fewer live
+  // VGPRs: the split instantiation then fits 3 workgroups per CU without spilling)
+  constexpr bool JIT = AFNO_C2R_JIT && !XLDS;
+  constexpr int JD = JIT ? 3 : kB;
+  auto ld_add = [&](int k2) {
+    ldx4<F32>(xb, lo + kA * k2 * C, xr[k2]);
+    sv[k2] = st[k1 + kA * k2];
+  };
   if constexpr (!XLDS) {
 #pragma unroll
-    for (int k2 = 0; k2 < kB; ++k2) {
-      ldx4<F32>(xb, lo + kA * k2 * C, xr[k2]);
-      sv[k2] = st[k1 + kA * k2];
-    }
+    for (int k2 = 0; k2 < JD; ++k2) ld_add(k2);
   }
   ChanParams cp;
   load_params(a, c0, cp);
@@ -433,6 +442,9 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
   float* const sbase_part = SPLIT ? a.part + (static_cast<int64_t>(o) * kL * a.nslab + slab) * 2 : nullptr;
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
+    if constexpr (JIT) {
+      if (k2 + JD < kB) ld_add(k2 + JD);
+    }
     float xp[kCh], h[kCh];
     if constexpr (XLDS) {
       const int n = k1 + kA * k2;

@@ -35,3 +35,9 @@ done
 # phase clocks of the fused FNO tail (fno_c2r_pw) and the rfft2 fixed passes (timing-only builds, variants/bin)
 TAILN=30 step r4s01_fno_stamps 120 ./variants/bin/fno_stamps
 TAILN=30 step r4s01_fft_stamps 120 ./variants/bin/fft_stamps
+# fp32 FourCastNet step: AFNO C2R (split epilogue) with addends loaded 3 positions ahead at 3 WGs/CU
+# (variants/c2rjit) vs all addends before the DFT at 2 WGs/CU (default), ABAB
+for r in 1 2; do
+  TAILN=1 step r4s02_step_def_$r 300 python -u bench.py --no-fft --extra-steps 0 --steps 10 --warmup 3
+  MI_DFT_LIB=$PWD/variants/c2rjit/_C.so TAILN=1 step r4s02_step_jit_$r 300 python -u bench.py --no-fft --extra-steps 0 --steps 10 --warmup 3
+done
