@@ -899,13 +899,17 @@ at::Tensor c2r_ln_add_meta(const at::Tensor&, int64_t, int64_t, double, const at
 // c2r_ln_add + the residual stream's bf16x3 split-pair rows and per-64-channel LayerNorm partials
 // (mean, M2), all from the one C2R epilogue (afno_wfft.hip SPLIT instantiation): the fp32 block's
 // fc1 then reads the pairs with LN2 folded in (linear3_ln) -- no LayerNorm / split pass.
+// The pairs hold out - mean(x) per token (stats[:, 0], the input's LayerNorm mean): centred, the
+// split keeps 2^-17 of the deviation rather than of |out|, and ln_stats_merge(part, eps, stats)
+// gives fc1 the matching centred mean.
 // Returns (out [..., W, C] fp32, pairs [tokens, 2C] bf16, part [tokens, C/64, 2] fp32).
-std::tuple<at::Tensor, at::Tensor, at::Tensor> split_and_partials(const at::Tensor& y) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor> split_and_partials(const at::Tensor& y, const at::Tensor& stats) {
   const int64_t C = y.size(-1);
   at::Tensor rows = y.reshape({-1, C}).to(at::kFloat);
-  at::Tensor hi = rows.to(at::kBFloat16);
-  at::Tensor lo = (rows - hi.to(at::kFloat)).to(at::kBFloat16);
   const int64_t M = rows.size(0);
+  at::Tensor z = rows - stats.reshape({-1, 2}).select(1, 0).to(at::kFloat).unsqueeze(1);
+  at::Tensor hi = z.to(at::kBFloat16);
+  at::Tensor lo = (z - hi.to(at::kFloat)).to(at::kBFloat16);
   at::Tensor pairs = at::cat({hi.reshape({M, C / 32, 32}), lo.reshape({M, C / 32, 32})}, -1).reshape({M, 2 * C}).contiguous();
   at::Tensor w = rows.reshape({M, C / 64, 64});
   at::Tensor mean = w.mean(2);
@@ -967,7 +971,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::T
     return {checked(out, "c2r_ln_add_split"), pairs, part};
   }
   fallback_note("c2r_ln_add_split", "no fused W-transform for this shape: c2r_ln_add + ATen split / statistics");
-  return split_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_));
+  return split_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_), stats_);
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale,
@@ -975,7 +979,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cpu(const at::Te
                                                                     const at::Tensor& g, const at::Tensor& b,
                                                                     const std::optional<at::Tensor>& pre) {
   check_split_out(X, x, "c2r_ln_add_split");
-  return split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre));
+  return split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre), stats);
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_meta(const at::Tensor&, int64_t, int64_t, double,

@@ -456,28 +456,43 @@ at::Tensor ln_stats_meta(const at::Tensor& x, const std::optional<at::Tensor>&, 
   return at::empty({x.numel() / std::max<int64_t>(x.size(-1), 1), 2}, x.options().dtype(at::kFloat));
 }
 
-// (mean, rstd) per row from [rows, nc, 2] per-64-chunk (mean, M2) partials (linear3_stats)
-at::Tensor ln_stats_merge_cpu(const at::Tensor& part, double eps) {
+// (mean, rstd) per row from [rows, nc, 2] per-64-chunk (mean, M2) partials (linear3_stats);
+// shift [rows, 2] (optional): its column 0 is subtracted from the mean (statistics of an operand
+// centred on that offset, e.g. c2r_ln_add_split's pairs)
+static void check_merge_shift(const at::Tensor& part, const std::optional<at::Tensor>& shift) {
   TORCH_CHECK(part.dim() == 3 && part.size(2) == 2, "amd_dft.ln_stats_merge: part must be [rows, chunks, 2]");
+  if (shift) {
+    TORCH_CHECK(shift->numel() == part.size(0) * 2 && shift->size(-1) == 2 && shift->device() == part.device(),
+                "amd_dft.ln_stats_merge: shift must hold [rows, 2] on the device of part");
+  }
+}
+
+at::Tensor ln_stats_merge_cpu(const at::Tensor& part, double eps, const std::optional<at::Tensor>& shift) {
+  check_merge_shift(part, shift);
   at::Tensor p = part.to(at::kFloat);
   at::Tensor m = p.select(2, 0), q = p.select(2, 1);
   at::Tensor mean = m.mean(1);
   at::Tensor m2 = q.sum(1) + 64.0 * (m - mean.unsqueeze(1)).pow(2).sum(1);
+  if (shift) mean = mean - shift->reshape({-1, 2}).select(1, 0).to(at::kFloat);
   return at::stack({mean, at::rsqrt(m2 / (64.0 * p.size(1)) + eps)}, 1).contiguous();
 }
 
-at::Tensor ln_stats_merge_cuda(const at::Tensor& part_, double eps) {
+at::Tensor ln_stats_merge_cuda(const at::Tensor& part_, double eps, const std::optional<at::Tensor>& shift_) {
   const c10::DeviceGuard guard(part_.device());
-  TORCH_CHECK(part_.dim() == 3 && part_.size(2) == 2 && part_.scalar_type() == at::kFloat,
-              "amd_dft.ln_stats_merge: part must be fp32 [rows, chunks, 2]");
+  check_merge_shift(part_, shift_);
+  TORCH_CHECK(part_.scalar_type() == at::kFloat, "amd_dft.ln_stats_merge: part must be fp32 [rows, chunks, 2]");
   at::Tensor part = part_.contiguous();
+  at::Tensor shift = shift_ ? shift_->to(at::kFloat).contiguous() : at::Tensor();
   at::Tensor st = at::empty({part.size(0), 2}, part.options());
   launch_ln_stats_merge(part.data_ptr<float>(), st.data_ptr<float>(), part.size(0), static_cast<int>(part.size(1)), 64,
-                        static_cast<float>(eps), c10::hip::getCurrentHIPStream(part.device().index()).stream());
+                        static_cast<float>(eps), c10::hip::getCurrentHIPStream(part.device().index()).stream(),
+                        shift.defined() ? shift.data_ptr<float>() : nullptr);
   return checked(st, "ln_stats_merge");
 }
 
-at::Tensor ln_stats_merge_meta(const at::Tensor& part, double) { return at::empty({part.size(0), 2}, part.options()); }
+at::Tensor ln_stats_merge_meta(const at::Tensor& part, double, const std::optional<at::Tensor>&) {
+  return at::empty({part.size(0), 2}, part.options());
+}
 
 at::Tensor afno_spectral_meta(const at::Tensor& xw, const at::Tensor&, const at::Tensor&, const at::Tensor&,
                               const at::Tensor&, double) {
@@ -493,7 +508,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("afno_spectral_shapes() -> int[]", &amd_dft::afno_spectral_shape_list);
   m.def("layer_norm(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("ln_stats(Tensor x, Tensor? pre=None, float eps=1e-6) -> Tensor");
-  m.def("ln_stats_merge(Tensor part, float eps=1e-6) -> Tensor");
+  m.def("ln_stats_merge(Tensor part, float eps=1e-6, Tensor? shift=None) -> Tensor");
   m.def("layer_norm_split(Tensor x, Tensor weight, Tensor bias, float eps, Tensor? pre=None) -> Tensor");
   m.def("fno_mix(Tensor x, Tensor w, int path=0) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");

@@ -82,7 +82,7 @@ struct WArgs {
   const float* pre;      // [C] or nullptr
   const void* spec;      // C2R input [O, KM, C, 2] bf16 / fp32
   void* out;             // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
-  uint16_t* pairs;       // C2R, SPLIT: [O * 180, 2C] bf16 split pairs of out
+  uint16_t* pairs;       // C2R, SPLIT: [O * 180, 2C] bf16 split pairs of out - mean(x) (stats .x)
   float* part;           // C2R, SPLIT: [O * 180, C / 64, 2] (mean, M2) of out per 64-channel slab
   int C, nslab;
   float scale;
@@ -289,7 +289,7 @@ __device__ __forceinline__ float row_sum16(float x) {
 }
 
 // SPLIT (fp32 block, round 4): the epilogue also writes the next GEMM's operand -- the bf16x3 split
-// pairs of y -- and the next LayerNorm's partial statistics of y over this workgroup's 64 channels
+// pairs of y - mean(x), centred per token -- and the next LayerNorm's partial statistics of y over this workgroup's 64 channels
 // (the 16 lanes of one DPP row hold one position's 64 channels).  That removes the separate
 // LayerNorm -> split pass over the residual stream (one full read of it per block); LN2 is then
 // folded into fc1's epilogue (linear3_ln) from per-token stats merged by ln_stats_merge.
@@ -463,10 +463,16 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
     stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
     if constexpr (SPLIT) {
       // workgroup-uniform bases (o's first token) + 32-bit lane offsets: position n = k1 + 12 k2
+      // the pairs hold y - mean(x) (x's LayerNorm mean, already in sv): the split then resolves y's
+      // deviation from a per-token offset to 2^-17 instead of its absolute value, so fc1's folded
+      // mean cancellation keeps fp32-class accuracy when |mean| >> std (ln_stats_merge(shift=) of
+      // the same stats hands fc1 mean(y) - mean(x))
       const int n = k1 + kA * k2;
-      const uint32_t h01 = bfpack(y[0], y[1]), h23 = bfpack(y[2], y[3]);
-      const uint32_t l01 = bfpack(y[0] - __uint_as_float(h01 << 16), y[1] - __uint_as_float(h01 & 0xffff0000u));
-      const uint32_t l23 = bfpack(y[2] - __uint_as_float(h23 << 16), y[3] - __uint_as_float(h23 & 0xffff0000u));
+      const float m0 = sv[k2].x;
+      const float z0 = y[0] - m0, z1 = y[1] - m0, z2 = y[2] - m0, z3 = y[3] - m0;
+      const uint32_t h01 = bfpack(z0, z1), h23 = bfpack(z2, z3);
+      const uint32_t l01 = bfpack(z0 - __uint_as_float(h01 << 16), z1 - __uint_as_float(h01 & 0xffff0000u));
+      const uint32_t l23 = bfpack(z2 - __uint_as_float(h23 << 16), z3 - __uint_as_float(h23 & 0xffff0000u));
       uint16_t* pr = pbase + (n * (2 * C) + (c0 >> 5) * 64 + (c0 & 31));  // k32-interleaved [hi(32) | lo(32)]
       *reinterpret_cast<uint2*>(pr) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(pr + 32) = make_uint2(l01, l23);

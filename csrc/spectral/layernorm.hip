@@ -481,10 +481,13 @@ __global__ void __launch_bounds__(256) split_bf16_kernel(const float* __restrict
 // epilogue leaves for the next block's LayerNorm (csrc/nn/gemm.hip, STATS)
 // 256 rows per workgroup: the block's partials ([256][nc] float2, contiguous) are staged in LDS
 // with coalesced 16-byte loads, then every thread merges its own row (Chan: M2 = sum M2_c +
-// width * sum (mean_c - mean)^2)
+// width * sum (mean_c - mean)^2).  shift (or nullptr): [rows] float2 whose .x is subtracted from the
+// mean -- the statistics of a split-pair operand that was written relative to that offset
+// (c2r_ln_add_split centres its pairs on the input stream's mean, see afno_wfft.hip)
 constexpr int kMergeMaxNc = 64;  // dynamic LDS 2 KB per chunk: <= 128 KB
 __global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __restrict__ part, float2* __restrict__ st,
-                                                             int64_t rows, int nc, float width, float eps) {
+                                                             const float2* __restrict__ shift, int64_t rows, int nc,
+                                                             float width, float eps) {
   extern __shared__ float4 tile[];  // [256 rows][nc] float2
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * 256;
   const int nrow = static_cast<int>(rows - r0 < 256 ? rows - r0 : 256);
@@ -503,10 +506,12 @@ __global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __res
     const float d = q.x - mean;
     m2 += fmaf(width * d, d, q.y);
   }
-  st[r0 + threadIdx.x] = make_float2(mean, rsqrtf(m2 / (width * static_cast<float>(nc)) + eps));
+  const float sh = shift ? shift[r0 + threadIdx.x].x : 0.f;
+  st[r0 + threadIdx.x] = make_float2(mean - sh, rsqrtf(m2 / (width * static_cast<float>(nc)) + eps));
 }
 
-void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream) {
+void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream,
+                           const float* shift) {
   if (rows <= 0) return;
   if (nc <= 0 || nc % 2 || nc > kMergeMaxNc || width <= 0)
     throw std::runtime_error("amd_dft: ln_stats_merge: needs an even chunk count <= 64");
@@ -524,7 +529,8 @@ void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc
     }
   }
   hipLaunchKernelGGL(ln_stats_merge_kernel, grid, dim3(256), lds, static_cast<hipStream_t>(stream),
-                     reinterpret_cast<const float2*>(part), reinterpret_cast<float2*>(stats), rows, nc,
+                     reinterpret_cast<const float2*>(part), reinterpret_cast<float2*>(stats),
+                     reinterpret_cast<const float2*>(shift), rows, nc,
                      static_cast<float>(width), eps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: ln_stats_merge launch: ") + hipGetErrorString(e));

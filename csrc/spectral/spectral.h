@@ -100,7 +100,8 @@ struct LnStatsLaunch {
 };
 void launch_ln_stats(const LnStatsLaunch& p, void* stream);
 // [rows, nc, 2] per-chunk (mean, M2) partials of chunk width `width` -> [rows, 2] (mean, rstd)
-void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream);
+void launch_ln_stats_merge(const float* part, float* stats, int64_t rows, int nc, int width, float eps, void* stream,
+                           const float* shift = nullptr);
 
 // ---- fp32 -> bf16 (hi, lo) split pairs for the bf16x3 GEMM: rows -> [rows, 2 cols] [hi | lo],
 // else planes [2, n]

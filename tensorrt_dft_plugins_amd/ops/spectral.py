@@ -331,10 +331,11 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
                                                  (first block: ln_stats over x)
       X_w   = R2C_W(LN1(x))                      afno_wfft fp32 instantiation, fp32 spectrum
       Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral bf16x3 variant (fp32 staging)
-      x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32, whose epilogue ALSO writes x1's
-                                                 bf16x3 split pairs and LN2's per-64-channel partials
+      x1    = C2R_W(Y_w) + LN1(x) + x            afno_wfft fp32, whose epilogue ALSO writes the
+                                                 bf16x3 split pairs of x1 - mean(x) (centred per
+                                                 token) and LN2's per-64-channel partials
                                                  (c2r_ln_add_split: no LayerNorm / split pass)
-      st2   = (mean, rstd) of x1                 ln_stats_merge (8 B per token)
+      st2   = (mean - mean(x), rstd) of x1       ln_stats_merge(shift=stats) (8 B per token)
       h     = split(GELU(LN2(x1) W1^T + b1))     bf16x3 GEMM on x1's pairs with LN2 folded into the
                                                  epilogue (linear3_ln), erf GELU, split-pair output
       x1    = x1 + h W2^T                        bf16x3 GEMM, fp32 residual epilogue, which also
@@ -359,8 +360,13 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
     x1, x1s, part2 = ops.c2r_ln_add_split(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    # x1s holds x1 - mean(x) per token (centred split): st2's mean is shifted to match.
     # ln_stats_merge takes <= 64 chunks of 64 channels
-    st2 = ops.ln_stats_merge(part2, n2.eps) if C <= 64 * 64 else ops.ln_stats(x1, None, n2.eps)
+    if C <= 64 * 64:
+        st2 = ops.ln_stats_merge(part2, n2.eps, stats)
+    else:
+        st2 = ops.ln_stats(x1, None, n2.eps)
+        st2 = torch.stack((st2[:, 0] - stats.reshape(-1, 2)[:, 0], st2[:, 1]), 1)
     w1s, c1, c2 = _ln_folded_fc3(m.fc1, n2)
     hid = ops.linear3_ln(x1s, w1s, c1, c2, st2, 1)
     w2s = module_cached(m, "fc2_split", (m.fc2.weight,), lambda: split_bf16(m.fc2.weight))

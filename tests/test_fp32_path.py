@@ -121,8 +121,12 @@ def test_c2r_ln_add_split_cpu_semantics():
     y, pairs, part = ops.c2r_ln_add_split(X, 2, W, 0.01, x, st, g, be, pre)
     assert torch.equal(y, ops.c2r_ln_add(X, 2, W, 0.01, x, st, g, be, pre))
     assert pairs.shape == (B * H * W, 2 * C) and part.shape == (B * H * W, C // 64, 2)
-    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C), True))
-    assert torch.allclose(ops.ln_stats_merge(part, 1e-6), _ln_stats_ref(y.reshape(-1, C)), rtol=1e-5, atol=1e-6)
+    # pairs are centred on the input's LayerNorm mean; ln_stats_merge(shift=st) centres the mean the same way
+    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C) - st[:, :1], True))
+    sref = _ln_stats_ref(y.reshape(-1, C))
+    assert torch.allclose(ops.ln_stats_merge(part, 1e-6), sref, rtol=1e-5, atol=1e-6)
+    sref[:, 0] -= st[:, 0]
+    assert torch.allclose(ops.ln_stats_merge(part, 1e-6, st), sref, rtol=1e-5, atol=1e-6)
     with pytest.raises(RuntimeError, match="fp32"):
         ops.c2r_ln_add_split(X.bfloat16(), 2, W, 0.01, x.bfloat16(), st, g, be, pre)
 
@@ -222,10 +226,12 @@ def test_linear3_stats_gpu(device, M, N, K, with_pre):
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,mean_scale", [(1000, 0.5), (777, 10.0), (300, 100.0)])
 def test_linear3_ln_gpu_vs_fp64(device, M, mean_scale):
-    """fc1 of the fp32 block: the LayerNorm folded into the bf16x3 GEMM's epilogue, from the raw
-    stream's split pairs.  Rows with a large common mean (|mean| / std = 10, 100) check the
-    mean cancellation rstd * (x W'^T - mean c1): c1 is summed from the same split pairs the GEMM
-    reads, so the error stays at the split's level instead of growing with |mean| / std."""
+    """fc1 of the fp32 block: the LayerNorm folded into the bf16x3 GEMM's epilogue.  Rows with a
+    large common mean (|mean| / std = 10, 100) check the mean cancellation rstd * (x W'^T - mean c1):
+    split pairs of the raw x resolve x to 2^-17 of |x|, so that error grows with |mean| / std
+    (measured 5.5e-6 at 0.5, 3.9e-5 at 10).  The fused block therefore splits x - m0, centred on a
+    per-token offset m0 (the previous stream's mean, which differs from x's own mean by O(std)):
+    m0 here is the true mean plus 0.5 std of noise, and the error must stay at the split's level."""
     torch.manual_seed(M)
     K, N = 768, 3072
     x = torch.randn(M, K) + mean_scale * torch.randn(M, 1)
@@ -233,13 +239,17 @@ def test_linear3_ln_gpu_vs_fp64(device, M, mean_scale):
     g, be = torch.randn(K) * 0.3 + 1, torch.randn(K) * 0.1
     ws, c1, c2 = _ln_fold_operands(w, b, g, be)
     st = _ln_stats_ref(x)
+    m0 = st[:, :1] + 0.5 * torch.randn(M, 1)
+    sts = torch.stack((st[:, 0] - m0[:, 0], st[:, 1]), 1)
     ref = F.gelu(F.linear(F.layer_norm(x.double(), (K,), g.double(), be.double(), 1e-6), w.double(), b.double()))
     d = lambda t: t.to(device)  # noqa: E731
-    y = ops.linear3_ln(ops.split_bf16(d(x), True), d(ws), d(c1), d(c2), d(st), 1)
+    y = ops.linear3_ln(ops.split_bf16(d(x - m0), True), d(ws), d(c1), d(c2), d(sts), 1)
     assert y.shape == (M, 2 * N) and y.dtype == torch.bfloat16
     err = rel_l2(unsplit_bf16(y.cpu()), ref)
-    print(f"linear3_ln |mean|/std ~ {mean_scale}: rel-L2 vs fp64 = {err:.2e}")
-    assert err < 2e-5 * max(1.0, mean_scale / 10)
+    print(f"linear3_ln |mean|/std ~ {mean_scale} (centred): rel-L2 vs fp64 = {err:.2e}")
+    assert err < 1e-5
+    yr = ops.linear3_ln(ops.split_bf16(d(x), True), d(ws), d(c1), d(c2), d(st), 1)  # uncentred, for the record
+    print(f"linear3_ln |mean|/std ~ {mean_scale} (raw pairs): rel-L2 vs fp64 = {rel_l2(unsplit_bf16(yr.cpu()), ref):.2e}")
 
 
 @pytest.mark.gpu
@@ -260,10 +270,13 @@ def test_c2r_ln_add_split_gpu(device, with_pre):
     assert S.fallback_counts() == {}
     ref = ops.c2r_ln_add(X, 2, W, 1.0 / math.sqrt(H * W), x, st, g, be, pre)
     assert rel_l2(y.cpu(), ref) < 2e-6
-    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C), True))
+    assert torch.equal(pairs, ops.split_bf16(y.reshape(-1, C) - d(st)[:, :1], True))
     stg = ops.ln_stats_merge(part, 1e-6).cpu()
     sref = _ln_stats_ref(y.cpu().reshape(-1, C))
     assert torch.allclose(stg, sref, rtol=2e-5, atol=2e-6), (stg - sref).abs().max()
+    sref[:, 0] -= st[:, 0]
+    sts = ops.ln_stats_merge(part, 1e-6, d(st)).cpu()
+    assert torch.allclose(sts, sref, rtol=2e-5, atol=2e-6), (sts - sref).abs().max()
 
 
 @pytest.mark.gpu
