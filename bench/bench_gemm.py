@@ -1,7 +1,8 @@
 """Hand-written fused-epilogue GEMM vs hipBLASLt (torch) on the FourCastNet MLP shapes,
 interleaved rounds in one process.
 
-Usage: python bench/bench_gemm.py [--rows 518400]
+Usage: python bench/bench_gemm.py [--rows 518400] [--x3]
+(MI_DFT_GEMM_PERSIST=1: the fp32 block's GEMMs on the persistent grid -- run once with each to A/B)
 """
 import argparse
 import json
@@ -54,9 +55,14 @@ def main(argv=None):
                    torch.randn(Hd, C, device=dev) * 0.02, torch.randn(C, Hd, device=dev) * 0.02)
         xs, hs, w1s, w2s = (ops.split_bf16(t) for t in src)
         r32 = torch.randn(M, C, device=dev)
+        st = ops.ln_stats(src[0], None, 1e-6)
+        c1 = torch.randn(Hd, device=dev)
         v = {
             "fc1_gelu x3 (split out)": lambda: ops.linear3(xs, w1s, b1, 1, None, True),
             "fc2 x3 (+fp32 residual)": lambda: ops.linear3(hs, w2s, None, 0, r32, False),
+            # the fp32 block's forms: LayerNorm folded into fc1; fc2 + the next LN's partial statistics
+            "fc1_gelu x3 LN (split out)": lambda: ops.linear3_ln(xs, w1s, c1, b1, st, 1),
+            "fc2 x3 (+residual, stats)": lambda: ops.linear3_stats(hs, w2s, r32, b2),
             "fc1_gelu amd": v["fc1_gelu amd"],
             "fc2 amd": v["fc2 amd"],
         }

@@ -13,13 +13,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r"""
-import sys, torch
+import os, sys, torch
 sys.path.insert(0, %(root)r)
 import tensorrt_dft_plugins_amd as tdp
 tdp.load_plugins()
 ops = torch.ops.amd_dft
 torch.manual_seed(0)
-M = 20000 + 77  # ragged last token tile
+M = 256 * 90 + 77  # ragged last token tile; > 256 tiles at N = 768 (the persistent grid is active)
 C, H = 768, 3072
 x = torch.randn(M, C, device="cuda")
 w1 = torch.randn(H, C, device="cuda") * 0.02
@@ -30,11 +30,21 @@ xs, w1s, w2s = ops.split_bf16(x), ops.split_bf16(w1), ops.split_bf16(w2)
 h = ops.linear3(xs, w1s, b1, 1, None, True)
 y = ops.linear3(h, w2s, None, 0, r.clone(), False)
 y1 = ops.linear3(xs, w1s, b1, 0, None, False)
+# the fp32 block's GEMMs (the persistent variants; staged epilogue only): LN-folded fc1, fc2 +
+# statistics, fc2 -> split pairs
+extra = {}
+if os.environ.get("MI_DFT_GEMM_EPI", "staged") != "direct":
+    st = ops.ln_stats(x, None, 1e-6)
+    c1, c2 = torch.randn(H, device="cuda"), torch.randn(H, device="cuda") * 0.02
+    ys, part = ops.linear3_stats(h, w2s, r.clone(), b1[:C])
+    extra = {"hl": ops.linear3_ln(xs, w1s, c1, c2, st, 1), "ys": ys, "part": part,
+             "yp": ops.linear3(h, w2s, None, 0, r.clone(), True)}
 xb, w1b, w2b = x.bfloat16(), w1.bfloat16(), w2.bfloat16()
 hb = ops.linear(xb, w1b, b1, 1, None)
 yb = ops.linear(hb, w2b, None, 0, r.bfloat16())
 torch.cuda.synchronize()
-torch.save({"h": h.cpu(), "y": y.cpu(), "y1": y1.cpu(), "hb": hb.cpu(), "yb": yb.cpu()}, sys.argv[1])
+out = {"h": h, "y": y, "y1": y1, "hb": hb, "yb": yb, **extra}
+torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[1])
 print("saved", sys.argv[1], flush=True)
 """
 

@@ -93,10 +93,17 @@ __device__ __forceinline__ int region_row(int r) {
 // MODE 1 (patch embedding): the token operand is gathered straight from the image -- K-tile kt
 // is channel kt and the 16-byte chunk c of a token row is patch row py = c (8 pixels), so the
 // un-patchified tensor never exists.
-template <int REG, int MODE, bool SPLIT>
+// OPQ (persistent kernel): the lane offsets are recomputed at every call from an opaque lane id
+// instead of being hoisted (held across the tile loop they spill: a few VALU ops per piece instead).
+// ASM (persistent kernel, the next tile's DMA issued at the epilogue's start): the DMA as inline asm,
+// invisible to the compiler's LDS-DMA hazard tracking -- which would otherwise put a vmcnt(0)
+// before the epilogue's first staging write (different LDS bytes) and drain these very DMAs.  Every
+// read of the regions they fill sits behind an explicit counted wait and a barrier.
+template <int REG, int MODE, bool SPLIT, bool OPQ = false, bool ASM = false>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
                                              int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
+  if constexpr (OPQ) asm volatile("" : "+v"(lane));
   char* dst = stage + REG * kRegion;
   // SPLIT: K-tile kt = logical k [32 kt, 32 kt + 32); its hi and lo halves are adjacent in the
   // k32-interleaved rows (row stride 2K), so the physical 64-element column block is kt * 64
@@ -124,7 +131,13 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
       const uint16_t* base = X + static_cast<int64_t>(t0) * ld + kt * kBK;  // uniform
       g = base + static_cast<uint32_t>(min(tr, M - 1 - t0) * static_cast<int>(ld) + chunk * 8);
     }
-    __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
+    if constexpr (ASM) {
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+          static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void*)(dst + rb * 128))));
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0v) : "memory", "m0");
+    } else {
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
+    }
   }
 }
 
@@ -194,6 +207,12 @@ __device__ __forceinline__ void wait_regions(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 #ifdef AMD_DFT_GEMM_STAMPS
 // slot 0 / 5: s_memrealtime at entry / exit; 1..4: s_memtime at entry, after the prologue,
 // after the main loop, after the epilogue (thread 0 only, vector store)
@@ -242,57 +261,51 @@ __device__ __forceinline__ float row_sum16(float x) {
 // per-channel p.stats_pre, the chunk's (mean, M2 = sum of squared deviations) into
 // p.stats_part[t][chunk] -- the next LayerNorm's statistics without a pass over the output
 // (merged per token by ln_stats_merge, Chan's formula)
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false>
+//
+// PERSIST (MODE 0, staged epilogue): one workgroup per CU walks the tiles vb, vb + grid, ...:
+//   * the epilogue first DMAs the next tile's K-tile 0 into stage 0 (idle after the last K-tile,
+//     which is odd: KT even) and R0 of its K-tile 1 into stage 1, then stages its outputs through
+//     regions R1 / R2 of stage 1 only (4 KB per wave, 16-token quarters);
+//   * vmcnt counts across the epilogue: it issues at least kEpiVm vector memory ops (residual
+//     loads, stores, statistics) behind the prefetched regions, so the waits that let those
+//     regions land allow that many younger ops in flight -- the stores drain while the next
+//     tile's first MFMAs run.  After a ragged tile (predicated stores) the transition waits
+//     for everything instead, and the first tile's prologue waits for all of its DMAs, so the
+//     relaxed waits of phases 0-2 of K-tile 0 are exact in every case;
+//   * the main loop is the one-tile loop unchanged (its register budget is full: a version that
+//     also streamed the next tile in under the last K-tile spilled its DMA addresses).
+// That removes the per-tile workgroup turnaround (launch, prologue DMA latency, epilogue drain)
+// which a grid of one tile per workgroup pays every round.
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
+  static_assert(!PERSIST || MODE == 0, "persistent tiles: token-major operands and outputs only");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
   const uint16_t* __restrict__ W = p.w;
   const uint16_t* __restrict__ X = p.x;
   const int M = p.M, N = p.N, K = p.K;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane0 = threadIdx.x & 63;
+  // PERSIST: the wave index as a scalar, so the DMA's LDS destinations are SGPR arithmetic instead
+  // of hoisted VGPRs (which spilled)
+  const int wave = PERSIST ? __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)) : static_cast<int>(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;  // 2 (features) x 4 (tokens)
   GEMM_STAMP(0, __builtin_amdgcn_s_memrealtime());
   GEMM_STAMP(1, __builtin_amdgcn_s_memtime());
-  // ---- XCD-aware tile order (bijective for any grid size)
+  // ---- XCD-aware tile order (bijective for any tile count).  PERSIST: virtual workgroup
+  // v = blockIdx + k grid (grid % 8 == 0, so v stays on blockIdx's XCD)
   const int tiles_f = N / kBF;
-  const int nwg = gridDim.x, b = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-  const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
-  const int f0 = ft * kBF, t0 = tt * kBT;
+  const int ntl = PERSIST ? p.ntiles : static_cast<int>(gridDim.x);
+  auto tile_of = [&](int v, int& f0_, int& t0_) {
+    const int q8 = ntl / 8, r8 = ntl % 8, xcd = v % 8;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + v / 8;
+    const int tt = lid / tiles_f, ft = lid - tt * tiles_f;  // token panel outer, feature panels inner
+    f0_ = ft * kBF;
+    t0_ = tt * kBT;
+  };
+  int vb = blockIdx.x, f0, t0;
+  tile_of(vb, f0, t0);
   const int KT = SPLIT ? K / 32 : K / kBK;  // SPLIT: 32-deep logical K-tiles (hi | lo = 64 elements)
   AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && (SPLIT ? (K / 32) * 32 : (K / kBK) * kBK) == K && KT > 0,
                     "gemm_bf16_kernel");
-  const int r16 = lane & 15, kq = lane >> 4;
-
-  // ---- output geometry: lane holds features f..f+3 of token t for each (i, j) accumulator tile
-  // (recomputed where used instead of held in registers across the main loop)
-  auto tok = [&](int j) { return t0 + wc * 64 + j * 16 + r16; };
-  auto tokc = [&](int j) { return min(tok(j), M - 1); };  // loads use clamped (valid) rows; stores check t < M
-  auto out_off = [&](int i, int j) -> int64_t {
-    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-    const int t = tokc(j);
-    if constexpr (MODE == 2) {  // un-patchify: feature f = (c, py, px), 4 consecutive px
-      const int hw = p.sh * p.sw;
-      const int bb = t / hw, rem = t - bb * hw;
-      const int ii = rem / p.sw, jj = rem - ii * p.sw;
-      return (static_cast<int64_t>(bb * p.sC + (f >> 6)) * (p.sh * 8) + ii * 8 + ((f >> 3) & 7)) * (p.sw * 8) + jj * 8 +
-             (f & 7);
-    } else {
-      return static_cast<int64_t>(t) * N + f;
-    }
-  };
-  auto res_off = [&](int i, int j) -> int64_t {
-    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-    if constexpr (MODE == 1) {
-      if (p.res_rows > 0) return static_cast<int64_t>(tokc(j) % p.res_rows) * N + f;
-    }
-    return out_off(i, j);
-  };
-  typedef typename std::conditional<OUT != 0, float4, uint2>::type ResT;  // split modes: fp32 residual
-  auto load_res = [&](int i, int j) -> ResT {
-    if constexpr (OUT != 0) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + res_off(i, j));
-    else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + res_off(i, j));
-  };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -304,6 +317,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   //   q = 0: R1(t+1)   q = 1: R2(t+1)   q = 2: R3(t+1)   q = 3: R0(t+2)
   auto tgt = [](int P) { return (P >> 2) + 1 + ((P & 3) == 3 ? 1 : 0); };
   auto issued = [&](int P) { return tgt(P) < KT ? 1 : 0; };
+  // PERSIST: vector memory ops the staged epilogue issues at least (full tiles) after the next
+  // tile's K-tile-0 / R0(1) DMA: per pass one store, the residual row (OUT 2: 2 loads), the statistics
+  constexpr int kNitE = OUT == 0 ? 8 : 16;
+  constexpr int kEpiVm = 2 * kNitE * (1 + (RES ? (OUT == 2 ? 2 : 1) : 0) + (STATS ? 1 : 0));
+  constexpr int kRelaxed = kEpiVm + 4 < 63 ? kEpiVm + 4 : 63;
 
   // MODE 1: per-lane token base offsets of the gathered image rows (regions 1, 2 x 2 pieces)
   int gb[2][2] = {{0, 0}, {0, 0}};
@@ -313,7 +331,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int row = (wave * 2 + i) * 8 + (lane >> 3);
+        const int row = (wave * 2 + i) * 8 + (lane0 >> 3);
         const int tr = r == 0 ? region_row<1>(row) : region_row<2>(row);
         const int t = min(t0 + tr, M - 1);
         const int b = t / hw, rem = t - b * hw;
@@ -322,297 +340,397 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       }
   }
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
-  stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
-  stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane, p, gb);
+  stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+  stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+  stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+  stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
   if (KT > 1) {
-    stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane, p, gb);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
+    stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane0, p, gb);
+    if constexpr (PERSIST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile 0 and R0(1) (see PERSIST)
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
   } else {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   barrier();
   bf16x8 a0[8], a1[8], b0[4], b1[4];
-  read_a<0>(a0, smem, wr, r16, kq);
+  read_a<0>(a0, smem, wr, lane0 & 15, lane0 >> 4);
   if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
-  GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
+  if constexpr (!PERSIST) GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
+
+  for (;;) {  // PERSIST: one pass per tile (otherwise exactly one)
+    // PERSIST: everything lane-derived (DMA offsets, output geometry) is re-derived per tile from
+    // an opaque copy of the lane id -- hoisted out of the tile loop it would stay live through
+    // the whole kernel and spill
+    int lane = lane0;
+    if constexpr (PERSIST) asm volatile("" : "+v"(lane));
+    const int r16 = lane & 15, kq = lane >> 4;
+
+    // ---- output geometry: lane holds features f..f+3 of token t for each (i, j) accumulator tile
+    // (recomputed where used instead of held in registers across the main loop)
+    auto tok = [&](int j) { return t0 + wc * 64 + j * 16 + r16; };
+    auto tokc = [&](int j) { return min(tok(j), M - 1); };  // loads use clamped (valid) rows; stores check t < M
+    auto out_off = [&](int i, int j) -> int64_t {
+      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+      const int t = tokc(j);
+      if constexpr (MODE == 2) {  // un-patchify: feature f = (c, py, px), 4 consecutive px
+        const int hw = p.sh * p.sw;
+        const int bb = t / hw, rem = t - bb * hw;
+        const int ii = rem / p.sw, jj = rem - ii * p.sw;
+        return (static_cast<int64_t>(bb * p.sC + (f >> 6)) * (p.sh * 8) + ii * 8 + ((f >> 3) & 7)) * (p.sw * 8) + jj * 8 +
+               (f & 7);
+      } else {
+        return static_cast<int64_t>(t) * N + f;
+      }
+    };
+    auto res_off = [&](int i, int j) -> int64_t {
+      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+      if constexpr (MODE == 1) {
+        if (p.res_rows > 0) return static_cast<int64_t>(tokc(j) % p.res_rows) * N + f;
+      }
+      return out_off(i, j);
+    };
+    typedef typename std::conditional<OUT != 0, float4, uint2>::type ResT;  // split modes: fp32 residual
+    auto load_res = [&](int i, int j) -> ResT {
+      if constexpr (OUT != 0) return *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + res_off(i, j));
+      else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + res_off(i, j));
+    };
 
 #ifndef GEMM_ABLATE
 #define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads,
 #endif                 // bit 2 = epilogue computes but skips its stores
-  for (int t = 0; t < KT; ++t) {
-    char* cur = smem + (t & 1) * kStage;
-    char* nxt = smem + ((t + 1) & 1) * kStage;
-    const int P = 4 * t;
-    // ---- phase 0: quadrant (mi 0, ni 0)
-    wait_regions(issued(P - 2) + issued(P - 1));
-    auto dma0 = [&] {
-      if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    };
-    if (!GEMM_DMA_MID) dma0();
-    if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 0, SPLIT>(acc, a0, b0, dma0);
-    barrier();
-    // ---- phase 1: (0, 1)
-    wait_regions(issued(P - 1) + issued(P));
-    auto dma1 = [&] {
-      if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    };
-    if (!GEMM_DMA_MID) dma1();
-    if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<0, 1, SPLIT>(acc, a0, b1, dma1);
-    barrier();
-    // ---- phase 2: (1, 1)
-    wait_regions(issued(P) + issued(P + 1));
-    auto dma2 = [&] {
-      if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
-    };
-    if (!GEMM_DMA_MID) dma2();
-    if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 1, SPLIT>(acc, a1, b1, dma2);
-    barrier();
-    // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
-    wait_regions(issued(P + 1) + issued(P + 2));
-    auto dma3 = [&] {
-      if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
-    };
-    if (!GEMM_DMA_MID) dma3();
-    if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mfma_quadrant<1, 0, SPLIT>(acc, a1, b0, dma3);
-    barrier();
-  }
-  if (wr == 0) barrier();  // re-align the two wave groups
-  GEMM_STAMP(3, __builtin_amdgcn_s_memtime());
+    for (int t = 0; t < KT; ++t) {
+      char* cur = smem + (t & 1) * kStage;
+      char* nxt = smem + ((t + 1) & 1) * kStage;
+      const int P = 4 * t;
+      // ---- phase 0: quadrant (mi 0, ni 0)
+      if (PERSIST && t == 0) wait_vm<kRelaxed>();
+      else wait_regions(issued(P - 2) + issued(P - 1));
+      auto dma0 = [&] {
+        if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+      };
+      if (!GEMM_DMA_MID) dma0();
+      if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<0, 0, SPLIT>(acc, a0, b0, dma0);
+      barrier();
+      // ---- phase 1: (0, 1)
+      if (PERSIST && t == 0) wait_vm<kRelaxed>();
+      else wait_regions(issued(P - 1) + issued(P));
+      auto dma1 = [&] {
+        if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+      };
+      if (!GEMM_DMA_MID) dma1();
+      if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<0, 1, SPLIT>(acc, a0, b1, dma1);
+      barrier();
+      // ---- phase 2: (1, 1)
+      if (PERSIST && t == 0) wait_vm<kRelaxed>();
+      else wait_regions(issued(P) + issued(P + 1));
+      auto dma2 = [&] {
+        if (!(GEMM_ABLATE & 1) && issued(P + 2)) stage_region<3, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+      };
+      if (!GEMM_DMA_MID) dma2();
+      if (!(GEMM_ABLATE & 2)) read_a<3>(a1, cur, wr, r16, kq);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<1, 1, SPLIT>(acc, a1, b1, dma2);
+      barrier();
+      // ---- phase 3: (1, 0); fragments A0 of K-tile t+1 are read here
+      wait_regions(issued(P + 1) + issued(P + 2));
+      auto dma3 = [&] {
+        if (!(GEMM_ABLATE & 1) && issued(P + 3)) stage_region<0, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 2, cur, wave, lane, p, gb);
+      };
+      if (!GEMM_DMA_MID) dma3();
+      if (!(GEMM_ABLATE & 2) && t + 1 < KT) read_a<0>(a0, nxt, wr, r16, kq);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_quadrant<1, 0, SPLIT>(acc, a1, b0, dma3);
+      barrier();
+    }
+    if (wr == 0) barrier();  // re-align the two wave groups
+    if constexpr (!PERSIST) GEMM_STAMP(3, __builtin_amdgcn_s_memtime());
 
-  // ---- epilogue: lane holds features f..f+3 of token t for each (i, j) tile.
-  // No load sits behind a per-element branch (hipcc would then wait for each one in turn:
-  // 32 serialised round trips per wave, ~20 us per tile): bias / c1 / LN statistics are loaded
-  // up front, residual rows from clamped (always valid) addresses two i-tiles at a time with
-  // the next pair in flight, and only the stores are predicated on t < M.
-  float4 bias4[8], c14[8];
+    // ---- epilogue: lane holds features f..f+3 of token t for each (i, j) tile.
+    // No load sits behind a per-element branch (hipcc would then wait for each one in turn:
+    // 32 serialised round trips per wave, ~20 us per tile): bias / c1 / LN statistics are loaded
+    // up front, residual rows from clamped (always valid) addresses two i-tiles at a time with
+    // the next pair in flight, and only the stores are predicated on t < M.
+    float4 bias4[8], c14[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-    bias4[i] = BIAS ? *reinterpret_cast<const float4*>(p.bias + f) : make_float4(0.f, 0.f, 0.f, 0.f);
-    c14[i] = LN ? *reinterpret_cast<const float4*>(p.ln_c1 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float2 lst[4];
+    for (int i = 0; i < 8; ++i) {
+      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+      bias4[i] = BIAS ? *reinterpret_cast<const float4*>(p.bias + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+      c14[i] = LN ? *reinterpret_cast<const float4*>(p.ln_c1 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float2 lst[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
-  if constexpr (MODE != 2) {  // token-major outputs (MODE 1 only gathers its B operand differently)
-    if (!p.direct_epi) {
-      // ---- LDS-staged epilogue (token-major outputs).  Writing straight from the MFMA layout
-      // makes every store instruction touch 16 rows with 32-64 B each (partial lines; the
-      // epilogue was 25 % of a bf16x3 fc1 tile and nearly all of it stores: profiles/
-      // gemm_epilogue_r2.txt).  Instead each wave parks act(acc + bias) as fp32 in its own 16 KB
-      // of the (now idle) stage buffers -- 64 tokens x 64 features per half, 16-byte chunks
-      // XOR-swizzled by row -- and reads it back row-contiguous: 16 B per lane, whole 128-byte
-      // lines per store instruction, the residual read the same coalesced way (prefetched
-      // before the half is staged), then the bf16 / fp32 / split-pair conversion.
-      barrier();  // every wave is past its last fragment read of the stage buffers
-      char* reg = smem + wave * (64 * 256);
-      const int tbase = t0 + wc * 64;
-      constexpr int LPR = OUT == 0 ? 8 : 16;    // lanes per token row
-      constexpr int RPI = 64 / LPR;             // rows per pass
-      constexpr int NIT = 64 / RPI;             // passes per half
-      const int c = lane % LPR, rsub = lane / LPR;
-      // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32 (the hi and the lo
-      // lane of a feature group both load it)
-      struct F8 { float4 a, b; };
-      typedef typename std::conditional<OUT == 1, float4, typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
-        RT rr[RES ? NIT : 1];
-        // residual rows are prefetched PD passes ahead of their use: all NIT before the half is
-        // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
-        // for OUT 2 (8 fp32 per pass: the whole half would hold 128 VGPRs beside the accumulators)
-        // -- each of those spilled when the whole half was prefetched
-        constexpr int PD = OUT == 2 ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
-        auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
-          int rt = min(tbase + it * RPI + rsub, M - 1);
-          if constexpr (MODE == 1) {
-            if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
-          }
-          if constexpr (OUT == 2) {
-            const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
-            const float* rp = static_cast<const float*>(p.residual) + o;
-            rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
-          } else {
-            const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
-            if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
-            else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+    for (int j = 0; j < 4; ++j)
+      lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
+    if constexpr (MODE != 2) {  // token-major outputs (MODE 1 only gathers its B operand differently)
+      if (PERSIST || !p.direct_epi) {
+        // ---- LDS-staged epilogue (token-major outputs).  Writing straight from the MFMA layout
+        // makes every store instruction touch 16 rows with 32-64 B each (partial lines; the
+        // epilogue was 25 % of a bf16x3 fc1 tile and nearly all of it stores: profiles/
+        // gemm_epilogue_r2.txt).  Instead each wave parks act(acc + bias) as fp32 in its own 16 KB
+        // of the (now idle) stage buffers -- 64 tokens x 64 features per half, 16-byte chunks
+        // XOR-swizzled by row -- and reads it back row-contiguous: 16 B per lane, whole 128-byte
+        // lines per store instruction, the residual read the same coalesced way (prefetched
+        // before the half is staged), then the bf16 / fp32 / split-pair conversion.
+        // PERSIST: stage 0 and region R0 of stage 1 receive the next tile's K-tile 0 and R0 of its
+        // K-tile 1, so each wave stages 16-token quarters in its 4 KB of regions R1 / R2 of stage 1
+        // (same passes and stores, four staging rounds per half)
+        // The next tile's DMAs are issued after the first staging writes (the compiler drains
+        // every LDS DMA it knows of before the epilogue's first LDS write) and before any
+        // epilogue load (so the compiler's own counted waits for those loads stay exact).
+        barrier();  // every wave is past its last fragment read of the stage buffers
+        int nf0 = 0, nt0 = 0;
+        const bool has_next = PERSIST && vb + static_cast<int>(gridDim.x) < ntl;
+        if constexpr (PERSIST) {
+          if (has_next) tile_of(vb + static_cast<int>(gridDim.x), nf0, nt0);
+        }
+        auto next_dma = [&] {
+          if (has_next) {
+            stage_region<0, MODE, SPLIT, true, true>(W, X, K, nf0, nt0, M, 0, smem, wave, lane, p, gb);
+            stage_region<1, MODE, SPLIT, true, true>(W, X, K, nf0, nt0, M, 0, smem, wave, lane, p, gb);
+            stage_region<2, MODE, SPLIT, true, true>(W, X, K, nf0, nt0, M, 0, smem, wave, lane, p, gb);
+            stage_region<3, MODE, SPLIT, true, true>(W, X, K, nf0, nt0, M, 0, smem, wave, lane, p, gb);
+            stage_region<0, MODE, SPLIT, true, true>(W, X, K, nf0, nt0, M, 1, smem + kStage, wave, lane, p, gb);
           }
         };
-        if constexpr (RES) {
+        constexpr int SUB = PERSIST ? 4 : 1;  // token sub-blocks per half
+        char* reg = PERSIST ? smem + kStage + kRegion + wave * (16 * 256) : smem + wave * (64 * 256);
+        const int tbase = t0 + wc * 64;
+        constexpr int LPR = OUT == 0 ? 8 : 16;    // lanes per token row
+        constexpr int RPI = 64 / LPR;             // rows per pass
+        constexpr int NIT = 64 / RPI;             // passes per half
+        const int c = lane % LPR, rsub = lane / LPR;
+        // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32 (the hi and the lo
+        // lane of a feature group both load it)
+        struct F8 { float4 a, b; };
+        typedef typename std::conditional<OUT == 1, float4, typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
 #pragma unroll
-          for (int it = 0; it < PD; ++it) load_rr(it);
-        }
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int i = 4 * h + ii;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            gelu_f2 v[2];
-            epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], v);
-            const int row = j * 16 + r16, ch = ii * 4 + kq;
-            *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
-          }
-        }
-        float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (STATS) {
-          if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
-        }
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-          if constexpr (RES && PD < NIT) {
-            if (it + PD < NIT) load_rr(it + PD);
-          }
-          const int row = it * RPI + rsub, t = tbase + row;
-          const char* rp = reg + row * 256;
-          if constexpr (OUT == 1) {
-            float4 v = *reinterpret_cast<const float4*>(rp + ((c ^ (row & 15)) << 4));
+        for (int h = 0; h < 2; ++h) {
+          const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
+          RT rr[RES ? NIT : 1];
+          // residual rows are prefetched PD passes ahead of their use: all NIT before the half is
+          // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
+          // for OUT 2 (8 fp32 per pass: the whole half would hold 128 VGPRs beside the accumulators)
+          // -- each of those spilled when the whole half was prefetched
+          constexpr int PD = (OUT == 2 || PERSIST) ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
+          auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
+            int rt = min(tbase + it * RPI + rsub, M - 1);
+            if constexpr (MODE == 1) {
+              if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
+            }
+            if constexpr (OUT == 2) {
+              const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
+              const float* rp = static_cast<const float*>(p.residual) + o;
+              rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
+            } else {
+              const int64_t o = static_cast<int64_t>(rt) * N + fh + (OUT == 1 ? 4 : 8) * c;
+              if constexpr (OUT == 1) rr[it] = *reinterpret_cast<const float4*>(static_cast<const float*>(p.residual) + o);
+              else rr[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p.residual) + o);
+            }
+          };
+          auto prefetch = [&] {
             if constexpr (RES) {
-              v.x += rr[it].x;
-              v.y += rr[it].y;
-              v.z += rr[it].z;
-              v.w += rr[it].w;
-            }
-            if (t < M) *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
-            if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
-              const float w0 = v.x + spre.x, w1 = v.y + spre.y, w2 = v.z + spre.z, w3 = v.w + spre.w;
-              const float mean = row_sum16((w0 + w1) + (w2 + w3)) * (1.f / 64.f);
-              const float d0 = w0 - mean, d1 = w1 - mean, d2 = w2 - mean, d3 = w3 - mean;
-              const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
-              if (c == 0 && t < M)
-                *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
-                    make_float2(mean, m2);
-            }
-          } else {
-            // OUT 0: lane = 8 features (chunks 2c, 2c+1); OUT 2: lane c = (half-chunk ch, part, sub)
-            const int fl = OUT == 0 ? 8 * c : (c >> 3) * 32 + (c & 3) * 8;
-            const float4 u0 = *reinterpret_cast<const float4*>(rp + (((fl >> 2) ^ (row & 15)) << 4));
-            const float4 u1 = *reinterpret_cast<const float4*>(rp + ((((fl >> 2) + 1) ^ (row & 15)) << 4));
-            float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-            if constexpr (OUT == 2 && RES) {
-              const float r8[8] = {rr[it].a.x, rr[it].a.y, rr[it].a.z, rr[it].a.w,
-                                   rr[it].b.x, rr[it].b.y, rr[it].b.z, rr[it].b.w};
 #pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] += r8[k];
+              for (int it = 0; it < PD; ++it) load_rr(it);
             }
-            if constexpr (OUT == 0 && RES) {
-              const uint32_t rw[4] = {rr[it].x, rr[it].y, rr[it].z, rr[it].w};
+          };
+          if (!PERSIST || h > 0) prefetch();
+          float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                v[2 * k] += __uint_as_float(rw[k] << 16);
-                v[2 * k + 1] += __uint_as_float(rw[k] & 0xffff0000u);
+          for (int sh = 0; sh < SUB; ++sh) {
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+              const int i = 4 * h + ii;
+#pragma unroll
+              for (int jj = 0; jj < 4 / SUB; ++jj) {
+                const int j = sh * (4 / SUB) + jj;
+                gelu_f2 v[2];
+                epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], v);
+                const int row = jj * 16 + r16, ch = ii * 4 + kq;  // row & 15 == r16 in either layout
+                *reinterpret_cast<float4*>(reg + row * 256 + ((ch ^ (row & 15)) << 4)) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
               }
             }
-            uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
-            if constexpr (OUT == 2) {  // lanes with (c >> 2) & 1 store the lo part: v - hi, branch-free
-              const bool lo = (c >> 2) & 1;
-              uint32_t* wp = &w.x;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const gelu_f2 hf = {__uint_as_float(wp[k] << 16), __uint_as_float(wp[k] & 0xffff0000u)};
-                const gelu_f2 d = gelu_f2{v[2 * k], v[2 * k + 1]} - hf;
-                const uint32_t lw = pk_bf16(d.x, d.y);
-                wp[k] = lo ? lw : wp[k];
+            if (sh == 0) {
+              if constexpr (PERSIST) {
+                if (h == 0) {
+                  next_dma();
+                  prefetch();
+                }
+              }
+              if constexpr (STATS) {
+                if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
               }
             }
-            if (t < M) {
-              if constexpr (OUT == 0) {
-                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+#pragma unroll
+            for (int it = sh * (NIT / SUB); it < (sh + 1) * (NIT / SUB); ++it) {
+              if constexpr (RES && PD < NIT) {
+                if (it + PD < NIT) load_rr(it + PD);
+              }
+              const int row = it * RPI + rsub, t = tbase + row;
+              const char* rp = reg + (row - sh * (64 / SUB)) * 256;  // same row & 15 (64 / SUB is a multiple of 16)
+              if constexpr (OUT == 1) {
+                float4 v = *reinterpret_cast<const float4*>(rp + ((c ^ (row & 15)) << 4));
+                if constexpr (RES) {
+                  v.x += rr[it].x;
+                  v.y += rr[it].y;
+                  v.z += rr[it].z;
+                  v.w += rr[it].w;
+                }
+                if (t < M) *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
+                if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
+                  const float w0 = v.x + spre.x, w1 = v.y + spre.y, w2 = v.z + spre.z, w3 = v.w + spre.w;
+                  const float mean = row_sum16((w0 + w1) + (w2 + w3)) * (1.f / 64.f);
+                  const float d0 = w0 - mean, d1 = w1 - mean, d2 = w2 - mean, d3 = w3 - mean;
+                  const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+                  if (c == 0 && t < M)
+                    *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
+                        make_float2(mean, m2);
+                }
               } else {
-                const int f = fh + fl;
-                *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
-                                          ((c >> 2) & 1) * 32 + (f & 31)) = w;
+                // OUT 0: lane = 8 features (chunks 2c, 2c+1); OUT 2: lane c = (half-chunk ch, part, sub)
+                const int fl = OUT == 0 ? 8 * c : (c >> 3) * 32 + (c & 3) * 8;
+                const float4 u0 = *reinterpret_cast<const float4*>(rp + (((fl >> 2) ^ (row & 15)) << 4));
+                const float4 u1 = *reinterpret_cast<const float4*>(rp + ((((fl >> 2) + 1) ^ (row & 15)) << 4));
+                float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+                if constexpr (OUT == 2 && RES) {
+                  const float r8[8] = {rr[it].a.x, rr[it].a.y, rr[it].a.z, rr[it].a.w,
+                                       rr[it].b.x, rr[it].b.y, rr[it].b.z, rr[it].b.w};
+#pragma unroll
+                  for (int k = 0; k < 8; ++k) v[k] += r8[k];
+                }
+                if constexpr (OUT == 0 && RES) {
+                  const uint32_t rw[4] = {rr[it].x, rr[it].y, rr[it].z, rr[it].w};
+#pragma unroll
+                  for (int k = 0; k < 4; ++k) {
+                    v[2 * k] += __uint_as_float(rw[k] << 16);
+                    v[2 * k + 1] += __uint_as_float(rw[k] & 0xffff0000u);
+                  }
+                }
+                uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+                if constexpr (OUT == 2) {  // lanes with (c >> 2) & 1 store the lo part: v - hi, branch-free
+                  const bool lo = (c >> 2) & 1;
+                  uint32_t* wp = &w.x;
+#pragma unroll
+                  for (int k = 0; k < 4; ++k) {
+                    const gelu_f2 hf = {__uint_as_float(wp[k] << 16), __uint_as_float(wp[k] & 0xffff0000u)};
+                    const gelu_f2 d = gelu_f2{v[2 * k], v[2 * k + 1]} - hf;
+                    const uint32_t lw = pk_bf16(d.x, d.y);
+                    wp[k] = lo ? lw : wp[k];
+                  }
+                }
+                if (t < M) {
+                  if constexpr (OUT == 0) {
+                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+                  } else {
+                    const int f = fh + fl;
+                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
+                                              ((c >> 2) & 1) * 32 + (f & 31)) = w;
+                  }
+                }
               }
             }
           }
         }
+        if constexpr (PERSIST) {
+          if (!has_next) return;
+          // ---- next tile: its K-tile 0 regions, R0 of its K-tile 1 and this epilogue's ops are in
+          // flight.  Wait for R0 / R1 of K-tile 0' (read next: fragments A0 here, B in phase 0) --
+          // younger: R2, R3, R0(1') (6) and the epilogue's >= kEpiVm ops; after a ragged tile for
+          // all of it -- and resume at phase 0 (relaxed waits in phases 0-2 of K-tile 0)
+          if (t0 + kBT <= M) wait_vm<kRelaxed + 2 < 63 ? kRelaxed + 2 : 63>();
+          else wait_vm<0>();
+          barrier();  // every wave's pieces landed, every wave past its staging reads
+          vb += gridDim.x;
+          f0 = nf0;
+          t0 = nt0;
+          read_a<0>(a0, smem, wr, r16, kq);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (wr == 1) barrier();  // the stagger again
+          continue;
+        }
+        GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
+        GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
+        return;
       }
-      GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
-      GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
-      return;
     }
-  }
-  constexpr bool ERES = RES;
-  ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
-  if constexpr (ERES) {
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rq[0][ii][j] = load_res(ii, j);
-  }
-#pragma unroll
-  for (int ip = 0; ip < 4; ++ip) {  // i-tile pairs (2 ip, 2 ip + 1)
+    constexpr bool ERES = RES;
+    ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
     if constexpr (ERES) {
-      if (ip + 1 < 4) {
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
+      for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) rq[(ip + 1) & 1][ii][j] = load_res(2 * (ip + 1) + ii, j);
-      }
+        for (int j = 0; j < 4; ++j) rq[0][ii][j] = load_res(ii, j);
     }
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      const int i = 2 * ip + ii;
-      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+    for (int ip = 0; ip < 4; ++ip) {  // i-tile pairs (2 ip, 2 ip + 1)
+      if constexpr (ERES) {
+        if (ip + 1 < 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        gelu_f2 vp[2];
-        epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], vp);
-        float v[4] = {vp[0].x, vp[0].y, vp[1].x, vp[1].y};
-        if constexpr (ERES) {
-          const ResT rr = rq[ip & 1][ii][j];
-          if constexpr (OUT != 0) {  // fp32 residual (in place allowed: same lane reads, then writes)
-            v[0] += rr.x;
-            v[1] += rr.y;
-            v[2] += rr.z;
-            v[3] += rr.w;
-          } else {
-            v[0] += __uint_as_float(rr.x << 16);
-            v[1] += __uint_as_float(rr.x & 0xffff0000u);
-            v[2] += __uint_as_float(rr.y << 16);
-            v[3] += __uint_as_float(rr.y & 0xffff0000u);
-          }
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rq[(ip + 1) & 1][ii][j] = load_res(2 * (ip + 1) + ii, j);
         }
-        if (tok(j) < M && !((GEMM_ABLATE & 4) && p.M > 0)) {
-          if constexpr (OUT == 1) {
-            *reinterpret_cast<float4*>(static_cast<float*>(p.y) + out_off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
-          } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
-            const uint2 hw = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
-            const gelu_f2 d0 = gelu_f2{v[0], v[1]} - gelu_f2{__uint_as_float(hw.x << 16), __uint_as_float(hw.x & 0xffff0000u)};
-            const gelu_f2 d1 = gelu_f2{v[2], v[3]} - gelu_f2{__uint_as_float(hw.y << 16), __uint_as_float(hw.y & 0xffff0000u)};
-            uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(tok(j)) * (2 * N) + (f >> 5) * 64 + (f & 31);
-            *reinterpret_cast<uint2*>(yr) = hw;
-            *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(d0.x, d0.y), pk_bf16(d1.x, d1.y));
-          } else {
-            *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + out_off(i, j)) =
-                make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+      }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * ip + ii;
+        const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          gelu_f2 vp[2];
+          epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], vp);
+          float v[4] = {vp[0].x, vp[0].y, vp[1].x, vp[1].y};
+          if constexpr (ERES) {
+            const ResT rr = rq[ip & 1][ii][j];
+            if constexpr (OUT != 0) {  // fp32 residual (in place allowed: same lane reads, then writes)
+              v[0] += rr.x;
+              v[1] += rr.y;
+              v[2] += rr.z;
+              v[3] += rr.w;
+            } else {
+              v[0] += __uint_as_float(rr.x << 16);
+              v[1] += __uint_as_float(rr.x & 0xffff0000u);
+              v[2] += __uint_as_float(rr.y << 16);
+              v[3] += __uint_as_float(rr.y & 0xffff0000u);
+            }
+          }
+          if (tok(j) < M && !((GEMM_ABLATE & 4) && p.M > 0)) {
+            if constexpr (OUT == 1) {
+              *reinterpret_cast<float4*>(static_cast<float*>(p.y) + out_off(i, j)) = make_float4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (OUT == 2) {  // split pair row, k32-interleaved: features f..f+3 in one chunk
+              const uint2 hw = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+              const gelu_f2 d0 = gelu_f2{v[0], v[1]} - gelu_f2{__uint_as_float(hw.x << 16), __uint_as_float(hw.x & 0xffff0000u)};
+              const gelu_f2 d1 = gelu_f2{v[2], v[3]} - gelu_f2{__uint_as_float(hw.y << 16), __uint_as_float(hw.y & 0xffff0000u)};
+              uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(tok(j)) * (2 * N) + (f >> 5) * 64 + (f & 31);
+              *reinterpret_cast<uint2*>(yr) = hw;
+              *reinterpret_cast<uint2*>(yr + 32) = make_uint2(pk_bf16(d0.x, d0.y), pk_bf16(d1.x, d1.y));
+            } else {
+              *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.y) + out_off(i, j)) =
+                  make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            }
           }
         }
       }
     }
-  }
-  GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
-  GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
+    GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
+    GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
+    return;
+  }  // tile loop
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false>
-void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
-  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS>;
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST>
+void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, PERSIST>;
   // the dynamic-LDS limit is a per-device function attribute: set it once per (instance, device)
   static std::atomic<uint64_t> attr_done{0};
   int dev = 0;
@@ -623,6 +741,25 @@ void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
     attr_done.fetch_or(uint64_t(1) << dev, std::memory_order_acq_rel);
   }
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
+}
+
+// CAN_PERSIST: the instance has a persistent variant (the fp32 block's GEMMs); p.ntiles > 0 (set by
+// launch_gemm, MI_DFT_GEMM_PERSIST=1) selects it with grid = workgroups, else one tile per workgroup
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool CAN_PERSIST = false>
+void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if constexpr (CAN_PERSIST) {
+    if (p.ntiles > 0) {
+      launch_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, true>(p, st, grid);
+      return;
+    }
+  }
+  if (p.ntiles > 0) {  // no persistent variant of this instance: one workgroup per tile
+    GemmLaunch q = p;
+    q.ntiles = 0;
+    launch_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, false>(q, st, dim3(static_cast<uint32_t>(p.ntiles)));
+    return;
+  }
+  launch_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, false>(p, st, grid);
 }
 
 // bf16 path: every (act, bias, residual, LN) combination of the plain GEMM
@@ -643,13 +780,13 @@ template <int ACT, bool BIAS>
 void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   if (p.ln_stats) {  // fc1 of the fp32 block: LayerNorm folded in (raw residual-stream pairs), split-pair output
     if (p.out != 2 || p.residual) throw std::runtime_error("amd_dft: gemm: a split LayerNorm fold writes split pairs, no residual");
-    launch_one<ACT, BIAS, false, true, 0, true, 2>(p, st, grid);
+    launch_one<ACT, BIAS, false, true, 0, true, 2, false, true>(p, st, grid);
     return;
   }
   if (p.out == 2) {
     if (p.residual) {  // last fp32 block: x + h W2^T straight to the head GEMM's split-pair operand
       if constexpr (ACT == 0 && !BIAS) {
-        launch_one<0, false, true, false, 0, true, 2>(p, st, grid);
+        launch_one<0, false, true, false, 0, true, 2, false, true>(p, st, grid);
       } else {
         throw std::runtime_error("amd_dft: gemm: a split-pair output takes a residual only without activation and bias");
       }
@@ -659,7 +796,7 @@ void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   } else if (p.residual && p.stats_part) {  // fc2 of the fp32 block: + next LayerNorm's partial statistics
     if constexpr (ACT == 0 && !BIAS) {
       if (p.direct_epi) throw std::runtime_error("amd_dft: gemm: statistics need the LDS-staged epilogue");
-      launch_one<ACT, BIAS, true, false, 0, true, 1, true>(p, st, grid);
+      launch_one<ACT, BIAS, true, false, 0, true, 1, true, true>(p, st, grid);
     } else {
       throw std::runtime_error("amd_dft: gemm: output statistics only without activation and bias");
     }
@@ -692,6 +829,29 @@ static int gemm_direct_epi() {
   return v;
 }
 
+// MI_DFT_GEMM_PERSIST=1: the fp32 block's GEMMs on a persistent grid (gemm_bf16_kernel PERSIST; A/B)
+static int gemm_persist() {
+  static const int v = [] {
+    const char* e = std::getenv("MI_DFT_GEMM_PERSIST");
+    return (e && std::string(e) == "1") ? 1 : 0;
+  }();
+  return v;
+}
+
+// persistent grid: one workgroup per CU (kLds = 128 KB), a multiple of 8 so that a workgroup's
+// virtual indices stay on its XCD
+static int persist_grid() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev] = cus / 8 * 8 > 0 ? cus / 8 * 8 : 8;
+  }
+  return cache[dev];
+}
+
 void launch_gemm(const GemmLaunch& p_, void* stream) {
   if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
   if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
@@ -701,7 +861,14 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   GemmLaunch p = p_;
   p.direct_epi = gemm_direct_epi();
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
-  const dim3 grid(static_cast<uint32_t>(nwg));
+  dim3 grid(static_cast<uint32_t>(nwg));
+  p.ntiles = 0;
+  // persistent variant: token-major split GEMMs with an even K-tile count (the next tile's K-tile
+  // 0 lands in stage 0) and more tiles than workgroups
+  if (gemm_persist() && p.split && p.gC == 0 && p.sC == 0 && (p.K / 32) % 2 == 0 && nwg > persist_grid()) {
+    p.ntiles = static_cast<int>(nwg);
+    grid = dim3(static_cast<uint32_t>(persist_grid()));
+  }
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool bias = p.bias != nullptr;
   if (p.gC > 0 || p.sC > 0) {  // patch-embedding gather / un-patchify scatter (no activation, no LN)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, GPU session 2: A/B runs (LDS-staged FFT twiddles, the dftw load-batch depth, the 720 = 24 x 30 plan)
+# Round 4, GPU session 2: the FNO mixing paths at batch 1 / 8 / 32, the FNO block; A/B runs (LDS-staged FFT twiddles, the dftw load-batch depth, the 720 = 24 x 30 plan)
 # and phase clocks of the FNO tail and the rfft2 passes.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -11,6 +11,8 @@ step() {
   echo "== $tag rc=$rc"; grep -v amdgpu.ids "gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
   if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
 }
+TAILN=8 step r4s02_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
+TAILN=6 step r4s02_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
 # rfft2 / irfft2 720x1440: LDS-staged twiddles (variants/twlds = -DAMD_DFT_TW_LDS=1) vs the L1-table prefetch, ABAB
 for r in 1 2; do
   step r4s01_fft_def_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_def_$r.json

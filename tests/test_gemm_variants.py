@@ -29,6 +29,17 @@ def _run(tmp_path, name, env_extra):
 
 
 @pytest.mark.gpu
+def test_gemm_persistent_matches_default(device, tmp_path):
+    """MI_DFT_GEMM_PERSIST=1: the fp32 block's GEMMs on a persistent grid (next tile's first K-tile
+    streamed in under the epilogue, counted waits across it) -- same MFMA order and epilogue
+    arithmetic, so every output must be bit-identical, the ragged last token tile included."""
+    base = _run(tmp_path, "default", {"MI_DFT_GEMM_PERSIST": "0"})
+    other = _run(tmp_path, "persist", {"MI_DFT_GEMM_PERSIST": "1"})
+    for k in base:
+        assert torch.equal(base[k], other[k]), (k, (base[k].float() - other[k].float()).abs().max().item())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("variant", [{"MI_DFT_GEMM_EPI": "direct"}], ids=["direct-epilogue"])
 def test_gemm_variant_matches_default(device, tmp_path, variant):
     from tensorrt_dft_plugins_amd.ops.spectral import unsplit_bf16
@@ -40,3 +51,4 @@ def test_gemm_variant_matches_default(device, tmp_path, variant):
     assert rel_l2(unsplit_bf16(other["h"]), unsplit_bf16(base["h"])) < 1e-6
     for k in ("y", "y1"):
         assert rel_l2(other[k], base[k]) < 1e-6, k
+    # (the fp32 block's GEMMs always use the staged epilogue: hl / ys / part / yp are not compared)
