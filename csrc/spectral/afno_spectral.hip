@@ -4,7 +4,11 @@
 // vectorizer on, both kernels of this file used to return slightly wrong values (bf16x3 rel-L2 ~6e-3
 // instead of 6.2e-6), differently from launch to launch, only when two or more workgroups shared a
 // CU; rounds 2-3 built the file with the vectorizer off.
-// Root cause (round 3): a gfx950 packed-FP32 fault, not a race in this source.  With the vectorizer
+// Root cause (round 3): a packed-FP32 misbehaviour observed on this toolchain and pool (ROCm 7.2.0,
+// AMD clang 22 / LLVM from /opt/rocm/lib/llvm, gfx950 MI355X boxes), not a race in this source.
+// Whether it is a hardware erratum or a hazard the compiler's hazard recognizer should pad (wait
+// states between MFMA co-runners and op_sel'd packed-FP32 reads) is not established -- only that
+// the form below fails there and the avoided form does not.  With the vectorizer
 // on, the pass-1 twiddle multiply was issued as `v_pk_mul_f32 vD, vA, vB op_sel:[0,1]` -- the high
 // half of the twiddle pair broadcast through src1's op_sel.  Packed-FP32 ops that select src1's high
 // half through op_sel (v_pk_mul_f32 and v_pk_fma_f32 alike) return wrong products while another wave
