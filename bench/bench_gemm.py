@@ -39,6 +39,9 @@ def main(argv=None):
     b2 = (torch.randn(C, device=dev) * 0.02)
     b1h, b2h = b1.to(torch.bfloat16), b2.to(torch.bfloat16)
     ops = torch.ops.amd_dft
+    st_b = ops.ln_stats(x.float(), None, 1e-6)
+    c1_b = torch.randn(Hd, device=dev)
+    rb = torch.randn(M, C, device=dev).to(torch.bfloat16)
     v = {
         "fc1_gelu amd": lambda: ops.linear(x, w1, b1, 1, None),
         "fc1_gelu hipblaslt": lambda: torch._addmm_activation(b1h, x, w1.t(), use_gelu=True),
@@ -46,6 +49,9 @@ def main(argv=None):
         "fc1 hipblaslt": lambda: F.linear(x, w1, b1h),
         "fc2 amd": lambda: ops.linear(h, w2, b2, 0, None),
         "fc2 hipblaslt": lambda: F.linear(h, w2, b2h),
+        # the bf16 block's forms (persistent variants under MI_DFT_GEMM_PERSIST=1)
+        "fc1_gelu amd LN": lambda: ops.linear_ln(x, w1, c1_b, b1, st_b, 1),
+        "fc2 amd (+res)": lambda: ops.linear(h, w2, b2, 0, rb),
     }
     if a.x3:
         # full fp32 operands (non-zero lo halves, as the model's activations and weights have)
@@ -65,6 +71,8 @@ def main(argv=None):
             "fc2 x3 (+residual, stats)": lambda: ops.linear3_stats(hs, w2s, r32, b2),
             "fc1_gelu amd": v["fc1_gelu amd"],
             "fc2 amd": v["fc2 amd"],
+            "fc1_gelu amd LN": v["fc1_gelu amd LN"],
+            "fc2 amd (+res)": v["fc2 amd (+res)"],
         }
     res = {k: [] for k in v}
     for _ in range(a.rounds):

@@ -38,7 +38,10 @@ if os.environ.get("MI_DFT_GEMM_EPI", "staged") != "direct":
     c1, c2 = torch.randn(H, device="cuda"), torch.randn(H, device="cuda") * 0.02
     ys, part = ops.linear3_stats(h, w2s, r.clone(), b1[:C])
     extra = {"hl": ops.linear3_ln(xs, w1s, c1, c2, st, 1), "ys": ys, "part": part,
-             "yp": ops.linear3(h, w2s, None, 0, r.clone(), True)}
+             "yp": ops.linear3(h, w2s, None, 0, r.clone(), True),
+             # the bf16 block's forms: LN-folded fc1 + GELU, fc2 + bias + residual
+             "hbl": ops.linear_ln(x.bfloat16(), w1.bfloat16(), c1, b1, st, 1),
+             "ybr": ops.linear(torch.randn(M, H, device="cuda").bfloat16(), w2.bfloat16(), b1[:C], 0, r.bfloat16())}
 xb, w1b, w2b = x.bfloat16(), w1.bfloat16(), w2.bfloat16()
 hb = ops.linear(xb, w1b, b1, 1, None)
 yb = ops.linear(hb, w2b, None, 0, r.bfloat16())

@@ -763,10 +763,11 @@ void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 }
 
 // bf16 path: every (act, bias, residual, LN) combination of the plain GEMM
+// (the bf16 block's forms -- LN-folded fc1, fc2 + residual -- have persistent variants)
 template <int ACT, bool BIAS, bool RES>
 void launch_ln(const GemmLaunch& p, hipStream_t st, dim3 grid) {
-  if (p.ln_stats) launch_one<ACT, BIAS, RES, true, 0, false, 0>(p, st, grid);
-  else launch_one<ACT, BIAS, RES, false, 0, false, 0>(p, st, grid);
+  if (p.ln_stats) launch_one<ACT, BIAS, RES, true, 0, false, 0, false, !RES>(p, st, grid);
+  else launch_one<ACT, BIAS, RES, false, 0, false, 0, false, RES>(p, st, grid);
 }
 
 template <int ACT, bool BIAS>
@@ -829,7 +830,7 @@ static int gemm_direct_epi() {
   return v;
 }
 
-// MI_DFT_GEMM_PERSIST=1: the fp32 block's GEMMs on a persistent grid (gemm_bf16_kernel PERSIST; A/B)
+// MI_DFT_GEMM_PERSIST=1: the FourCastNet block GEMMs on a persistent grid (gemm_bf16_kernel PERSIST; A/B)
 static int gemm_persist() {
   static const int v = [] {
     const char* e = std::getenv("MI_DFT_GEMM_PERSIST");
@@ -863,9 +864,10 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
   dim3 grid(static_cast<uint32_t>(nwg));
   p.ntiles = 0;
-  // persistent variant: token-major split GEMMs with an even K-tile count (the next tile's K-tile
-  // 0 lands in stage 0) and more tiles than workgroups
-  if (gemm_persist() && p.split && p.gC == 0 && p.sC == 0 && (p.K / 32) % 2 == 0 && nwg > persist_grid()) {
+  // persistent variant: token-major GEMMs with an even K-tile count (the next tile's K-tile 0 lands
+  // in stage 0) and more tiles than workgroups; instances without one fall back to a full grid
+  if (gemm_persist() && !p.direct_epi && p.gC == 0 && p.sC == 0 && (p.split ? p.K / 32 : p.K / kBK) % 2 == 0 &&
+      nwg > persist_grid()) {
     p.ntiles = static_cast<int>(nwg);
     grid = dim3(static_cast<uint32_t>(persist_grid()));
   }
