@@ -269,9 +269,9 @@ __device__ __forceinline__ float row_sum16(float x) {
 //   * vmcnt counts across the epilogue: it issues at least kEpiVm vector memory ops (residual
 //     loads, stores, statistics) behind the prefetched regions, so the waits that let those
 //     regions land allow that many younger ops in flight -- the stores drain while the next
-//     tile's first MFMAs run.  After a ragged tile (predicated stores) the transition waits
-//     for everything instead, and the first tile's prologue waits for all of its DMAs, so the
-//     relaxed waits of phases 0-2 of K-tile 0 are exact in every case;
+//     tile's first MFMAs run (the epilogue's stores are unconditional, ragged tiles included);
+//     the first tile's prologue waits for all of its DMAs, so the relaxed waits of phases 0-2 of
+//     K-tile 0 are exact in every case;
 //   * the main loop is the one-tile loop unchanged (its register budget is full: a version that
 //     also streamed the next tile in under the last K-tile spilled its DMA addresses).
 // That removes the per-tile workgroup turnaround (launch, prologue DMA latency, epilogue drain)
@@ -573,7 +573,13 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               if constexpr (RES && PD < NIT) {
                 if (it + PD < NIT) load_rr(it + PD);
               }
-              const int row = it * RPI + rsub, t = tbase + row;
+              // Stores are unconditional: a token row t >= M (ragged last panel) was computed from
+              // the clamped operand / residual / statistics rows of M - 1, so its values equal row
+              // M - 1's bit for bit and it is stored there (a benign duplicate).  Predicated stores
+              // would sit behind exec branches, and the compiler's vmcnt bookkeeping then assumes
+              // they may not have issued: its waits for the residual prefetch came out as
+              // vmcnt(4), i.e. waiting for the stores of two passes back to complete.
+              const int row = it * RPI + rsub, t = min(tbase + row, M - 1);
               const char* rp = reg + (row - sh * (64 / SUB)) * 256;  // same row & 15 (64 / SUB is a multiple of 16)
               if constexpr (OUT == 1) {
                 float4 v = *reinterpret_cast<const float4*>(rp + ((c ^ (row & 15)) << 4));
@@ -583,13 +589,13 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                   v.z += rr[it].z;
                   v.w += rr[it].w;
                 }
-                if (t < M) *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
+                *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
                 if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
                   const float w0 = v.x + spre.x, w1 = v.y + spre.y, w2 = v.z + spre.z, w3 = v.w + spre.w;
                   const float mean = row_sum16((w0 + w1) + (w2 + w3)) * (1.f / 64.f);
                   const float d0 = w0 - mean, d1 = w1 - mean, d2 = w2 - mean, d3 = w3 - mean;
                   const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
-                  if (c == 0 && t < M)
+                  if (c == 0)
                     *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
                         make_float2(mean, m2);
                 }
@@ -625,14 +631,12 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                     wp[k] = lo ? lw : wp[k];
                   }
                 }
-                if (t < M) {
-                  if constexpr (OUT == 0) {
-                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
-                  } else {
-                    const int f = fh + fl;
-                    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
-                                              ((c >> 2) & 1) * 32 + (f & 31)) = w;
-                  }
+                if constexpr (OUT == 0) {
+                  *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+                } else {
+                  const int f = fh + fl;
+                  *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
+                                            ((c >> 2) & 1) * 32 + (f & 31)) = w;
                 }
               }
             }
@@ -642,10 +646,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           if (!has_next) return;
           // ---- next tile: its K-tile 0 regions, R0 of its K-tile 1 and this epilogue's ops are in
           // flight.  Wait for R0 / R1 of K-tile 0' (read next: fragments A0 here, B in phase 0) --
-          // younger: R2, R3, R0(1') (6) and the epilogue's >= kEpiVm ops; after a ragged tile for
-          // all of it -- and resume at phase 0 (relaxed waits in phases 0-2 of K-tile 0)
-          if (t0 + kBT <= M) wait_vm<kRelaxed + 2 < 63 ? kRelaxed + 2 : 63>();
-          else wait_vm<0>();
+          // younger: R2, R3, R0(1') (6) and the epilogue's >= kEpiVm ops -- and resume at phase 0
+          // (relaxed waits in phases 0-2 of K-tile 0)
+          wait_vm<kRelaxed + 2 < 63 ? kRelaxed + 2 : 63>();  // (ragged tiles store every pass too)
           barrier();  // every wave's pieces landed, every wave past its staging reads
           vb += gridDim.x;
           f0 = nf0;
