@@ -99,6 +99,9 @@ __device__ __forceinline__ int region_row(int r) {
 // invisible to the compiler's LDS-DMA hazard tracking -- which would otherwise put a vmcnt(0)
 // before the epilogue's first staging write (different LDS bytes) and drain these very DMAs.  Every
 // read of the regions they fill sits behind an explicit counted wait and a barrier.
+#ifndef GEMM_DMA_DWORD
+#define GEMM_DMA_DWORD 0  // timing-only ablation: bit R = region R's DMA moves 4 instead of 16 bytes per lane
+#endif                    // (same instructions and vmcnt counts, a quarter of the bytes: power vs operand traffic)
 template <int REG, int MODE, bool SPLIT, bool OPQ = false, bool ASM = false>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
@@ -136,7 +139,10 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
           static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void*)(dst + rb * 128))));
       asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0v) : "memory", "m0");
     } else {
-      __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
+      if constexpr ((GEMM_DMA_DWORD >> REG) & 1)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 4, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(g), (lds_void*)(dst + rb * 128), 16, 0, 0);
     }
   }
 }
@@ -541,8 +547,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               for (int it = 0; it < PD; ++it) load_rr(it);
             }
           };
-          if (!PERSIST || h > 0) prefetch();
           float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
+          if constexpr (STATS && !PERSIST) {  // ahead of the residual prefetch: the wait for its first row covers it
+            if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
+          }
+          if (!PERSIST || h > 0) prefetch();
 #pragma unroll
           for (int sh = 0; sh < SUB; ++sh) {
 #pragma unroll
@@ -564,7 +573,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                   prefetch();
                 }
               }
-              if constexpr (STATS) {
+              if constexpr (STATS && PERSIST) {
                 if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
               }
             }
