@@ -22,6 +22,13 @@
     }                                                                                \
   } while (0)
 
+__global__ void fill_stats(float* st, int64_t rows) {  // (mean, rstd) = (0.1, 1)
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < rows; i += 256LL * gridDim.x) {
+    st[2 * i] = 0.1f;
+    st[2 * i + 1] = 1.f;
+  }
+}
+
 __global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
   for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += 256LL * gridDim.x) {
     uint32_t h = static_cast<uint32_t>(i) * 2654435761u ^ seed;
@@ -127,6 +134,20 @@ int main() {
   f2.out = 1;
   f2.stamps = stamps;
   run("fc2 x3 (+fp32 residual)", f2, stamps);
+  // the fp32 block's forms: LayerNorm folded into fc1 (ln_stats / c1), fc2 + the next LN's partial statistics
+  float *lnst = nullptr, *c1 = nullptr, *part = nullptr;
+  CK(hipMalloc(&lnst, sizeof(float) * 2 * static_cast<size_t>(M)));
+  CK(hipMalloc(&c1, sizeof(float) * Hd));
+  CK(hipMalloc(&part, sizeof(float) * 2 * static_cast<size_t>(M) * (C / 64)));
+  hipLaunchKernelGGL(fill_stats, dim3(1024), dim3(256), 0, 0, lnst, static_cast<int64_t>(M));
+  CK(hipMemset(c1, 0, sizeof(float) * Hd));
+  GemmLaunch f1l = f1;
+  f1l.ln_stats = lnst;
+  f1l.ln_c1 = c1;
+  run("fc1 x3 + LN fold + GELU (split out)", f1l, stamps);
+  GemmLaunch f2s = f2;
+  f2s.stats_part = part;
+  run("fc2 x3 (+fp32 residual, LN partials)", f2s, stamps);
   // bf16 operands (the bf16 model's MLP): x rows [M, K], hidden [M, 4C] bf16, bf16 residual
   GemmLaunch g1;
   g1.x = x;

@@ -11,6 +11,8 @@ step() {
   echo "== $tag rc=$rc"; grep -v amdgpu.ids "gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
   if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
 }
+# GEMM phase clocks (prologue / main loop / epilogue per workgroup) incl. the LN-fold fc1 and the statistics fc2
+TAILN=60 step r4s02_gemm_stamps 200 ./variants/bin/gemm_stamps
 TAILN=8 step r4s02_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
 TAILN=6 step r4s02_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
 # rfft2 / irfft2 720x1440: LDS-staged twiddles (variants/twlds = -DAMD_DFT_TW_LDS=1) vs the L1-table prefetch, ABAB
