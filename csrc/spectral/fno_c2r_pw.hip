@@ -268,30 +268,55 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 
 
+  // ---- tables: every load issued before the first is consumed -- loop-carried loads waited one
+  // memory latency per iteration (the setup was a third of a wave's cycles, profiles/fno_r3_fused_mix.txt);
+  // addresses clamped so nothing sits behind a branch, out-of-range entries masked after the wait
   const int nrot = nch * 16 * KS;
-  for (int t = threadIdx.x; t < nrot; t += 256) rots[t] = rot[t];
-  for (int t = threadIdx.x; t < KS * PT * NG * 64; t += 256) {
+  constexpr int NRT = kFnoRotMax / 256;                // rotation entries per thread, upper bound
+  constexpr int NGT = (KS * PT * NG * 64 + 255) / 256;  // G-table fragments per thread
+  float2 rv[NRT];
+  bf16x8 gv[NGT];
+#pragma unroll
+  for (int q = 0; q < NRT; ++q) rv[q] = rot[min(static_cast<int>(threadIdx.x) + 256 * q, nrot - 1)];
+#pragma unroll
+  for (int q = 0; q < NGT; ++q) {
+    const int t = min(static_cast<int>(threadIdx.x) + 256 * q, KS * PT * NG * 64 - 1);
     const int ln = t & 63, r = t >> 6;
     const int hl = r % NG, f = r / NG;  // f = ks * PT + pt
-    (&g0s[0][0][0][0])[t] = g0[(f * 2 + hl) * 64 + ln];
+    gv[q] = g0[(f * 2 + hl) * 64 + ln];
   }
   // conv B operand: Wc^T[i][o], lane holds i = 8lq + j of channel 16ot + l15
-  bf16x8 Wh[CO], Wl[CO];
-  float bo[CO];
+  float wcv[CO][8], bo[CO];
 #pragma unroll
   for (int ot = 0; ot < CO; ++ot) {
-    const int o = 16 * ot + l15;
+    const int o = min(16 * ot + l15, Cout - 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wcv[ot][j] = wc[o * Cin + min(8 * lq + j, Cin - 1)];
+    bo[ot] = bias != nullptr ? bias[o] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < NRT; ++q) {
+    const int t = static_cast<int>(threadIdx.x) + 256 * q;
+    if (t < nrot) rots[t] = rv[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NGT; ++q) {
+    const int t = static_cast<int>(threadIdx.x) + 256 * q;
+    if (t < KS * PT * NG * 64) (&g0s[0][0][0][0])[t] = gv[q];
+  }
+  bf16x8 Wh[CO], Wl[CO];
+#pragma unroll
+  for (int ot = 0; ot < CO; ++ot) {
+    const bool ok = 16 * ot + l15 < Cout;
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = 8 * lq + 2 * j;
-      const float v0 = (o < Cout && i < Cin) ? wc[o * Cin + i] : 0.f;
-      const float v1 = (o < Cout && i + 1 < Cin) ? wc[o * Cin + i + 1] : 0.f;
-      split_pk(v0, v1, hi[j], lo[j]);
+      split_pk(ok && i < Cin ? wcv[ot][2 * j] : 0.f, ok && i + 1 < Cin ? wcv[ot][2 * j + 1] : 0.f, hi[j], lo[j]);
     }
     Wh[ot] = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
     Wl[ot] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-    bo[ot] = (bias != nullptr && o < Cout) ? bias[o] : 0.f;
+    if (!ok) bo[ot] = 0.f;
   }
   // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not); rows < Cin
   // are rewritten by every chunk before they are read

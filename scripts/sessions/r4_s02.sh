@@ -5,16 +5,23 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+ROOT=$PWD
 step() {
   local tag=$1 t=$2; shift 2
-  timeout -k 10 "$t" "$@" > "gpurun_out/$tag.log" 2>&1; local rc=$?
-  echo "== $tag rc=$rc"; grep -v amdgpu.ids "gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
+  timeout -k 10 "$t" "$@" > "$ROOT/gpurun_out/$tag.log" 2>&1; local rc=$?
+  echo "== $tag rc=$rc"; grep -v amdgpu.ids "$ROOT/gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
   if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
 }
 # GEMM phase clocks (prologue / main loop / epilogue per workgroup) incl. the LN-fold fc1 and the statistics fc2
 TAILN=60 step r4s02_gemm_stamps 200 ./variants/bin/gemm_stamps
+TAILN=20 step r4s02_afno_stamps 200 ./variants/bin/afno_stamps
 TAILN=8 step r4s02_fnomix 400 python -u bench/bench_fno_mix.py --rounds 3
 TAILN=6 step r4s02_fno_b1 300 python -u bench/bench_fno.py --amd-only --rounds 6
+# FNO block, this round (batched table setup, unit counters) vs the round-3 state (variants/r3), ABAB
+for r in 1 2; do
+  TAILN=2 step r4s02_fno_new_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5
+  (cd variants/r3 && TAILN=2 step r4s02_fno_old_$r 200 python -u bench/bench_fno.py --amd-only --rounds 5) || exit 1
+done
 # rfft2 / irfft2 720x1440: LDS-staged twiddles (variants/twlds = -DAMD_DFT_TW_LDS=1) vs the L1-table prefetch, ABAB
 for r in 1 2; do
   step r4s01_fft_def_$r 200 python -u bench/bench_fft.py --rounds 8 --json gpurun_out/r4s01_fft_def_$r.json
