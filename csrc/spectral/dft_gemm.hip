@@ -107,8 +107,18 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
   Raw buf[PF][kNKS][NR];
 #pragma unroll
   for (int j = 0; j < PF; ++j) load(min(wv + NW * j, nblk - 1), buf[j]);
+  // the phase table: every entry's load issued before the first store (clamped, unconditional) --
+  // a copy loop waits one L2 round trip per iteration (up to 4 for a 1440-wide row) behind the batch
   const int nph = nblk * 16 * G;
-  for (int t = threadIdx.x; t < nph; t += 64 * NW) phs[t] = ph[t];
+  constexpr int NPH = (kDftwPhMax + 64 * NW - 1) / (64 * NW);
+  float2 phv[NPH];
+#pragma unroll
+  for (int q = 0; q < NPH; ++q) phv[q] = ph[min(static_cast<int>(threadIdx.x) + 64 * NW * q, nph - 1)];
+#pragma unroll
+  for (int q = 0; q < NPH; ++q) {
+    const int t = static_cast<int>(threadIdx.x) + 64 * NW * q;
+    if (t < nph) phs[t] = phv[q];
+  }
   __syncthreads();
   for (int s0 = wv; s0 < nblk; s0 += NW * PF) {
     if (s0 != wv) {

@@ -493,7 +493,18 @@ __global__ void __launch_bounds__(256) ln_stats_merge_kernel(const float2* __res
   const int nrow = static_cast<int>(rows - r0 < 256 ? rows - r0 : 256);
   const int n4 = nrow * nc / 2;  // nc is even (checked on the host)
   const float4* src = reinterpret_cast<const float4*>(part + r0 * nc);
-  for (int i = threadIdx.x; i < n4; i += 256) tile[i] = src[i];
+  // 8 loads in flight per thread before the first store (clamped, unconditional): the plain copy
+  // loop waited one memory round trip per iteration (6 for 12 chunks)
+  for (int b = 0; b < n4; b += 256 * 8) {
+    float4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = src[min(b + 256 * q + static_cast<int>(threadIdx.x), n4 - 1)];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = b + 256 * q + static_cast<int>(threadIdx.x);
+      if (i < n4) tile[i] = v[q];
+    }
+  }
   __syncthreads();
   if (static_cast<int>(threadIdx.x) >= nrow) return;
   const float2* pp = reinterpret_cast<const float2*>(tile) + threadIdx.x * nc;
