@@ -147,6 +147,7 @@ int main() {
   run("fc1 x3 + LN fold + GELU (split out)", f1l, stamps);
   GemmLaunch f2s = f2;
   f2s.stats_part = part;
+  f2s.stats_pre = c1;  // zeros (the op layer passes zeros when there is no per-channel pre)
   run("fc2 x3 (+fp32 residual, LN partials)", f2s, stamps);
   // bf16 operands (the bf16 model's MLP): x rows [M, K], hidden [M, 4C] bf16, bf16 residual
   GemmLaunch g1;

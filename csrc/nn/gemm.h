@@ -28,7 +28,7 @@ struct GemmLaunch {
   int sC = 0, sh = 0, sw = 0;
   int direct_epi = 0;        // gemm.hip MODE 0: 1 = store straight from the MFMA layout (A/B only)
   float* stats_part = nullptr;       // split mode, fp32 + residual output: [M, N/64, 2] (mean, M2) per 64-feature chunk
-  const float* stats_pre = nullptr;  // [N] added to the output before the statistics (or nullptr)
+  const float* stats_pre = nullptr;  // [N] added to the output before the statistics (required with stats_part)
   int ntiles = 0;            // set by launch_gemm: > 0 = persistent grid (gemm.hip PERSIST), tiles in turn
 #ifdef AMD_DFT_GEMM_STAMPS
   long long* stamps = nullptr;  // diagnostic build only (bench/gemm_stamps.hip): per-block phase clocks

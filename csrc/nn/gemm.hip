@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           };
           float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
           if constexpr (STATS && !PERSIST) {  // ahead of the residual prefetch: the wait for its first row covers it
-            if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
+            spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);  // required (host: zeros if none)
           }
           if (!PERSIST || h > 0) prefetch();
 #pragma unroll
@@ -574,7 +574,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                 }
               }
               if constexpr (STATS && PERSIST) {
-                if (p.stats_pre) spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
+                spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);
               }
             }
 #pragma unroll
@@ -599,7 +599,12 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                   v.w += rr[it].w;
                 }
                 *reinterpret_cast<float4*>(static_cast<float*>(p.y) + static_cast<int64_t>(t) * N + fh + 4 * c) = v;
-                if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
+                if constexpr (STATS && !PERSIST) {
+                  // v + pre back into the staging slot; the statistics are taken per row after the
+                  // half's passes (one lane per token row: no cross-lane reductions)
+                  *reinterpret_cast<float4*>(const_cast<char*>(rp) + ((c ^ (row & 15)) << 4)) =
+                      make_float4(v.x + spre.x, v.y + spre.y, v.z + spre.z, v.w + spre.w);
+                } else if constexpr (STATS) {  // the 16 lanes of this token row hold its 64 features fh .. fh + 63
                   const float w0 = v.x + spre.x, w1 = v.y + spre.y, w2 = v.z + spre.z, w3 = v.w + spre.w;
                   const float mean = row_sum16((w0 + w1) + (w2 + w3)) * (1.f / 64.f);
                   const float d0 = w0 - mean, d1 = w1 - mean, d2 = w2 - mean, d3 = w3 - mean;
@@ -649,6 +654,25 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                 }
               }
             }
+          }
+          if constexpr (STATS && !PERSIST) {
+            // lane l: token row l of this half, its 64 features (output + pre) from the staging slots
+            // written above -- two sweeps (mean, then M2 about it) instead of two 16-lane DPP
+            // reductions per pass (~45 VALU per pass: 9.6k cycles per tile, profiles/phases_r4.txt)
+            const char* rl = reg + lane * 256;
+            f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ch = 0; ch < 16; ++ch) sv += *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4));
+            const float mean = ((sv[0] + sv[1]) + (sv[2] + sv[3])) * (1.f / 64.f);
+            f32x4 qv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ch = 0; ch < 16; ++ch) {
+              const f32x4 d = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4)) - mean;
+              qv += d * d;
+            }
+            const int t = min(tbase + lane, M - 1);  // rows >= M: bit-identical copies of row M - 1
+            *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
+                make_float2(mean, (qv[0] + qv[1]) + (qv[2] + qv[3]));
           }
         }
         if constexpr (PERSIST) {
@@ -807,6 +831,7 @@ void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
     }
     launch_one<ACT, BIAS, false, false, 0, true, 2>(p, st, grid);
   } else if (p.residual && p.stats_part) {  // fc2 of the fp32 block: + next LayerNorm's partial statistics
+    if (!p.stats_pre) throw std::runtime_error("amd_dft: gemm: statistics need stats_pre (zeros when there is none)");
     if constexpr (ACT == 0 && !BIAS) {
       if (p.direct_epi) throw std::runtime_error("amd_dft: gemm: statistics need the LDS-staged epilogue");
       launch_one<ACT, BIAS, true, false, 0, true, 1, true, true>(p, st, grid);

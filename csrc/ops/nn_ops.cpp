@@ -459,10 +459,14 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_cuda(const at::Tensor& xs_, con
   TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_stats: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0");
   TORCH_CHECK(residual.numel() == M * N, "amd_dft.linear3_stats: residual must have the output's shape");
   at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous(), r = residual.to(at::kFloat).contiguous();
+  // the kernel always reads pre (zeros when absent): an optional load behind a branch made the compiler
+  // wait for it -- and for every store before it -- right where it was issued
   at::Tensor pre;
   if (pre_.has_value() && pre_->defined()) {
     pre = pre_->to(at::kFloat).contiguous();
     TORCH_CHECK(pre.numel() == N, "amd_dft.linear3_stats: pre must have N entries");
+  } else {
+    pre = at::zeros({N}, xs.options().dtype(at::kFloat));
   }
   std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
   os.back() = N;
@@ -479,7 +483,7 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_cuda(const at::Tensor& xs_, con
   p.split = 1;
   p.out = 1;
   p.stats_part = part.data_ptr<float>();
-  p.stats_pre = pre.defined() ? pre.data_ptr<float>() : nullptr;
+  p.stats_pre = pre.data_ptr<float>();
   if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
   return {y, part};
 }
