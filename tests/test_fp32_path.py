@@ -208,8 +208,9 @@ def test_linear3_gpu_vs_fp32(device, M, N, K, act, bias, res, split_out):
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,with_pre", [(777, 768, 3072, True), (300, 256, 64, False), (1, 512, 128, True)])
 def test_linear3_stats_gpu(device, M, N, K, with_pre):
-    """The fc2 epilogue's LayerNorm partials (DPP row reductions over 16 lanes) merged by
-    ln_stats_merge match an fp64 LayerNorm-statistics reference of the output + pre."""
+    """The fc2 epilogue's LayerNorm partials (one lane per token row sweeping its 64 staged values;
+    ragged M: rows past M are clamped copies of row M - 1) merged by ln_stats_merge match an fp64
+    LayerNorm-statistics reference of the output + pre."""
     torch.manual_seed(M + N + K)
     x, w, r = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(M, N) * 3 + 1
     pre = torch.randn(N) * 0.5 if with_pre else None
