@@ -125,10 +125,22 @@ __device__ __forceinline__ void st_r(void* p, int32_t off, float v) {
   if constexpr (BF) static_cast<uint16_t*>(p)[off] = static_cast<uint16_t>(f_to_bf(v));
   else static_cast<float*>(p)[off] = v;
 }
+// AMD_DFT_FFT_NT_STORE=1 (A/B build): complex stores non-temporal -- written through to memory / the
+// Infinity Cache instead of left dirty in the XCD's L2, which a kernel boundary then writes back
+#ifndef AMD_DFT_FFT_NT_STORE
+#define AMD_DFT_FFT_NT_STORE 0
+#endif
 template <bool BF>
 __device__ __forceinline__ void st_c(void* p, int32_t off, float2 v) {
-  if constexpr (BF) *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(p) + off) = f_to_bf(v.x) | (f_to_bf(v.y) << 16);
-  else *reinterpret_cast<float2*>(static_cast<float*>(p) + off) = v;
+  if constexpr (BF) {
+    *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(p) + off) = f_to_bf(v.x) | (f_to_bf(v.y) << 16);
+  } else if constexpr (AMD_DFT_FFT_NT_STORE) {
+    float* q = static_cast<float*>(p) + off;
+    __builtin_nontemporal_store(v.x, q);
+    __builtin_nontemporal_store(v.y, q + 1);
+  } else {
+    *reinterpret_cast<float2*>(static_cast<float*>(p) + off) = v;
+  }
 }
 template <bool BF>
 __device__ __forceinline__ void st_c2(void* p, int32_t off, float2 a, float2 b) {
