@@ -280,8 +280,10 @@ __device__ __forceinline__ float row_sum16(float x) {
 //     K-tile 0 are exact in every case;
 //   * the main loop is the one-tile loop unchanged (its register budget is full: a version that
 //     also streamed the next tile in under the last K-tile spilled its DMA addresses).
-// That removes the per-tile workgroup turnaround (launch, prologue DMA latency, epilogue drain)
-// which a grid of one tile per workgroup pays every round.
+// It removes the per-tile workgroup turnaround (launch, prologue DMA latency, epilogue drain) of a
+// grid of one tile per workgroup -- and measured 4-12 % SLOWER (profiles/gemm_persistent_r4.txt: the
+// GEMMs run power-limited, the turnaround gaps were the cheap part), so it stays opt-in
+// (MI_DFT_GEMM_PERSIST=1, bit-exact: tests/test_gemm_variants.py).
 template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   static_assert(!PERSIST || MODE == 0, "persistent tiles: token-major operands and outputs only");
