@@ -11,9 +11,9 @@ step() {
   echo "== $tag rc=$rc"; grep -v amdgpu.ids "$ROOT/gpurun_out/$tag.log" | grep -v "warning: failed to meet" | tail -${TAILN:-12}
   if [ $rc -ne 0 ]; then echo "stopping: $tag failed ($rc)"; exit $rc; fi
 }
-TAILN=14 step r4s05_gemm_stamps 200 ./variants/bin/gemm_stamps
-TAILN=1 step r4s05_bench 400 python -u bench.py --no-fft --extra-steps 0 --steps 10 --warmup 3
-TAILN=6 step r4s05_gpu_tier 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
+
+
+TAILN=6 step r4s05_gpu_tier 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
 # rfft2 / irfft2: non-temporal complex stores (variants/ntstore, -DAMD_DFT_FFT_NT_STORE=1) vs default, ABAB, then a kernel
 # trace of the graph replays (the gap between the row and the column kernel of one call)
 for r in 1 2; do

@@ -30,13 +30,18 @@ def _run(tmp_path, name, env_extra):
 
 @pytest.mark.gpu
 def test_gemm_persistent_matches_default(device, tmp_path):
-    """MI_DFT_GEMM_PERSIST=1: the fp32 block's GEMMs on a persistent grid (next tile's first K-tile
-    streamed in under the epilogue, counted waits across it) -- same MFMA order and epilogue
-    arithmetic, so every output must be bit-identical, the ragged last token tile included."""
+    """MI_DFT_GEMM_PERSIST=1: the FourCastNet block GEMMs on a persistent grid (next tile's first
+    K-tile streamed in under the epilogue, counted waits across it) -- same MFMA order and epilogue
+    arithmetic, so every output must be bit-identical, the ragged last token tile included; the LN
+    partial statistics ('part') are summed in another order there (16-lane DPP sums instead of the
+    default's per-row sweeps) and agree to fp32 rounding."""
     base = _run(tmp_path, "default", {"MI_DFT_GEMM_PERSIST": "0"})
     other = _run(tmp_path, "persist", {"MI_DFT_GEMM_PERSIST": "1"})
     for k in base:
-        assert torch.equal(base[k], other[k]), (k, (base[k].float() - other[k].float()).abs().max().item())
+        if k == "part":
+            assert torch.allclose(base[k], other[k], rtol=1e-5, atol=1e-5), (base[k] - other[k]).abs().max()
+        else:
+            assert torch.equal(base[k], other[k]), (k, (base[k].float() - other[k].float()).abs().max().item())
 
 
 @pytest.mark.gpu
