@@ -327,8 +327,8 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   auto issued = [&](int P) { return tgt(P) < KT ? 1 : 0; };
   // PERSIST: vector memory ops the staged epilogue issues at least (full tiles) after the next
   // tile's K-tile-0 / R0(1) DMA: per pass one store, the residual row (OUT 2: 2 loads), the statistics
-  constexpr int kNitE = OUT == 0 ? 8 : 16;
-  constexpr int kEpiVm = 2 * kNitE * (1 + (RES ? (OUT == 2 ? 2 : 1) : 0) + (STATS ? 1 : 0));
+  constexpr int kNitE = OUT == 1 ? 16 : 8;  // passes per half
+  constexpr int kEpiVm = 2 * kNitE * ((OUT == 2 ? 2 : 1) + (RES ? (OUT == 2 ? 2 : 1) : 0) + (STATS ? 1 : 0));
   constexpr int kRelaxed = kEpiVm + 4 < 63 ? kEpiVm + 4 : 63;
 
   // MODE 1: per-lane token base offsets of the gathered image rows (regions 1, 2 x 2 pieces)
@@ -511,12 +511,13 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         constexpr int SUB = PERSIST ? 4 : 1;  // token sub-blocks per half
         char* reg = PERSIST ? smem + kStage + kRegion + wave * (16 * 256) : smem + wave * (64 * 256);
         const int tbase = t0 + wc * 64;
-        constexpr int LPR = OUT == 0 ? 8 : 16;    // lanes per token row
+        // OUT 0 / 2: a lane owns 8 consecutive features (OUT 2: writes their hi AND lo halves --
+        // 16 B each into the k32-interleaved pair row), OUT 1: 4
+        constexpr int LPR = OUT == 1 ? 16 : 8;    // lanes per token row
         constexpr int RPI = 64 / LPR;             // rows per pass
         constexpr int NIT = 64 / RPI;             // passes per half
         const int c = lane % LPR, rsub = lane / LPR;
-        // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32 (the hi and the lo
-        // lane of a feature group both load it)
+        // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32
         struct F8 { float4 a, b; };
         typedef typename std::conditional<OUT == 1, float4, typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
 #pragma unroll
@@ -534,7 +535,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
             }
             if constexpr (OUT == 2) {
-              const int64_t o = static_cast<int64_t>(rt) * N + fh + (c >> 3) * 32 + (c & 3) * 8;
+              const int64_t o = static_cast<int64_t>(rt) * N + fh + 8 * c;
               const float* rp = static_cast<const float*>(p.residual) + o;
               rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
             } else {
@@ -616,8 +617,8 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                         make_float2(mean, m2);
                 }
               } else {
-                // OUT 0: lane = 8 features (chunks 2c, 2c+1); OUT 2: lane c = (half-chunk ch, part, sub)
-                const int fl = OUT == 0 ? 8 * c : (c >> 3) * 32 + (c & 3) * 8;
+                // lane = 8 features fl .. fl + 7 (staging chunks 2c, 2c + 1)
+                const int fl = 8 * c;
                 const float4 u0 = *reinterpret_cast<const float4*>(rp + (((fl >> 2) ^ (row & 15)) << 4));
                 const float4 u1 = *reinterpret_cast<const float4*>(rp + ((((fl >> 2) + 1) ^ (row & 15)) << 4));
                 float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -636,23 +637,22 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                   }
                 }
                 uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
-                if constexpr (OUT == 2) {  // lanes with (c >> 2) & 1 store the lo part: v - hi, branch-free
-                  const bool lo = (c >> 2) & 1;
-                  uint32_t* wp = &w.x;
+                if constexpr (OUT == 0) {
+                  *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+                } else {  // split pair: hi = bf16(v), lo = bf16(v - hi), both stored by this lane
+                  uint4 lw;
+                  const uint32_t* wp = &w.x;
+                  uint32_t* lp = &lw.x;
 #pragma unroll
                   for (int k = 0; k < 4; ++k) {
                     const gelu_f2 hf = {__uint_as_float(wp[k] << 16), __uint_as_float(wp[k] & 0xffff0000u)};
                     const gelu_f2 d = gelu_f2{v[2 * k], v[2 * k + 1]} - hf;
-                    const uint32_t lw = pk_bf16(d.x, d.y);
-                    wp[k] = lo ? lw : wp[k];
+                    lp[k] = pk_bf16(d.x, d.y);
                   }
-                }
-                if constexpr (OUT == 0) {
-                  *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
-                } else {
                   const int f = fh + fl;
-                  *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 +
-                                            ((c >> 2) & 1) * 32 + (f & 31)) = w;
+                  uint16_t* yr = static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * (2 * N) + (f >> 5) * 64 + (f & 31);
+                  *reinterpret_cast<uint4*>(yr) = w;
+                  *reinterpret_cast<uint4*>(yr + 32) = lw;
                 }
               }
             }
