@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 4, GPU session 5: the fc2 statistics epilogue rewrite (phase clocks, headline step) and the full GPU tier.
+# Round 4, GPU sessions 5-6: the fc2 statistics / split-pair epilogue rewrites (phase clocks, headline step), the full GPU
+# tier, and the non-temporal FFT store A/B.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
@@ -13,6 +14,8 @@ step() {
 }
 
 
+TAILN=30 step r4s06_gemm_stamps 200 ./variants/bin/gemm_stamps
+TAILN=1 step r4s06_bench 400 python -u bench.py --no-fft --extra-steps 0 --steps 10 --warmup 3
 TAILN=6 step r4s05_gpu_tier 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
 # rfft2 / irfft2: non-temporal complex stores (variants/ntstore, -DAMD_DFT_FFT_NT_STORE=1) vs default, ABAB, then a kernel
 # trace of the graph replays (the gap between the row and the column kernel of one call)
