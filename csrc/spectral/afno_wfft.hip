@@ -433,6 +433,9 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
   __builtin_amdgcn_sched_barrier(0);
   Dft<kB>::run(u);
   __builtin_amdgcn_sched_barrier(0);
+  // SPLIT: the staging buffer takes the outputs for the per-position statistics below -- every
+  // wave past its pass-1 reads first (the k1 >= 12 wave has exited: barriers count live waves)
+  if constexpr (SPLIT) __syncthreads();
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
   const int64_t obase = xbase;
   void* ob = F32 ? static_cast<void*>(static_cast<float*>(a.out) + obase)
@@ -476,14 +479,41 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
       uint16_t* pr = pbase + (n * (2 * C) + (c0 >> 5) * 64 + (c0 & 31));  // k32-interleaved [hi(32) | lo(32)]
       *reinterpret_cast<uint2*>(pr) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(pr + 32) = make_uint2(l01, l23);
-      const float mean = row_sum16((y[0] + y[1]) + (y[2] + y[3])) * (1.f / 64.f);
-      const float d0 = y[0] - mean, d1 = y[1] - mean, d2 = y[2] - mean, d3 = y[3] - mean;
-      const float m2 = row_sum16((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
-      if (g == 0) *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) = make_float2(mean, m2);
+      *reinterpret_cast<float4*>(lds + n * kPitch + kPPL * g) = make_float4(y[0], y[1], y[2], y[3]);
     }
     // one output position at a time: interleaving the positions' epilogues (the scheduler's
     // choice) keeps several positions' temporaries live and spills the fp32 instantiations
     if constexpr (F32) __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (SPLIT) {
+    // LN2 partials of this slab: one thread per output position sweeps its 64 staged channels
+    // (mean, then M2 about it) -- two 16-lane DPP reductions per position and lane cost ~10x the VALU
+    __syncthreads();
+    const int n = threadIdx.x;
+    if (n < kL) {
+      const float4* row = reinterpret_cast<const float4*>(lds + n * kPitch);
+      float4 sv4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < kG; ++j) {
+        const float4 q = row[j];
+        sv4.x += q.x;
+        sv4.y += q.y;
+        sv4.z += q.z;
+        sv4.w += q.w;
+      }
+      const float mean = ((sv4.x + sv4.y) + (sv4.z + sv4.w)) * (1.f / 64.f);
+      float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < kG; ++j) {
+        const float4 q = row[j];
+        const float d0 = q.x - mean, d1 = q.y - mean, d2 = q.z - mean, d3 = q.w - mean;
+        m4.x = fmaf(d0, d0, m4.x);
+        m4.y = fmaf(d1, d1, m4.y);
+        m4.z = fmaf(d2, d2, m4.z);
+        m4.w = fmaf(d3, d3, m4.w);
+      }
+      *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) = make_float2(mean, (m4.x + m4.y) + (m4.z + m4.w));
+    }
   }
 }
 
