@@ -279,18 +279,10 @@ constexpr int c2r_load_kind(int n1) {
   return all ? 1 : (any ? 2 : 0);
 }
 
-// sum over a 16-lane DPP row (every lane gets the total): quad swaps, then the 8- and 16-lane mirrors
-__device__ __forceinline__ float row_sum16(float x) {
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xf, 0xf, false));  // row_half_mirror
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));  // row_mirror
-  return x;
-}
 
 // SPLIT (fp32 block, round 4): the epilogue also writes the next GEMM's operand -- the bf16x3 split
 // pairs of y - mean(x), centred per token -- and the next LayerNorm's partial statistics of y over this workgroup's 64 channels
-// (the 16 lanes of one DPP row hold one position's 64 channels).  That removes the separate
+// (y staged in the LDS buffer, one thread per position sweeping its 64 channels).  That removes the separate
 // LayerNorm -> split pass over the residual stream (one full read of it per block); LN2 is then
 // folded into fc1's epilogue (linear3_ln) from per-token stats merged by ln_stats_merge.
 // Register budget (workgroups per CU): the fp32 instantiation holds the 15-point DFT (60 VGPRs) and
