@@ -12,12 +12,14 @@
 //    v_mfma_f32_16x16x32_bf16 (8 x 4 accumulator tiles = 128 fp32 per lane);
 //  * ping-pong schedule: the two wave groups (wr = 0 / 1, one wave of each per SIMD) run one
 //    barrier apart, so on every SIMD one wave issues its LDS fragment reads and DMA while the
-//    other one runs its 16-MFMA cluster;
-//  * each 64-deep K-tile is 4 phases (one 64x32 quadrant of the wave's output per phase, snake
-//    order so fragments are reused) and 4 LDS regions of 16 KB; every phase DMAs one region of
-//    the K-tile 1..2 ahead with global_load_lds_dwordx4 (no VGPR round trip), so 3 regions
-//    (6 DMA instructions per wave) stay in flight across the barriers: counted vmcnt, never 0
-//    in the main loop, raw s_barrier (no __syncthreads, which would drain the DMA);
+//    other one runs its MFMA cluster;
+//  * each 64-deep K-tile is 2 phases (GEMM_HALF, default: one 64x64 half of the wave's output
+//    per phase, 32 bf16 / 48 bf16x3 MFMAs) over 4 LDS regions of 16 KB, filled with
+//    global_load_lds_dwordx4 (no VGPR round trip) one K-tile ahead: counted vmcnt, never 0 in the
+//    main loop, raw s_barrier (no __syncthreads, which would drain the DMA).  The 4-phase
+//    schedule (64x32 quadrants, 16 / 24 MFMAs per phase) remains for the persistent variant and
+//    the gathered patch embedding (MODE 1); the 2-phase one measured 6-9 % faster on the bf16 and
+//    3-5 % on the bf16x3 MLP GEMMs (profiles/gemm_half_r4.txt);
 //  * region = 128 rows x 128 B with the 16-byte chunk XOR-swizzled by (row & 7): the DMA writes
 //    lane-linear, so the swizzle is applied to the SOURCE address; fragment reads are
 //    bank-conflict free for the ds_read_b128 lane groups;
@@ -102,18 +104,20 @@ __device__ __forceinline__ int region_row(int r) {
 #ifndef GEMM_DMA_DWORD
 #define GEMM_DMA_DWORD 0  // timing-only ablation: bit R = region R's DMA moves 4 instead of 16 bytes per lane
 #endif                    // (same instructions and vmcnt counts, a quarter of the bytes: power vs operand traffic)
-template <int REG, int MODE, bool SPLIT, bool OPQ = false, bool ASM = false>
+// NPC: pieces (8-row instructions) per calling wave; wave = the caller's slot (rows 8 NPC wave ..)
+template <int REG, int MODE, bool SPLIT, bool OPQ = false, bool ASM = false, int NPC = 2>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
                                              int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
+  static_assert(NPC == 2 || MODE != 1, "gathered token rows: 2 pieces per wave");
   if constexpr (OPQ) asm volatile("" : "+v"(lane));
   char* dst = stage + REG * kRegion;
   // SPLIT: K-tile kt = logical k [32 kt, 32 kt + 32); its hi and lo halves are adjacent in the
   // k32-interleaved rows (row stride 2K), so the physical 64-element column block is kt * 64
   const int64_t ld = SPLIT ? 2 * K : K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rb = (wave * 2 + i) * 8;
+  for (int i = 0; i < NPC; ++i) {
+    const int rb = (wave * NPC + i) * 8;
     const int row = rb + (lane >> 3), pos = lane & 7;
     const int chunk = pos ^ (row & 7);  // source swizzle = inverse of the read swizzle
     const int tr = region_row<REG>(row);
@@ -180,6 +184,11 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 // the pieces then start half a phase later and the MFMA cluster itself stalls on their issue.
 #ifndef GEMM_DMA_MID
 #define GEMM_DMA_MID 0
+#endif
+// GEMM_HALF: the two-phase K-tile schedule of the main loop (32 / 48 MFMAs per section instead of
+// 16 / 24) -- bit 0: bf16 instances, bit 1: bf16x3 (SPLIT) instances; 0 = the 4-phase schedule (A/B)
+#ifndef GEMM_HALF
+#define GEMM_HALF 3
 #endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
@@ -347,6 +356,34 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         gb[r][i] = (b * p.gC * (p.gh * 8) + ii * 8) * rowlen + jj * 8;
       }
   }
+  // HALF: two-phase K-tile schedule (see the main loop); wave group as a scalar for its branches
+  constexpr bool HALF = ((GEMM_HALF >> (SPLIT ? 1 : 0)) & 1) && !PERSIST && MODE != 1;
+  const int wrs = __builtin_amdgcn_readfirstlane(wr);
+  // HALF batch(kt): R0 (each group its own feature rows) + R1 / R2 (all token rows, wave group 1 only)
+  auto half_batch = [&](int kt, char* st) {
+    if constexpr (HALF) {
+      stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, kt, st, wave, lane0, p, gb);
+      if (wrs == 1) {
+        stage_region<1, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, kt, st, wave - 4, lane0, p, gb);
+        stage_region<2, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, kt, st, wave - 4, lane0, p, gb);
+      }
+    }
+  };
+  bf16x8 a0[8], a1[8], b0[4], b1[4];
+  if constexpr (HALF) {
+    // ---- prologue: batch(0), R3(0), batch(1)
+    half_batch(0, smem);
+    stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+    if (KT > 1) {
+      half_batch(1, smem + kStage);
+      if (wrs == 1) wait_vm<12>();  // batch(0) landed; younger: R3(0) (2) + batch(1) (10 / 2)
+      else wait_vm<4>();
+    } else {
+      wait_vm<2>();
+    }
+    barrier();
+    if (wr == 1) barrier();  // stagger
+  } else {
   // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
   stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
   stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
@@ -360,9 +397,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   barrier();
-  bf16x8 a0[8], a1[8], b0[4], b1[4];
   read_a<0>(a0, smem, wr, lane0 & 15, lane0 >> 4);
   if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
+  }
   if constexpr (!PERSIST) GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
 
   for (;;) {  // PERSIST: one pass per tile (otherwise exactly one)
@@ -406,6 +443,48 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
 #ifndef GEMM_ABLATE
 #define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads,
 #endif                 // bit 2 = epilogue computes but skips its stores
+    if constexpr (HALF) {
+      // Two phases per K-tile instead of four: A(t) = feature rows mi 0 x all 4 token tiles (32 bf16 /
+      // 48 bf16x3 MFMAs; reads R0, R1, R2), B(t) = mi 1 x all token tiles (reads R3, B fragments
+      // kept).  Each wave alternates a read section and an MFMA section, the two wave groups one
+      // barrier apart as above.  DMA: each group fills its own A rows of R0 / R3 (rows 64 wr ..), and
+      // wave group 1 alone fills the B regions R1 / R2 (4 pieces per wave) -- so a region is never
+      // refilled while the other group's reads of it may still be in flight:
+      //   read A(t): wait R3(t) (issued at A(t-1)), DMA R3(t+1);
+      //   read B(t): wait batch(t+1) = R0 (+ R1, R2) (issued at B(t-1)), DMA batch(t+2) into stage t & 1
+      // (every region read by group 0 in section k was confirmed by both groups' waits in sections
+      // <= k - 1; a refill of stage t & 1 starts two barriers after the last read of the old contents).
+      for (int t = 0; t < KT; ++t) {
+        char* cur = smem + (t & 1) * kStage;
+        char* nxt = smem + ((t + 1) & 1) * kStage;
+        const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
+        // ---- read A(t)
+        if (n1) {
+          if (wrs == 1) wait_vm<10>();  // R3(t) landed; younger: batch(t+1)
+          else wait_vm<2>();
+          stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
+        } else {
+          wait_vm<0>();
+        }
+        read_a<0>(a0, cur, wr, r16, kq);
+        read_b<1>(b0, cur, wc, r16, kq);
+        read_b<2>(b1, cur, wc, r16, kq);
+        barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mfma_quadrant<0, 0, SPLIT>(acc, a0, b0, [] {});
+        mfma_quadrant<0, 1, SPLIT>(acc, a0, b1, [] {});
+        barrier();
+        // ---- read B(t)
+        if (n1) wait_vm<2>();  // batch(t+1) landed; younger: R3(t+1)
+        if (n2) half_batch(t + 2, cur);
+        read_a<3>(a0, cur, wr, r16, kq);
+        barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mfma_quadrant<1, 0, SPLIT>(acc, a0, b0, [] {});
+        mfma_quadrant<1, 1, SPLIT>(acc, a0, b1, [] {});
+        barrier();
+      }
+    } else
     for (int t = 0; t < KT; ++t) {
       char* cur = smem + (t & 1) * kStage;
       char* nxt = smem + ((t + 1) & 1) * kStage;
