@@ -27,7 +27,7 @@ struct GemmLaunch {
   // Un-patchify scatter (y is an image [B, sC, sh*8, sw*8]; feature order (c, py, px)).
   int sC = 0, sh = 0, sw = 0;
   int direct_epi = 0;        // gemm.hip MODE 0: 1 = store straight from the MFMA layout (A/B only)
-  float* stats_part = nullptr;       // split mode, fp32 + residual output: [M, N/64, 2] (mean, M2) per 64-feature chunk
+  float* stats_part = nullptr;       // + residual output (fp32 split mode or bf16): [M, N/64, 2] (mean, M2) per 64-feature chunk
   const float* stats_pre = nullptr;  // [N] added to the output before the statistics (required with stats_part)
   int ntiles = 0;            // set by launch_gemm: > 0 = persistent grid (gemm.hip PERSIST), tiles in turn
 #ifdef AMD_DFT_GEMM_STAMPS

@@ -272,8 +272,8 @@ __device__ __forceinline__ float row_sum16(float x) {
   return x;
 }
 
-// STATS (fp32 output, LDS-staged epilogue): per token and 64-feature chunk of the output plus the
-// per-channel p.stats_pre, the chunk's (mean, M2 = sum of squared deviations) into
+// STATS (fp32 or bf16 output, LDS-staged epilogue): per token and 64-feature chunk of the output (bf16:
+// the stored, rounded values) plus the per-channel p.stats_pre, the chunk's (mean, M2 = sum of squared deviations) into
 // p.stats_part[t][chunk] -- the next LayerNorm's statistics without a pass over the output
 // (merged per token by ln_stats_merge, Chan's formula)
 //
@@ -629,9 +629,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               for (int it = 0; it < PD; ++it) load_rr(it);
             }
           };
-          float4 spre = make_float4(0.f, 0.f, 0.f, 0.f);
+          float4 spre = make_float4(0.f, 0.f, 0.f, 0.f), spre2 = spre;  // OUT 0: the lane's 8 features
           if constexpr (STATS && !PERSIST) {  // ahead of the residual prefetch: the wait for its first row covers it
-            spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + 4 * c);  // required (host: zeros if none)
+            // required (host: zeros if none)
+            spre = *reinterpret_cast<const float4*>(p.stats_pre + fh + (OUT == 1 ? 4 : 8) * c);
+            if constexpr (OUT == 0) spre2 = *reinterpret_cast<const float4*>(p.stats_pre + fh + 8 * c + 4);
           }
           if (!PERSIST || h > 0) prefetch();
 #pragma unroll
@@ -718,6 +720,17 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                 uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
                 if constexpr (OUT == 0) {
                   *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
+                  if constexpr (STATS && !PERSIST) {
+                    // the STORED (bf16-rounded) values + pre back into the two staging slots: the
+                    // statistics describe exactly the tensor the next LayerNorm reads
+                    char* rw = const_cast<char*>(rp);
+                    *reinterpret_cast<float4*>(rw + (((fl >> 2) ^ (row & 15)) << 4)) =
+                        make_float4(__uint_as_float(w.x << 16) + spre.x, __uint_as_float(w.x & 0xffff0000u) + spre.y,
+                                    __uint_as_float(w.y << 16) + spre.z, __uint_as_float(w.y & 0xffff0000u) + spre.w);
+                    *reinterpret_cast<float4*>(rw + ((((fl >> 2) + 1) ^ (row & 15)) << 4)) =
+                        make_float4(__uint_as_float(w.z << 16) + spre2.x, __uint_as_float(w.z & 0xffff0000u) + spre2.y,
+                                    __uint_as_float(w.w << 16) + spre2.z, __uint_as_float(w.w & 0xffff0000u) + spre2.w);
+                  }
                 } else {  // split pair: hi = bf16(v), lo = bf16(v - hi), both stored by this lane
                   uint4 lw;
                   const uint32_t* wp = &w.x;
@@ -738,22 +751,23 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           }
           if constexpr (STATS && !PERSIST) {
             // lane l: token row l of this half, its 64 features (output + pre) from the staging slots
-            // written above -- two sweeps (mean, then M2 about it) instead of two 16-lane DPP
-            // reductions per pass (~45 VALU per pass: 9.6k cycles per tile, profiles/phases_r4.txt)
+            // written above, in ONE sweep of shifted sums (shift = the row's first value, so the
+            // M2 = S2 - S1^2 / 64 cancellation stays at a few std): no cross-lane reductions
+            // (~45 VALU per pass as 16-lane DPP row sums: 9.6k cycles per tile, profiles/phases_r4.txt)
             const char* rl = reg + lane * 256;
-            f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4 q0 = *reinterpret_cast<const f32x4*>(rl + ((0 ^ (lane & 15)) << 4));
+            const float sh = q0[0];
+            f32x4 s1 = q0 - sh, s2 = s1 * s1;
 #pragma unroll
-            for (int ch = 0; ch < 16; ++ch) sv += *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4));
-            const float mean = ((sv[0] + sv[1]) + (sv[2] + sv[3])) * (1.f / 64.f);
-            f32x4 qv = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ch = 0; ch < 16; ++ch) {
-              const f32x4 d = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4)) - mean;
-              qv += d * d;
+            for (int ch = 1; ch < 16; ++ch) {
+              const f32x4 d = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4)) - sh;
+              s1 += d;
+              s2 += d * d;
             }
+            const float t1 = (s1[0] + s1[1]) + (s1[2] + s1[3]), t2 = (s2[0] + s2[1]) + (s2[2] + s2[3]);
             const int t = min(tbase + lane, M - 1);  // rows >= M: bit-identical copies of row M - 1
             *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
-                make_float2(mean, (qv[0] + qv[1]) + (qv[2] + qv[3]));
+                make_float2(sh + t1 * (1.f / 64.f), fmaxf(t2 - t1 * t1 * (1.f / 64.f), 0.f));
           }
         }
         if constexpr (PERSIST) {
@@ -883,6 +897,15 @@ void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 // (the bf16 block's forms -- LN-folded fc1, fc2 + residual -- have persistent variants)
 template <int ACT, bool BIAS, bool RES>
 void launch_ln(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if constexpr (RES && ACT == 0 && !BIAS) {
+    if (p.stats_part) {  // fc2 of the bf16 block: + the next LayerNorm's partial statistics (staged epilogue)
+      if (p.ln_stats || p.direct_epi || !p.stats_pre)
+        throw std::runtime_error("amd_dft: gemm: bf16 statistics need the staged epilogue, stats_pre and no LayerNorm fold");
+      launch_one<0, false, true, false, 0, false, 0, true>(p, st, grid);
+      return;
+    }
+  }
+  if (p.stats_part) throw std::runtime_error("amd_dft: gemm: output statistics only with a residual, no activation / bias");
   if (p.ln_stats) launch_one<ACT, BIAS, RES, true, 0, false, 0, false, !RES>(p, st, grid);
   else launch_one<ACT, BIAS, RES, false, 0, false, 0, false, RES>(p, st, grid);
 }

@@ -982,6 +982,81 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cpu(const at::Te
   return split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre), stats);
 }
 
+// bf16 block: c2r_ln_add + the next LayerNorm's per-64-channel partials (mean, M2) of the STORED
+// (bf16-rounded) output, from the one C2R epilogue (afno_wfft.hip PART instantiation); ln_stats_merge
+// turns them into LN2's (mean, rstd) without an ln_stats pass over the residual stream.
+// Returns (out [..., W, C] bf16, part [tokens, C/64, 2] fp32).
+std::tuple<at::Tensor, at::Tensor> out_and_partials(const at::Tensor& y) {
+  const int64_t C = y.size(-1);
+  at::Tensor w = y.reshape({-1, C / 64, 64}).to(at::kFloat);
+  at::Tensor mean = w.mean(2);
+  at::Tensor m2 = (w - mean.unsqueeze(2)).pow(2).sum(2);
+  return {y, at::stack({mean, m2}, 2).contiguous()};
+}
+
+void check_part_out(const at::Tensor& X, const at::Tensor& x, const char* op) {
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "amd_dft.", op,
+              ": bf16 spectrum and residual stream (the fp32 block uses c2r_ln_add_split)");
+  TORCH_CHECK(x.size(-1) % 64 == 0, "amd_dft.", op, ": C must be a multiple of 64");
+}
+
+std::tuple<at::Tensor, at::Tensor> c2r_ln_add_part_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double scale,
+                                                        const at::Tensor& x_, const at::Tensor& stats_, const at::Tensor& g_,
+                                                        const at::Tensor& b_, const std::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(X_.device());
+  check_ln_args(x_, dim, stats_, g_, b_, pre_, "c2r_ln_add_part");
+  check_part_out(X_, x_, "c2r_ln_add_part");
+  const int64_t axis = x_.dim() - 2;
+  TORCH_CHECK(X_.dim() == x_.dim() + 1 && X_.size(-1) == 2 && x_.size(axis) == n &&
+                  X_.sizes().slice(0, axis) == x_.sizes().slice(0, axis) && X_.size(axis + 1) == x_.size(-1) &&
+                  X_.size(axis) <= n / 2 + 1,
+              "amd_dft.c2r_ln_add_part: X must be [..., km, C, 2] with the leading dims and C of x and km <= n/2+1");
+  at::Tensor X = X_.contiguous(), x = x_.contiguous();
+  const int64_t km = X.size(axis), C = x.size(-1);
+  if (X.numel() > 0 && afno_w_enabled() && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
+      x.numel() / (n * C) < (int64_t(1) << 31)) {
+    at::Tensor stats = stats_.to(at::kFloat).contiguous(), g = g_.to(at::kFloat).contiguous(),
+               b = b_.to(at::kFloat).contiguous();
+    at::Tensor pre;
+    if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
+    const int64_t M = x.numel() / C;
+    at::Tensor out = at::empty_like(x);
+    at::Tensor part = at::empty({M, C / 64, 2}, x.options().dtype(at::kFloat));
+    AfnoWLaunch p;  // bf16 two-pass kernel with the partial-statistics epilogue (afno_wfft.hip PART)
+    p.x = x.data_ptr();
+    p.stats = stats.data_ptr<float>();
+    p.gamma = g.data_ptr<float>();
+    p.beta = b.data_ptr<float>();
+    p.pre = pre_.has_value() ? pre.data_ptr<float>() : nullptr;
+    p.spec = X.data_ptr();
+    p.out = out.data_ptr();
+    p.part = part.data_ptr<float>();
+    p.O = static_cast<int>(M / n);
+    p.L = static_cast<int>(n);
+    p.C = static_cast<int>(C);
+    p.KM = static_cast<int>(km);
+    p.scale = static_cast<float>(scale);
+    launch_afno_w_c2r_ln(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    return {checked(out, "c2r_ln_add_part"), part};
+  }
+  fallback_note("c2r_ln_add_part", "no fused W-transform for this shape: c2r_ln_add + ATen statistics");
+  return out_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_));
+}
+
+std::tuple<at::Tensor, at::Tensor> c2r_ln_add_part_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale,
+                                                       const at::Tensor& x, const at::Tensor& stats, const at::Tensor& g,
+                                                       const at::Tensor& b, const std::optional<at::Tensor>& pre) {
+  check_part_out(X, x, "c2r_ln_add_part");
+  return out_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre));
+}
+
+std::tuple<at::Tensor, at::Tensor> c2r_ln_add_part_meta(const at::Tensor&, int64_t, int64_t, double, const at::Tensor& x,
+                                                        const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                                                        const std::optional<at::Tensor>&) {
+  const int64_t C = x.size(-1), M = x.numel() / std::max<int64_t>(C, 1);
+  return {at::empty_like(x), at::empty({M, C / 64, 2}, x.options().dtype(at::kFloat))};
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_meta(const at::Tensor&, int64_t, int64_t, double,
                                                                      const at::Tensor& x, const at::Tensor&, const at::Tensor&,
                                                                      const at::Tensor&, const std::optional<at::Tensor>&) {
@@ -1168,6 +1243,8 @@ TORCH_LIBRARY(amd_dft, m) {
         "Tensor? pre=None) -> Tensor");
   m.def("c2r_ln_add_split(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
         "Tensor? pre=None) -> (Tensor, Tensor, Tensor)");
+  m.def("c2r_ln_add_part(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
+        "Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("Irfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");
   m.def("plan_info(int n) -> str", &amd_dft::plan_info);
@@ -1188,6 +1265,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cuda));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cuda));
   m.impl("c2r_ln_add_split", AMD_DFT_TRACED("amd_dft::c2r_ln_add_split", amd_dft::c2r_ln_add_split_cuda));
+  m.impl("c2r_ln_add_part", AMD_DFT_TRACED("amd_dft::c2r_ln_add_part", amd_dft::c2r_ln_add_part_cuda));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -1201,6 +1279,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("r2c_ln", AMD_DFT_TRACED("amd_dft::r2c_ln", amd_dft::r2c_ln_cpu));
   m.impl("c2r_ln_add", AMD_DFT_TRACED("amd_dft::c2r_ln_add", amd_dft::c2r_ln_add_cpu));
   m.impl("c2r_ln_add_split", AMD_DFT_TRACED("amd_dft::c2r_ln_add_split", amd_dft::c2r_ln_add_split_cpu));
+  m.impl("c2r_ln_add_part", AMD_DFT_TRACED("amd_dft::c2r_ln_add_part", amd_dft::c2r_ln_add_part_cpu));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -1214,6 +1293,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("r2c_ln", &amd_dft::r2c_ln_meta);
   m.impl("c2r_ln_add", &amd_dft::c2r_ln_add_meta);
   m.impl("c2r_ln_add_split", &amd_dft::c2r_ln_add_split_meta);
+  m.impl("c2r_ln_add_part", &amd_dft::c2r_ln_add_part_meta);
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CompositeImplicitAutograd, m) {

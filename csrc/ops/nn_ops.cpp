@@ -496,6 +496,70 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_meta(const at::Tensor& xs, cons
   return {at::empty(os, xs.options().dtype(at::kFloat)), at::empty({M, ws.size(0) / 64, 2}, xs.options().dtype(at::kFloat))};
 }
 
+// fc2 of the bf16 FourCastNet block: y = x w^T + residual (bf16) and, from the same epilogue, the
+// next LayerNorm's partial statistics of y + pre -- taken on the stored (bf16-rounded) y, so they
+// describe exactly the tensor that LayerNorm reads: part [M, N/64, 2] = per 64-feature chunk
+// (mean, M2), merged by ln_stats_merge (replaces an ln_stats pass over y)
+std::tuple<at::Tensor, at::Tensor> chunk_partials(const at::Tensor& y, const c10::optional<at::Tensor>& pre, int64_t N) {
+  at::Tensor w = y.to(at::kFloat).reshape({-1, N});
+  if (pre.has_value() && pre->defined()) w = w + pre->to(at::kFloat).reshape({1, N});
+  w = w.reshape({w.size(0), N / 64, 64});
+  at::Tensor mean = w.mean(2);
+  at::Tensor m2 = (w - mean.unsqueeze(2)).pow(2).sum(2);
+  return {y, at::stack({mean, m2}, 2).contiguous()};
+}
+
+std::tuple<at::Tensor, at::Tensor> linear_stats_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& residual,
+                                                    const c10::optional<at::Tensor>& pre) {
+  TORCH_CHECK(w.dim() == 2 && x.size(-1) == w.size(1), "amd_dft.linear_stats: x [..., K], w [N, K]");
+  const int64_t N = w.size(0);
+  TORCH_CHECK(N % 64 == 0, "amd_dft.linear_stats: N must be a multiple of 64");
+  TORCH_CHECK(!pre.has_value() || !pre->defined() || pre->numel() == N, "amd_dft.linear_stats: pre must have N entries");
+  return chunk_partials(linear_ref(x, w, c10::nullopt, 0, residual), pre, N);
+}
+
+std::tuple<at::Tensor, at::Tensor> linear_stats_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::Tensor& residual,
+                                                     const c10::optional<at::Tensor>& pre_) {
+  const c10::DeviceGuard guard(x_.device());
+  TORCH_CHECK(w_.dim() == 2 && x_.size(-1) == w_.size(1), "amd_dft.linear_stats: x [..., K], w [N, K]");
+  const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(N % 64 == 0, "amd_dft.linear_stats: N must be a multiple of 64");
+  TORCH_CHECK(residual.numel() == M * N, "amd_dft.linear_stats: residual must have the output's shape");
+  TORCH_CHECK(!pre_.has_value() || !pre_->defined() || pre_->numel() == N, "amd_dft.linear_stats: pre must have N entries");
+  if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K)) {
+    fallback_note("linear_stats", "needs bf16 operands, N % 256 == 0, K % 64 == 0");
+    return chunk_partials(linear_ref(x_, w_, c10::nullopt, 0, residual), pre_, N);
+  }
+  at::Tensor x = x_.contiguous(), w = w_.contiguous(), r = residual.to(at::kBFloat16).contiguous();
+  // the kernel always reads pre (zeros when absent): see linear3_stats
+  at::Tensor pre = pre_.has_value() && pre_->defined() ? pre_->to(at::kFloat).contiguous()
+                                                       : at::zeros({N}, x.options().dtype(at::kFloat));
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = N;
+  at::Tensor y = at::empty(os, x.options());
+  at::Tensor part = at::empty({M, N / 64, 2}, x.options().dtype(at::kFloat));
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  p.residual = r.data_ptr();
+  p.y = y.data_ptr();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.stats_part = part.data_ptr<float>();
+  p.stats_pre = pre.data_ptr<float>();
+  if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  return {y, part};
+}
+
+std::tuple<at::Tensor, at::Tensor> linear_stats_meta(const at::Tensor& x, const at::Tensor& w, const at::Tensor&,
+                                                     const c10::optional<at::Tensor>&) {
+  std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
+  os.back() = w.size(0);
+  const int64_t M = x.numel() / std::max<int64_t>(x.size(-1), 1);
+  return {at::empty(os, x.options()), at::empty({M, w.size(0) / 64, 2}, x.options().dtype(at::kFloat))};
+}
+
 // fc1 of the fp32 FourCastNet block: y = split(act(LN(x) W^T + b)) from the split pairs of the RAW
 // residual stream x (the AFNO C2R epilogue writes them, c2r_ln_add_split), the LayerNorm folded into
 // the bf16x3 GEMM's epilogue exactly as linear_ln does for bf16: ws = split(W * gamma),
@@ -679,6 +743,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
   m.def("linear3(Tensor xs, Tensor ws, Tensor? bias=None, int act=0, Tensor? residual=None, bool split_out=False) -> Tensor");
   m.def("linear3_stats(Tensor xs, Tensor ws, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
+  m.def("linear_stats(Tensor x, Tensor w, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("linear3_ln(Tensor xs, Tensor ws, Tensor c1, Tensor? bias, Tensor stats, int act=0) -> Tensor");
   m.def("patch_linear3(Tensor xs, Tensor ws, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
   m.def("linear_unpatch3(Tensor ts, Tensor ws, Tensor? bias, int C, int h, int w, int p=8) -> Tensor");
@@ -693,6 +758,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cuda));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cuda));
+  m.impl("linear_stats", AMD_DFT_TRACED("amd_dft::linear_stats", amd_dft::linear_stats_cuda));
   m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cuda));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cuda));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cuda));
@@ -707,6 +773,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cpu));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cpu));
+  m.impl("linear_stats", AMD_DFT_TRACED("amd_dft::linear_stats", amd_dft::linear_stats_cpu));
   m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cpu));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cpu));
   m.impl("linear_unpatch3", AMD_DFT_TRACED("amd_dft::linear_unpatch3", amd_dft::linear_unpatch3_cpu));
@@ -721,6 +788,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("split_bf16", &amd_dft::split_bf16_meta);
   m.impl("linear3", &amd_dft::linear3_meta);
   m.impl("linear3_stats", &amd_dft::linear3_stats_meta);
+  m.impl("linear_stats", &amd_dft::linear_stats_meta);
   m.impl("linear3_ln", &amd_dft::linear3_ln_meta);
   m.impl("patch_linear3", &amd_dft::patch_linear3_meta);
   m.impl("linear_unpatch3", &amd_dft::linear_unpatch3_meta);

@@ -83,7 +83,7 @@ struct WArgs {
   const void* spec;      // C2R input [O, KM, C, 2] bf16 / fp32
   void* out;             // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
   uint16_t* pairs;       // C2R, SPLIT: [O * 180, 2C] bf16 split pairs of out - mean(x) (stats .x)
-  float* part;           // C2R, SPLIT: [O * 180, C / 64, 2] (mean, M2) of out per 64-channel slab
+  float* part;           // C2R, SPLIT / PART: [O * 180, C / 64, 2] (mean, M2) of out per 64-channel slab
   int C, nslab;
   float scale;
 };
@@ -294,9 +294,13 @@ constexpr int c2r_load_kind(int n1) {
 #ifndef AFNO_C2R_JIT
 #define AFNO_C2R_JIT 0  // fp32: addends loaded 3 positions ahead inside the epilogue (A/B; see below)
 #endif
-template <int KM, bool F32, bool SPLIT = false>
+// PART (bf16 block): the epilogue also writes the next LayerNorm's per-64-channel partials of the STORED
+// (bf16-rounded) output -- the rounded values staged in the (then idle) fp16 FFT buffer, one thread per
+// position sweeping its 64 channels -- so the bf16 block needs no ln_stats pass over x1 either.
+template <int KM, bool F32, bool SPLIT = false, bool PART = false>
 __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(!SPLIT || F32, "split-pair outputs come with the fp32 instantiation");
+  static_assert(!PART || (!F32 && AFNO_C2R_XLDS), "bf16 partials: the fp16-staged bf16 instantiation");
   static_assert(KM >= 1 && 2 * KM <= kL, "pruned half spectrum");
   // bf16 (XLDS): fp16 FFT staging (24.5 KB) + the residual tile x[o, 0..179, slab] (23 KB) + its
   // LN statistics: 49.6 KB -> still 3 workgroups per CU, and the addends need no VGPRs.
@@ -427,14 +431,14 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
   __builtin_amdgcn_sched_barrier(0);
   // SPLIT: the staging buffer takes the outputs for the per-position statistics below -- every
   // wave past its pass-1 reads first (the k1 >= 12 wave has exited: barriers count live waves)
-  if constexpr (SPLIT) __syncthreads();
+  if constexpr (SPLIT || PART) __syncthreads();
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
   const int64_t obase = xbase;
   void* ob = F32 ? static_cast<void*>(static_cast<float*>(a.out) + obase)
                  : static_cast<void*>(static_cast<uint16_t*>(a.out) + obase);
   const float sc = a.scale;
   uint16_t* const pbase = SPLIT ? a.pairs + static_cast<int64_t>(o) * kL * (2 * C) : nullptr;
-  float* const sbase_part = SPLIT ? a.part + (static_cast<int64_t>(o) * kL * a.nslab + slab) * 2 : nullptr;
+  float* const sbase_part = SPLIT || PART ? a.part + (static_cast<int64_t>(o) * kL * a.nslab + slab) * 2 : nullptr;
 #pragma unroll
   for (int k2 = 0; k2 < kB; ++k2) {
     if constexpr (JIT) {
@@ -456,6 +460,10 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
       y[2 * p + 1] = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
     }
     stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
+    if constexpr (PART) {  // the stored bf16 values (8 B) into position n's row of the idle staging buffer
+      const int n = k1 + kA * k2;
+      *reinterpret_cast<uint2*>(smem + n * (kPitch * 4) + 8 * g) = make_uint2(bfpack(y[0], y[1]), bfpack(y[2], y[3]));
+    }
     if constexpr (SPLIT) {
       // workgroup-uniform bases (o's first token) + 32-bit lane offsets: position n = k1 + 12 k2
       // the pairs hold y - mean(x) (x's LayerNorm mean, already in sv): the split then resolves y's
@@ -478,33 +486,58 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
     if constexpr (F32) __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (SPLIT) {
-    // LN2 partials of this slab: one thread per output position sweeps its 64 staged channels
-    // (mean, then M2 about it) -- two 16-lane DPP reductions per position and lane cost ~10x the VALU
+    // LN2 partials of this slab: one thread per output position sweeps its 64 staged channels once,
+    // as shifted sums (shift = the position's first value: M2 = S2 - S1^2 / 64 cancels only a few std)
+    // -- two 16-lane DPP reductions per position and lane cost ~10x the VALU
     __syncthreads();
     const int n = threadIdx.x;
     if (n < kL) {
       const float4* row = reinterpret_cast<const float4*>(lds + n * kPitch);
-      float4 sv4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float sh = row[0].x;
+      float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
 #pragma unroll
       for (int j = 0; j < kG; ++j) {
         const float4 q = row[j];
-        sv4.x += q.x;
-        sv4.y += q.y;
-        sv4.z += q.z;
-        sv4.w += q.w;
+        const float d0 = q.x - sh, d1 = q.y - sh, d2 = q.z - sh, d3 = q.w - sh;
+        s1.x += d0;
+        s1.y += d1;
+        s1.z += d2;
+        s1.w += d3;
+        s2.x = fmaf(d0, d0, s2.x);
+        s2.y = fmaf(d1, d1, s2.y);
+        s2.z = fmaf(d2, d2, s2.z);
+        s2.w = fmaf(d3, d3, s2.w);
       }
-      const float mean = ((sv4.x + sv4.y) + (sv4.z + sv4.w)) * (1.f / 64.f);
-      float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float t1 = (s1.x + s1.y) + (s1.z + s1.w), t2 = (s2.x + s2.y) + (s2.z + s2.w);
+      *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) =
+          make_float2(sh + t1 * (1.f / 64.f), fmaxf(t2 - t1 * t1 * (1.f / 64.f), 0.f));
+    }
+  }
+  if constexpr (PART) {
+    // one sweep of shifted sums (shift = the position's first value; M2 = S2 - S1^2 / 64 then cancels
+    // only a few std): the 64 stored values are read once
+    __syncthreads();
+    const int n = threadIdx.x;
+    if (n < kL) {
+      const uint4* row = reinterpret_cast<const uint4*>(smem + n * (kPitch * 4));
+      const float sh = __uint_as_float(row[0].x << 16);
+      float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
 #pragma unroll
-      for (int j = 0; j < kG; ++j) {
-        const float4 q = row[j];
-        const float d0 = q.x - mean, d1 = q.y - mean, d2 = q.z - mean, d3 = q.w - mean;
-        m4.x = fmaf(d0, d0, m4.x);
-        m4.y = fmaf(d1, d1, m4.y);
-        m4.z = fmaf(d2, d2, m4.z);
-        m4.w = fmaf(d3, d3, m4.w);
+      for (int j = 0; j < 8; ++j) {  // 8 bf16 per 16 B
+        const uint4 q = row[j];
+        const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+        float* a1 = &s1.x;
+        float* a2 = &s2.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d0 = __uint_as_float(u[k] << 16) - sh, d1 = __uint_as_float(u[k] & 0xffff0000u) - sh;
+          a1[k] += d0 + d1;
+          a2[k] = fmaf(d0, d0, fmaf(d1, d1, a2[k]));
+        }
       }
-      *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) = make_float2(mean, (m4.x + m4.y) + (m4.z + m4.w));
+      const float t1 = (s1.x + s1.y) + (s1.z + s1.w), t2 = (s2.x + s2.y) + (s2.z + s2.w);
+      *reinterpret_cast<float2*>(sbase_part + n * (2 * a.nslab)) =
+          make_float2(sh + t1 * (1.f / 64.f), fmaxf(t2 - t1 * t1 * (1.f / 64.f), 0.f));
     }
   }
 }
@@ -551,9 +584,10 @@ void launch_afno_w_c2r_ln(const AfnoWLaunch& p, void* stream) {
   check_launch(p, "afno_w_c2r_ln");
   const WArgs a = make_args(p);
   const dim3 grid(static_cast<uint32_t>(static_cast<int64_t>(p.O) * a.nslab));
-  if ((p.pairs != nullptr) != (p.part != nullptr) || (p.pairs && !p.f32))
-    throw std::runtime_error("amd_dft: afno_w_c2r_ln: split pairs and partial statistics come together, fp32 only");
+  if (p.f32 ? (p.pairs != nullptr) != (p.part != nullptr) : p.pairs != nullptr)
+    throw std::runtime_error("amd_dft: afno_w_c2r_ln: fp32: split pairs and partial statistics come together; bf16: partials only");
   if (p.pairs) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+  else if (p.part) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, false, false, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   else if (p.f32) hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, true>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   else hipLaunchKernelGGL((afno_w_c2r_ln_kernel<46, false>), grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();

@@ -168,7 +168,7 @@ def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
 
 class LnCarry(NamedTuple):
     """A per-channel pending bias plus the next LayerNorm's statistics of ``x + bias`` as
-    per-64-channel partials (``linear3_stats``), carried from one fp32 block to the next."""
+    per-64-channel partials (``linear3_stats`` / ``linear_stats``), carried from one block to the next."""
     bias: torch.Tensor
     part: torch.Tensor
 
@@ -190,7 +190,7 @@ def afno_block_amd(blk, x: torch.Tensor, pending=None, split_out: bool = False):
     Residual-stream fusion: the block returns ``(x, p)`` with the true block output being
     ``x + p``.  ``p`` is either a per-channel vector (the fc2 bias; LayerNorm-fused paths, see
     :func:`afno_block_fused` / :func:`afno_block_fused_f32`), an :class:`LnCarry` (that vector
-    plus the next LayerNorm's partial statistics, fp32 path), or a full tensor (the fc2 output;
+    plus the next LayerNorm's partial statistics, LN-fused paths), or a full tensor (the fc2 output;
     generic path, where the addition is fused into the next block's LN1).
     ``split_out`` (last block before the fp32 head): the fp32 fused path may return its output as
     :class:`SplitRows` instead of an fp32 tensor.
@@ -203,7 +203,7 @@ def afno_block_amd(blk, x: torch.Tensor, pending=None, split_out: bool = False):
     if (pending is None or pending.dim() == 1) and _ln_fused_ok(blk, x):
         if x.dtype == torch.float32:
             return afno_block_fused_f32(blk, x, pending, part, split_out)
-        return afno_block_fused(blk, x, pending)
+        return afno_block_fused(blk, x, pending, part)
     x, yn = afno_block_spectral(blk, x, pending)
     return x, afno_block_mlp(blk, yn)
 
@@ -238,23 +238,30 @@ def _mlp_gemm_ok(m, split: bool) -> bool:
             and k_ok(f2.in_features))
 
 
-def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
+def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None):
     """FourCastNet block (bf16) with LN1 fused into the AFNO W-transforms and fc2 accumulated
     in place.
 
     The residual stream is carried as ``(xs, pre)`` with true x = xs + pre (pre = the previous
     block's fc2 bias, per channel, or None):
 
-      stats = (mean, rstd) of x                  ln_stats: reads xs once, writes 8 B/token
+      stats = (mean, rstd) of x                  ln_stats_merge of the previous fc2's partials
+                                                 (first block: ln_stats over xs)
       X_w   = R2C_W(LN1(x))                      LN applied on load (no normalised copy in HBM)
       Y_w   = FFT_H -> block MLP -> IFFT_H       afno_spectral (MFMA)
-      x1    = C2R_W(Y_w) + LN1(x) + x            both skips from one read of xs
-      h     = GELU(fc1(LN2(x1)))                 ln_stats + hand MFMA GEMM with LN2 folded in
+      x1    = C2R_W(Y_w) + LN1(x) + x            both skips from one read of xs; the epilogue also
+                                                 writes LN2's per-64-channel partials of the stored
+                                                 x1 (c2r_ln_add_part)
+      h     = GELU(fc1(LN2(x1)))                 ln_stats_merge + hand MFMA GEMM with LN2 folded in
                                                  (linear_ln) and the erf GELU in the epilogue
-      x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue
+      x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue, which also
+                                                 emits the next LN1's partials of x1 + b2
+                                                 (linear_stats)
 
-    Returns (x1, fc2.bias): the bias is folded into the next block's statistics and loads
-    (or the head GEMM's bias).
+    ``part``: those partials from the previous block (else ln_stats runs).  Returns
+    (x1, LnCarry(fc2.bias, partials)): the bias is folded into the next block's statistics and
+    loads (or the head GEMM's bias).  No pass over the residual stream beyond the block's own
+    kernels (round 3: two ln_stats passes per block, 0.28 ms of 6.3).
     """
     from ..models.afno import kept_window
 
@@ -268,20 +275,30 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None):
     m = blk.mlp
     pre32 = None if pre is None else _f32(blk, "pre", pre)
     g1, be1 = _f32(blk, "g1", n1.weight), _f32(blk, "b1", n1.bias)
-    stats = ops.ln_stats(xs, pre32, n1.eps)
+    stats = ops.ln_stats_merge(part, n1.eps) if part is not None else ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.bfloat16)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
     if mlp_on_hand_gemm():
         # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
         # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL
         # collective blocks), which stall hipBLASLt's persistent stream-K grid.  LN2 is folded
-        # into fc1 (linear_ln): only the per-token statistics are computed, no normalised copy.
-        st2 = ops.ln_stats(x1, None, blk.norm2.eps)
+        # into fc1 (linear_ln): only the per-token statistics, merged from the C2R epilogue's
+        # partials (ln_stats_merge takes <= 64 chunks of 64 channels).
+        if C <= 64 * 64:
+            x1, part2 = ops.c2r_ln_add_part(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+            st2 = ops.ln_stats_merge(part2, blk.norm2.eps)
+        else:
+            x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+            st2 = ops.ln_stats(x1, None, blk.norm2.eps)
         w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
         hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 1)
-        x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
-        return x1, m.fc2.bias
+        if C > 64 * 64:
+            x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
+            return x1, m.fc2.bias
+        b2 = _f32(m, "fc2_b", m.fc2.bias)
+        x1n, part_next = ops.linear_stats(hid, m.fc2.weight, x1.reshape(-1, C), b2)
+        return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
+    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
     yn, _ = layer_norm(x1, blk.norm2)
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
     if torch.jit.is_tracing():
