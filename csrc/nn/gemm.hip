@@ -190,28 +190,10 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 #ifndef GEMM_HALF
 #define GEMM_HALF 3
 #endif
-// GEMM_X3_TILE (A/B): bf16x3 products grouped per accumulator tile ((hi,hi), (lo,hi), (hi,lo) of one tile in
-// a row: operand fragments reused by consecutive MFMAs) instead of products outermost
-#ifndef GEMM_X3_TILE
-#define GEMM_X3_TILE 0
-#endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
                                               Mid&& mid) {
   __builtin_amdgcn_s_setprio(1);
-  if constexpr (SPLIT && GEMM_X3_TILE) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4& c = acc[MI * 4 + i][NI * 2 + j];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[4 + i], b[j], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[2 + j], c, 0, 0, 0);
-      }
-    __builtin_amdgcn_s_setprio(0);
-    return;
-  }
   constexpr int NP = SPLIT ? 3 : 2;
 #pragma unroll
   for (int s = 0; s < NP; ++s) {
