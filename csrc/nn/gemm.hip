@@ -794,6 +794,60 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         return;
       }
     }
+    if constexpr (MODE == 2 && !PERSIST) {  // MI_DFT_GEMM_EPI=direct: the scatter straight from the MFMA layout (A/B)
+      if (!p.direct_epi) {
+        // ---- un-patchify epilogue through LDS (the head GEMM).  Straight from the MFMA layout a lane
+        // writes 4 pixels (8 / 16 B) of one (token, feature row) -- partial lines all over the image.
+        // A half is one output channel's 64 (py, px) features: it is parked as fp32 like the
+        // token-major epilogue above, then pass py has lane l write the 8 pixels px = 0..7 of token
+        // tbase + l in image row (patch row) * 8 + py -- consecutive tokens of one patch row are
+        // consecutive 8-pixel runs, so a store instruction covers whole lines (16 / 32 B per lane).
+        // Token rows >= M (ragged last panel) hold bit-identical copies of row M - 1 and are stored
+        // there (benign duplicates), so no store is predicated.  fp32 head 2468 -> 2277 us per call
+        // (profiles/kernels_r4_final_fp32.txt vs session 18).
+        barrier();  // every wave is past its last fragment read of the stage buffers
+        char* reg = smem + wave * (64 * 256);
+        const int t = min(t0 + wc * 64 + lane, M - 1);
+        const int hw = p.sh * p.sw;
+        const int bb = t / hw, rem = t - bb * hw;
+        const int pi = rem / p.sw, pj = rem - pi * p.sw;
+        const int64_t rowlen = static_cast<int64_t>(p.sw) * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = (f0 + wr * 128 + h * 64) >> 6;  // output channel of this half
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * h + ii;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              gelu_f2 v[2];
+              epi_act<ACT, LN>(acc[i][j], bias4[i], c14[i], lst[j], v);
+              const int row = j * 16 + r16, chk = ii * 4 + kq;
+              *reinterpret_cast<float4*>(reg + row * 256 + ((chk ^ (row & 15)) << 4)) = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+            }
+          }
+          const char* rl = reg + lane * 256;  // this lane's token row of the staged half
+          const int64_t obase = ((static_cast<int64_t>(bb) * p.sC + ch) * (p.sh * 8) + pi * 8) * rowlen + pj * 8;
+#pragma unroll
+          for (int py = 0; py < 8; ++py) {
+            const float4 u0 = *reinterpret_cast<const float4*>(rl + (((2 * py) ^ (lane & 15)) << 4));
+            const float4 u1 = *reinterpret_cast<const float4*>(rl + (((2 * py + 1) ^ (lane & 15)) << 4));
+            const int64_t o = obase + py * rowlen;
+            if constexpr (OUT == 1) {
+              float* yp = static_cast<float*>(p.y) + o;
+              *reinterpret_cast<float4*>(yp) = u0;
+              *reinterpret_cast<float4*>(yp + 4) = u1;
+            } else {
+              *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + o) =
+                  make_uint4(pk_bf16(u0.x, u0.y), pk_bf16(u0.z, u0.w), pk_bf16(u1.x, u1.y), pk_bf16(u1.z, u1.w));
+            }
+          }
+        }
+        GEMM_STAMP(4, __builtin_amdgcn_s_memtime());
+        GEMM_STAMP(5, __builtin_amdgcn_s_memrealtime());
+        return;
+      }
+    }
     constexpr bool ERES = RES;
     ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
     if constexpr (ERES) {
