@@ -295,8 +295,8 @@ constexpr int c2r_load_kind(int n1) {
 #define AFNO_C2R_JIT 0  // fp32: addends loaded 3 positions ahead inside the epilogue (A/B; see below)
 #endif
 // PART (bf16 block): the epilogue also writes the next LayerNorm's per-64-channel partials of the STORED
-// (bf16-rounded) output -- the rounded values staged in the (then idle) fp16 FFT buffer, one thread per
-// position sweeping its 64 channels -- so the bf16 block needs no ln_stats pass over x1 either.
+// (bf16-rounded) output -- the rounded values written over the lane's own slot of the residual tile in LDS,
+// one thread per position sweeping its 64 channels -- so the bf16 block needs no ln_stats pass over x1 either.
 template <int KM, bool F32, bool SPLIT = false, bool PART = false>
 __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno_w_c2r_ln_kernel(const WArgs a) {
   static_assert(!SPLIT || F32, "split-pair outputs come with the fp32 instantiation");
@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
   __builtin_amdgcn_sched_barrier(0);
   // SPLIT: the staging buffer takes the outputs for the per-position statistics below -- every
   // wave past its pass-1 reads first (the k1 >= 12 wave has exited: barriers count live waves)
-  if constexpr (SPLIT || PART) __syncthreads();
+  if constexpr (SPLIT) __syncthreads();
   // ---- epilogue: y = scale * conj(u) + x' + LN(x'), output n = k1 + 12 k2
   const int64_t obase = xbase;
   void* ob = F32 ? static_cast<void*>(static_cast<float*>(a.out) + obase)
@@ -460,9 +460,11 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
       y[2 * p + 1] = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
     }
     stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
-    if constexpr (PART) {  // the stored bf16 values (8 B) into position n's row of the idle staging buffer
+    if constexpr (PART) {
+      // the stored bf16 values (8 B) over this lane's own residual slot of the LDS image, which no other
+      // thread reads: no barrier between the FFT and the epilogue (one before the sweep below)
       const int n = k1 + kA * k2;
-      *reinterpret_cast<uint2*>(smem + n * (kPitch * 4) + 8 * g) = make_uint2(bfpack(y[0], y[1]), bfpack(y[2], y[3]));
+      reinterpret_cast<uint2*>(dimg)[n * kG + g] = make_uint2(bfpack(y[0], y[1]), bfpack(y[2], y[3]));
     }
     if constexpr (SPLIT) {
       // workgroup-uniform bases (o's first token) + 32-bit lane offsets: position n = k1 + 12 k2
@@ -519,7 +521,7 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
     __syncthreads();
     const int n = threadIdx.x;
     if (n < kL) {
-      const uint4* row = reinterpret_cast<const uint4*>(smem + n * (kPitch * 4));
+      const uint4* row = reinterpret_cast<const uint4*>(dimg + n * (kG * 8));
       const float sh = __uint_as_float(row[0].x << 16);
       float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
 #pragma unroll
