@@ -384,21 +384,21 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     barrier();
     if (wr == 1) barrier();  // stagger
   } else {
-  // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
-  stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
-  stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
-  stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
-  stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
-  if (KT > 1) {
-    stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane0, p, gb);
-    if constexpr (PERSIST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile 0 and R0(1) (see PERSIST)
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
-  } else {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  }
-  barrier();
-  read_a<0>(a0, smem, wr, lane0 & 15, lane0 >> 4);
-  if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
+    // ---- prologue: R0(0) R1(0) R2(0) R3(0) R0(1) = phases -5..-1
+    stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+    stage_region<1, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+    stage_region<2, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+    stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
+    if (KT > 1) {
+      stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, 1, smem + kStage, wave, lane0, p, gb);
+      if constexpr (PERSIST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile 0 and R0(1) (see PERSIST)
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // R0(0), R1(0) landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    barrier();
+    read_a<0>(a0, smem, wr, lane0 & 15, lane0 >> 4);
+    if (wr == 1) barrier();  // stagger: wave group 1 runs one barrier behind group 0
   }
   if constexpr (!PERSIST) GEMM_STAMP(2, __builtin_amdgcn_s_memtime());
 
