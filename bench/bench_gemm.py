@@ -52,6 +52,9 @@ def main(argv=None):
         # the bf16 block's forms (persistent variants under MI_DFT_GEMM_PERSIST=1)
         "fc1_gelu amd LN": lambda: ops.linear_ln(x, w1, c1_b, b1, st_b, 1),
         "fc2 amd (+res)": lambda: ops.linear(h, w2, b2, 0, rb),
+        # the model's fc2: bias pending into the next block, + the next LN's partial statistics
+        "fc2 amd (+res, no bias)": lambda: ops.linear(h, w2, None, 0, rb),
+        "fc2 amd (+res, stats)": lambda: ops.linear_stats(h, w2, rb, b2),
     }
     if a.x3:
         # full fp32 operands (non-zero lo halves, as the model's activations and weights have)
