@@ -723,13 +723,19 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                   if constexpr (STATS && !PERSIST) {
                     // the STORED (bf16-rounded) values + pre back into the two staging slots: the
                     // statistics describe exactly the tensor the next LayerNorm reads
+                    // (the stored words pinned: unpacked as stored, not re-converted from v; + pre as
+                    // packed adds)
+                    uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+                    asm volatile("" : "+v"(ws[0]), "+v"(ws[1]), "+v"(ws[2]), "+v"(ws[3]));
+                    const gelu_f2 pp[4] = {{spre.x, spre.y}, {spre.z, spre.w}, {spre2.x, spre2.y}, {spre2.z, spre2.w}};
+                    gelu_f2 sv[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                      sv[k] = gelu_f2{__uint_as_float(ws[k] << 16), __uint_as_float(ws[k] & 0xffff0000u)} + pp[k];
                     char* rw = const_cast<char*>(rp);
-                    *reinterpret_cast<float4*>(rw + (((fl >> 2) ^ (row & 15)) << 4)) =
-                        make_float4(__uint_as_float(w.x << 16) + spre.x, __uint_as_float(w.x & 0xffff0000u) + spre.y,
-                                    __uint_as_float(w.y << 16) + spre.z, __uint_as_float(w.y & 0xffff0000u) + spre.w);
+                    *reinterpret_cast<float4*>(rw + (((fl >> 2) ^ (row & 15)) << 4)) = make_float4(sv[0].x, sv[0].y, sv[1].x, sv[1].y);
                     *reinterpret_cast<float4*>(rw + ((((fl >> 2) + 1) ^ (row & 15)) << 4)) =
-                        make_float4(__uint_as_float(w.z << 16) + spre2.x, __uint_as_float(w.z & 0xffff0000u) + spre2.y,
-                                    __uint_as_float(w.w << 16) + spre2.z, __uint_as_float(w.w & 0xffff0000u) + spre2.w);
+                        make_float4(sv[2].x, sv[2].y, sv[3].x, sv[3].y);
                   }
                 } else {  // split pair: hi = bf16(v), lo = bf16(v - hi), both stored by this lane
                   uint4 lw;
@@ -755,16 +761,22 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             // M2 = S2 - S1^2 / 64 cancellation stays at a few std): no cross-lane reductions
             // (~45 VALU per pass as 16-lane DPP row sums: 9.6k cycles per tile, profiles/phases_r4.txt)
             const char* rl = reg + lane * 256;
+            // (pairs as packed VALU: one v_pk_add / v_pk_fma per two values)
             const f32x4 q0 = *reinterpret_cast<const f32x4*>(rl + ((0 ^ (lane & 15)) << 4));
             const float sh = q0[0];
-            f32x4 s1 = q0 - sh, s2 = s1 * s1;
+            const gelu_f2 shv = {sh, sh};
+            gelu_f2 s1a = gelu_f2{q0[0], q0[1]} - shv, s1b = gelu_f2{q0[2], q0[3]} - shv;
+            gelu_f2 s2a = s1a * s1a, s2b = s1b * s1b;
 #pragma unroll
             for (int ch = 1; ch < 16; ++ch) {
-              const f32x4 d = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4)) - sh;
-              s1 += d;
-              s2 += d * d;
+              const f32x4 q = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4));
+              const gelu_f2 d0 = gelu_f2{q[0], q[1]} - shv, d1 = gelu_f2{q[2], q[3]} - shv;
+              s1a += d0;
+              s1b += d1;
+              s2a = __builtin_elementwise_fma(d0, d0, s2a);
+              s2b = __builtin_elementwise_fma(d1, d1, s2b);
             }
-            const float t1 = (s1[0] + s1[1]) + (s1[2] + s1[3]), t2 = (s2[0] + s2[1]) + (s2[2] + s2[3]);
+            const float t1 = (s1a.x + s1a.y) + (s1b.x + s1b.y), t2 = (s2a.x + s2a.y) + (s2b.x + s2b.y);
             const int t = min(tbase + lane, M - 1);  // rows >= M: bit-identical copies of row M - 1
             *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
                 make_float2(sh + t1 * (1.f / 64.f), fmaxf(t2 - t1 * t1 * (1.f / 64.f), 0.f));
