@@ -440,6 +440,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       else return *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p.residual) + res_off(i, j));
     };
 
+#ifndef GEMM_STATS_ABL
+#define GEMM_STATS_ABL 0  // timing-only (wrong partials): bit 0 = no per-row sweep, bit 1 = no partials store,
+#endif                    // bit 2 = no write-back of the stored values into the staging slots
 #ifndef GEMM_ABLATE
 #define GEMM_ABLATE 0  // timing-only: bit 0 = no main-loop DMA, bit 1 = no main-loop fragment reads,
 #endif                 // bit 2 = epilogue computes but skips its stores
@@ -720,7 +723,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
                 uint4 w = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
                 if constexpr (OUT == 0) {
                   *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p.y) + static_cast<int64_t>(t) * N + fh + fl) = w;
-                  if constexpr (STATS && !PERSIST) {
+                  if constexpr (STATS && !PERSIST && !(GEMM_STATS_ABL & 4)) {
                     // the STORED (bf16-rounded) values + pre back into the two staging slots: the
                     // statistics describe exactly the tensor the next LayerNorm reads
                     // (the stored words pinned: unpacked as stored, not re-converted from v; + pre as
@@ -768,7 +771,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             gelu_f2 s1a = gelu_f2{q0[0], q0[1]} - shv, s1b = gelu_f2{q0[2], q0[3]} - shv;
             gelu_f2 s2a = s1a * s1a, s2b = s1b * s1b;
 #pragma unroll
-            for (int ch = 1; ch < 16; ++ch) {
+            for (int ch = 1; ch < ((GEMM_STATS_ABL & 1) ? 1 : 16); ++ch) {
               const f32x4 q = *reinterpret_cast<const f32x4*>(rl + ((ch ^ (lane & 15)) << 4));
               const gelu_f2 d0 = gelu_f2{q[0], q[1]} - shv, d1 = gelu_f2{q[2], q[3]} - shv;
               s1a += d0;
@@ -778,6 +781,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
             }
             const float t1 = (s1a.x + s1a.y) + (s1b.x + s1b.y), t2 = (s2a.x + s2a.y) + (s2b.x + s2b.y);
             const int t = min(tbase + lane, M - 1);  // rows >= M: bit-identical copies of row M - 1
+            if (!(GEMM_STATS_ABL & 2) || t1 == 1234.5f)
             *reinterpret_cast<float2*>(p.stats_part + (static_cast<int64_t>(t) * (N / 64) + fh / 64) * 2) =
                 make_float2(sh + t1 * (1.f / 64.f), fmaxf(t2 - t1 * t1 * (1.f / 64.f), 0.f));
           }
