@@ -246,11 +246,16 @@ __device__ __forceinline__ void epi_act(const f32x4& a4, const float4& bias, con
   v[0] = gelu_f2{a4[0], a4[1]};
   v[1] = gelu_f2{a4[2], a4[3]};
   if constexpr (LN) {
-    v[0] = gelu_f2(st.y) * __builtin_elementwise_fma(gelu_f2(-st.x), gelu_f2{c1.x, c1.y}, v[0]);
-    v[1] = gelu_f2(st.y) * __builtin_elementwise_fma(gelu_f2(-st.x), gelu_f2{c1.z, c1.w}, v[1]);
+    // rstd (acc - mean c1) + bias = rstd acc + (bias - rstd mean c1): two packed FMAs per pair
+    // (st.x = -rstd * mean, st.y = rstd: the per-token operands folded once by the caller)
+    v[0] = __builtin_elementwise_fma(gelu_f2(st.y), v[0],
+                                     __builtin_elementwise_fma(gelu_f2(st.x), gelu_f2{c1.x, c1.y}, gelu_f2{bias.x, bias.y}));
+    v[1] = __builtin_elementwise_fma(gelu_f2(st.y), v[1],
+                                     __builtin_elementwise_fma(gelu_f2(st.x), gelu_f2{c1.z, c1.w}, gelu_f2{bias.z, bias.w}));
+  } else {
+    v[0] += gelu_f2{bias.x, bias.y};
+    v[1] += gelu_f2{bias.z, bias.w};
   }
-  v[0] += gelu_f2{bias.x, bias.y};
-  v[1] += gelu_f2{bias.z, bias.w};
   if constexpr (ACT == 1) {
     v[0] = gelu_erf2(v[0]);
     v[1] = gelu_erf2(v[1]);
@@ -557,8 +562,10 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     }
     float2 lst[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) {
       lst[j] = LN ? *reinterpret_cast<const float2*>(p.ln_stats + 2 * static_cast<int64_t>(tokc(j))) : make_float2(0.f, 1.f);
+      lst[j].x = -lst[j].x * lst[j].y;  // (mean, rstd) -> (-rstd mean, rstd), epi_act's operands
+    }
     if constexpr (MODE != 2) {  // token-major outputs (MODE 1 only gathers its B operand differently)
       if (PERSIST || !p.direct_epi) {
         // ---- LDS-staged epilogue (token-major outputs).  Writing straight from the MFMA layout
