@@ -54,6 +54,17 @@ def test_engine_execute_v2_host_pointers_cpu():
     assert torch.allclose(y, torch.view_as_real(torch.fft.rfft2(x)), atol=1e-5)
 
 
+def test_engine_execute_v2_copy_path_cpu():
+    """No hipGraph on the CPU: caller buffers always go through the engine's bindings (counted)."""
+    x = torch.randn(1, 1, 4, 8)
+    eng = Engine.build(Rfft2Model(), (x,), device="cpu")
+    y = torch.empty(1, 1, 4, 5, 2)
+    for _ in range(3):
+        assert eng.execute_v2([x, y])
+    assert eng.bound_stats == {"copies": 3, "captures": 0, "replays": 0, "evictions": 0}
+    assert torch.allclose(y, torch.view_as_real(torch.fft.rfft2(x)), atol=1e-5)
+
+
 def test_engine_execute_v2_own_bindings_zero_copy_cpu():
     """Bindings that are the engine's own buffers run in place (TensorRT-style preallocated
     bindings); execute_async_v2 returns without waiting."""
@@ -117,6 +128,35 @@ def test_engine_hipgraph_gpu(device, tmp_path):
     assert torch.allclose(eng2.binding_tensors[1].cpu(), 0.5 * x, atol=1e-5)
     st = eng2.benchmark(iterations=20, warmup=2)
     assert st["latency_median_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_engine_execute_v2_bound_graphs_gpu(device):
+    """Caller-owned device pointers: copied through the engine buffers on first use, then a graph
+    captured on exactly those pointers (inputs read in place) is replayed; new data in the same
+    buffers is picked up, LRU eviction past BOUND_GRAPH_MAX, results equal torch.fft throughout."""
+    torch.manual_seed(3)
+    eng = Engine.build(Rfft2Model(), (torch.randn(2, 3, 720, 1440),), device=device)
+    eng.BOUND_GRAPH_MAX = 2
+    bufs = [(torch.empty(2, 3, 720, 1440, device=device), torch.empty(2, 3, 720, 721, 2, device=device))
+            for _ in range(3)]
+    for rnd in range(3):
+        for x, y in bufs:
+            x.copy_(torch.randn(2, 3, 720, 1440))
+            y.fill_(float("nan"))
+            assert eng.execute_v2([x.data_ptr(), y.data_ptr()])
+            ref = torch.view_as_real(torch.fft.rfft2(x.cpu().double()))
+            err = ((y.cpu().double() - ref.double()).norm() / ref.double().norm()).item()
+            assert err < 1e-6, (rnd, err)
+    st = dict(eng.bound_stats)
+    print("bound-graph stats", st)
+    # round 0: 3 copies; round 1: 3 captures + replays (the third evicts buffer 0's graph); round 2:
+    # buffer 0 is counted again (a copy), buffers 1 and 2 replay
+    assert st == {"copies": 4, "captures": 3, "evictions": 1, "replays": 5}
+    own_in, own_out = eng.binding_tensors
+    own_in.copy_(bufs[0][0])
+    eng.execute_v2(eng.binding_ptrs())  # the engine's own buffers: the main graph, no bookkeeping
+    assert torch.equal(own_out, bufs[0][1]) and eng.bound_stats == st
 
 
 @pytest.mark.gpu
