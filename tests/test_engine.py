@@ -65,6 +65,47 @@ def test_engine_execute_v2_copy_path_cpu():
     assert torch.allclose(y, torch.view_as_real(torch.fft.rfft2(x)), atol=1e-5)
 
 
+def test_engine_bound_graph_bookkeeping_cpu(monkeypatch):
+    """The pointer-set bookkeeping of execute_async_v2 (bind on second use, LRU eviction, raw-pointer
+    hot path, the engine's own buffers untouched) with a stand-in for the captured graph that runs
+    the model eagerly on the bound views -- the GPU test covers the real capture."""
+    x = torch.randn(1, 1, 4, 8)
+    eng = Engine.build(Rfft2Model(), (x,), device="cpu")
+
+    class FakeMain:  # "a main graph exists": replays the model on the engine's own buffers
+        def replay(self):
+            (o,) = eng.graph.run(eng.static_inputs[0])
+            eng.static_outputs[0].copy_(o)
+
+    eng._cuda_graph = FakeMain()
+
+    class FakeGraph:
+        def __init__(self, views):
+            self.views, self.replays = views, 0
+
+        def replay(self):
+            self.replays += 1
+            (o,) = eng.graph.run(self.views[0])
+            self.views[1].copy_(o)
+
+    monkeypatch.setattr(eng, "_capture_bound", lambda views: FakeGraph(views))
+    eng.BOUND_GRAPH_MAX = 2
+    bufs = [(torch.randn(1, 1, 4, 8), torch.empty(1, 1, 4, 5, 2)) for _ in range(3)]
+    for _ in range(2):
+        for xb, yb in bufs:
+            assert eng.execute_async_v2([xb.data_ptr(), yb.data_ptr()])
+            assert torch.allclose(yb, torch.view_as_real(torch.fft.rfft2(xb)), atol=1e-5)
+    assert eng.bound_stats == {"copies": 3, "captures": 3, "replays": 3, "evictions": 1}
+    assert len(eng._bound) == 2 and (bufs[0][0].data_ptr(), bufs[0][1].data_ptr()) not in eng._bound
+    xb, yb = bufs[2]
+    xb.copy_(torch.randn(1, 1, 4, 8))
+    eng.execute_async_v2([xb.data_ptr(), yb.data_ptr()])  # hot path: raw pointers of a bound set
+    assert eng.bound_stats["replays"] == 4
+    assert torch.allclose(yb, torch.view_as_real(torch.fft.rfft2(xb)), atol=1e-5)
+    eng.execute_async_v2([torch.randn(1, 1, 4, 8), torch.empty(1, 1, 4, 5, 4)[..., :2]])  # strided: copy path
+    assert eng.bound_stats["copies"] == 4
+
+
 def test_engine_execute_v2_own_bindings_zero_copy_cpu():
     """Bindings that are the engine's own buffers run in place (TensorRT-style preallocated
     bindings); execute_async_v2 returns without waiting."""
