@@ -131,9 +131,38 @@ def _build_info_obj(obj_dir: str, digest: str) -> str:
     return obj
 
 
-def _headers_mtime() -> float:
-    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
-    return max([os.path.getmtime(h) for h in hs] + [0.0])
+def _headers_digest() -> str:
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+        h.update(os.path.relpath(f, CSRC).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _object_key(src: str, needs_torch: bool, asan: bool, hdr_digest: str) -> str:
+    """What an object was compiled from: the source's content, every header's content and the
+    compile configuration.  Stored next to the object (``.o.key``); an object is reused only when
+    its key matches (file times are not trusted: a snapshot or ``cp -p`` can restore older source
+    times over newer objects)."""
+    h = hashlib.sha256()
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    h.update(f"|{hdr_digest}|{ARCH}|{_FLAGS_VERSION}|{needs_torch}|{asan}|{os.environ.get('MI_DFT_HIPCC_EXTRA', '')}|"
+             f"{os.environ.get('MI_DFT_DEVICE_CHECKS', '0')}".encode())
+    return h.hexdigest()
+
+
+def _key_path(obj: str) -> str:
+    return obj + ".key"
+
+
+def _read_key(obj: str) -> str | None:
+    try:
+        with open(_key_path(obj)) as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def _obj_path(src: str, asan: bool = False, obj_dir: str | None = None) -> str:
@@ -205,12 +234,14 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
     if not (force or from_source) and embedded_digest(lib) == digest:
         return lib  # up to date with exactly these sources
     tinc, tlib, abi = _torch_paths()
-    hdr = _headers_mtime()
+    hdr = _headers_digest()
     srcs = sources()
     todo = []
+    keys = {}
     for src, nt in srcs:
         obj = _obj_path(src, asan, obj_dir)
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
+        keys[src] = _object_key(src, nt, asan and not src.endswith(".hip"), hdr)
+        if force or not os.path.exists(obj) or _read_key(obj) != keys[src]:
             todo.append((src, nt))
     jobs = jobs or max(1, min(int(os.environ.get("MAX_JOBS", "8") or 8), os.cpu_count() or 4, 16))
     t0 = time.time()
@@ -221,11 +252,15 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True, as
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             futs = {ex.submit(_compile, s, nt, tinc, abi, asan, obj_dir): s for s, nt in todo}
             for f in cf.as_completed(futs):
-                f.result()
+                obj = f.result()
+                with open(_key_path(obj), "w") as kf:
+                    kf.write(keys[futs[f]] + "\n")
                 if verbose:
                     print("  built", os.path.relpath(futs[f], ROOT), flush=True)
     objs = [_obj_path(s, asan, obj_dir) for s, _ in srcs]
-    if True:  # digest mismatch, --force or from_source: always relink (with a fresh provenance record)
+    # digest mismatch, --force or from_source: always relink (with a fresh provenance record); every
+    # object's key was checked against its source above, so the stamped digest is true
+    if True:
         objs = objs + [_build_info_obj(obj_dir or (BUILD_ASAN if asan else BUILD), digest)]
         tmp = lib + ".tmp"
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + [

@@ -41,6 +41,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--noCudaGraph", action="store_true", help="run eagerly instead of replaying a hipGraph")
     ap.add_argument("--device", default=None)
     ap.add_argument("--exportTimes", help="write the timing summary as JSON")
+    ap.add_argument("--noOptimize", action="store_true",
+                    help="build without the graph rewrite pass (stock nodes run one by one; comparator)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -59,14 +61,21 @@ def main(argv: Optional[List[str]] = None) -> int:
         print(f"[dftexec] loaded engine {a.loadEngine} (arch {eng.header.arch}, format {eng.header.format_version})")
     elif a.onnx:
         shapes = _parse_shapes(a.shapes)
-        from ..onnx.runner import OnnxGraph
+        from .engine import graph_inputs
 
-        g = OnnxGraph(open(a.onnx, "rb").read(), device="cpu")
+        ins = graph_inputs(open(a.onnx, "rb").read())
         in_shapes = None
         if shapes is not None:
-            in_shapes = [shapes.get(n, s) for n, s in zip(g.input_names, g.input_shapes)]
-        eng = Engine.build(a.onnx, shapes=in_shapes, device=device, use_graph=not a.noCudaGraph)
+            in_shapes = [shapes.get(n, s) for n, s, _ in ins]
+        eng = Engine.build(a.onnx, shapes=in_shapes, device=device, use_graph=not a.noCudaGraph,
+                           optimize=not a.noOptimize)
         print(f"[dftexec] built engine from {a.onnx}")
+        opt = eng.header.extra.get("optimizer")
+        if opt is not None:
+            print(f"[dftexec] graph optimizer: {opt['nodes_before']} -> {opt['nodes_after']} nodes, "
+                  f"rewrites {opt['applied']} ({opt['seconds']} s)")
+            for r in opt["rejected"] if a.verbose else []:
+                print(f"[dftexec]   kept {r['pattern']} at {r['at']}: {r['why']}")
     else:
         ap.error("one of --onnx or --loadEngine is required")
         return 2

@@ -78,6 +78,20 @@ class EngineHeader:
         return cls(**d)
 
 
+def graph_inputs(onnx_bytes: bytes) -> List[tuple]:
+    """(name, shape (-1 = dynamic), dtype) of a model's non-initializer inputs, from the proto only."""
+    m = P.load_model(onnx_bytes)
+    inits = {t.name for t in m.graph.initializer}
+    out = []
+    for i in m.graph.input:
+        if i.name in inits:
+            continue
+        tt = i.type.tensor_type
+        out.append((i.name, [d.dim_value if d.HasField("dim_value") else -1 for d in tt.shape.dim],
+                    P.onnx_dtype_to_torch(tt.elem_type) if tt.elem_type else torch.float32))
+    return out
+
+
 def _device_arch(device: torch.device) -> str:
     if device.type == "cuda" and torch.cuda.is_available():
         return getattr(torch.cuda.get_device_properties(device), "gcnArchName", "unknown")
@@ -93,10 +107,30 @@ class Engine:
 
     def __init__(self, onnx_bytes: bytes, input_shapes: Sequence[Sequence[int]],
                  input_dtypes: Optional[Sequence[torch.dtype]] = None, device: Optional[torch.device] = None,
-                 use_graph: bool = True, warmup: int = 2, header: Optional[EngineHeader] = None):
+                 use_graph: bool = True, warmup: int = 2, header: Optional[EngineHeader] = None,
+                 optimize: bool = True):
         load_plugins()
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        opt_info = None
+        if optimize and header is None:
+            # build-time graph rewrite (TensorRT's layer fusion step): stock spectral / LayerNorm /
+            # MLP patterns -> this library's kernels, each rewrite verified on the build device
+            from ..onnx.optimizer import optimize as _optimize
+
+            t0 = time.perf_counter()
+            shp = [list(map(int, s)) for s in input_shapes]
+            onnx_bytes, rep = _optimize(onnx_bytes, shp, input_dtypes, self.device)
+            counts: Dict[str, int] = {}
+            for a in rep.applied:
+                counts[a["pattern"]] = counts.get(a["pattern"], 0) + 1
+            opt_info = {"applied": counts, "rejected": rep.rejected, "nodes_before": rep.nodes_before,
+                        "nodes_after": rep.nodes_after, "seconds": round(time.perf_counter() - t0, 2)}
+            self.optimize_report = rep
+            if rep.applied:
+                _log.info("graph optimizer: %s (%d -> %d nodes)", counts, rep.nodes_before, rep.nodes_after)
+            for r in rep.rejected:
+                _log.info("graph optimizer: kept %s at %s: %s", r["pattern"], r["at"], r["why"])
         self.onnx_bytes = onnx_bytes
         self.graph = OnnxGraph(onnx_bytes, self.device)
         if len(input_shapes) != len(self.graph.input_names):
@@ -125,6 +159,8 @@ class Engine:
             # plans and graphs are rebuilt on load, so this is informational, not an error
             _log.warning("engine was built for %s, running on %s", built_for, self.header.arch)
         self.header.use_graph = self.use_graph
+        if opt_info is not None:
+            self.header.extra["optimizer"] = opt_info
         self.header.bindings = (
             [Binding(n, s, _dtype_name(t.dtype), True)
              for n, s, t in zip(self.graph.input_names, self.input_shapes, self.static_inputs)]
@@ -135,8 +171,10 @@ class Engine:
     @classmethod
     def build(cls, source: Union[torch.nn.Module, bytes, str], inputs: Optional[Sequence[torch.Tensor]] = None,
               shapes: Optional[Sequence[Sequence[int]]] = None, *, device=None, use_graph: bool = True,
-              opset_version: int = onnx_export.DEFAULT_OPSET, dtypes=None) -> "Engine":
-        """Build from an ``nn.Module`` (exported to ONNX with ``inputs``), ONNX bytes or a path."""
+              opset_version: int = onnx_export.DEFAULT_OPSET, dtypes=None, optimize: bool = True) -> "Engine":
+        """Build from an ``nn.Module`` (exported to ONNX with ``inputs``), ONNX bytes or a path.
+        ``optimize``: run the build-time graph rewrite (``onnx/optimizer.py``) that maps stock
+        spectral / LayerNorm / MLP patterns onto the hand kernels (default on; off = node-by-node)."""
         if isinstance(source, torch.nn.Module):
             if inputs is None:
                 raise ValueError("building from a module needs example inputs")
@@ -151,11 +189,12 @@ class Engine:
         else:
             onnx_bytes = open(source, "rb").read() if isinstance(source, str) else bytes(source)
             if shapes is None:
-                g = OnnxGraph(onnx_bytes, device="cpu")
-                shapes = g.input_shapes
+                shapes = [s for _, s, _ in graph_inputs(onnx_bytes)]
                 if any(d < 0 for s in shapes for d in s):
                     raise ValueError(f"model has dynamic input dims {shapes}: pass shapes= (trtexec --shapes)")
-        return cls(onnx_bytes, shapes, dtypes, device=device, use_graph=use_graph)
+            if dtypes is None:
+                dtypes = [d for _, _, d in graph_inputs(onnx_bytes)]
+        return cls(onnx_bytes, shapes, dtypes, device=device, use_graph=use_graph, optimize=optimize)
 
     # ------------------------------------------------------------------ execution
     def _run_eager(self) -> List[torch.Tensor]:

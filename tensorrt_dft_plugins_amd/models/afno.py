@@ -13,6 +13,11 @@ slicing), softshrink(0.01), irfft2, + the filter input.
 
 Backends:
 * ``"torch"``  -- plain PyTorch (torch.fft, einsum): the numerics oracle and eager comparator.
+* ``"contrib"`` -- the same network written the reference's way: the FFTs are the ONNX-contrib
+  ``OnnxRfft2`` / ``OnnxIrfft2`` Functions (/root/reference/tests/test_dft.py:35-60) around a
+  channel-last permute, so it exports to a stock ONNX graph (Rfft / Irfft + einsums, LayerNorms,
+  MatMuls) that the engine's build-time rewrite pass (``onnx/optimizer.py``) maps onto the hand
+  kernels.
 * ``"amd"``    -- MI355X path: pruned hand-written FFTs (only kept modes are computed),
   fused spectral-MLP kernel (MFMA), fused LayerNorm, bf16 GEMMs.
 """
@@ -82,6 +87,34 @@ def afno2d_reference(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_thr
     return x.type(dtype) + bias
 
 
+def afno2d_contrib(x, w1, b1, w2, b2, num_blocks, sparsity_threshold, hard_thresholding_fraction):
+    """FourCastNet AFNO2D with the ONNX-contrib DFT ops (exportable the reference's way).
+
+    ``Rfft`` / ``Irfft`` transform the LAST two dims with the "backward" norm (the contrib
+    contract), so the channel-last tokens are permuted to [B, C, H, W] around them and the ortho
+    scales are explicit multiplies; the kept-mode window is sliced out, run through the
+    block-diagonal complex MLP as real/imaginary einsums, softshrunk and zero-padded back."""
+    from ..onnx.exporter import OnnxIrfft2, OnnxRfft2
+
+    bias = x
+    B, H, W, C = (int(d) for d in x.shape)
+    nb = int(num_blocks)
+    bs = C // nb
+    wf = W // 2 + 1
+    r0, r1, km = kept_window(H, W, hard_thresholding_fraction)
+    X = OnnxRfft2.apply(x.float().permute(0, 3, 1, 2)) * (1.0 / math.sqrt(H * W))  # [B, C, H, wf, 2], ortho
+    X = X.permute(0, 2, 3, 1, 4)[:, r0:r1, :km].reshape(B, r1 - r0, km, nb, bs, 2)
+    xr, xi = X[..., 0], X[..., 1]
+    o1r = F.relu(torch.einsum("...bi,bio->...bo", xr, w1[0]) - torch.einsum("...bi,bio->...bo", xi, w1[1]) + b1[0])
+    o1i = F.relu(torch.einsum("...bi,bio->...bo", xi, w1[0]) + torch.einsum("...bi,bio->...bo", xr, w1[1]) + b1[1])
+    o2r = torch.einsum("...bi,bio->...bo", o1r, w2[0]) - torch.einsum("...bi,bio->...bo", o1i, w2[1]) + b2[0]
+    o2i = torch.einsum("...bi,bio->...bo", o1i, w2[0]) + torch.einsum("...bi,bio->...bo", o1r, w2[1]) + b2[1]
+    o2 = F.softshrink(torch.stack([o2r, o2i], dim=-1), lambd=sparsity_threshold).reshape(B, r1 - r0, km, C, 2)
+    o2 = F.pad(o2, (0, 0, 0, 0, 0, wf - km, r0, H - r1))  # zero modes outside the window
+    y = OnnxIrfft2.apply(o2.permute(0, 3, 1, 2, 4)) * math.sqrt(H * W)  # Irfft is 1/N: ortho = x sqrt(N)
+    return y.permute(0, 2, 3, 1).to(x.dtype) + bias
+
+
 def kept_window(H: int, W: int, fraction: float) -> Tuple[int, int, int]:
     """(row_start, row_stop, kept_w_modes) of FourCastNet's mode slicing."""
     total = H // 2 + 1
@@ -106,6 +139,9 @@ class AFNO2D(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         c = self.cfg
+        if self.backend == "contrib":
+            return afno2d_contrib(x, self.w1, self.b1, self.w2, self.b2, c.num_blocks, c.sparsity_threshold,
+                                  c.hard_thresholding_fraction)
         if self.backend == "torch":
             return afno2d_reference(x, self.w1, self.b1, self.w2, self.b2, c.num_blocks, c.sparsity_threshold,
                                     c.hard_thresholding_fraction)

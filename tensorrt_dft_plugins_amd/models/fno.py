@@ -16,7 +16,10 @@ kernels per stage, and the full-resolution spectral output is never written to H
      along W on MFMA fused with the 1x1 convolution, bias and GELU
      (``csrc/spectral/fno_c2r_pw.hip``) -- reads x, writes y, nothing else.
 
-Backends: ``"torch"`` (torch.fft + einsum + conv2d, the numerics oracle) and ``"amd"``.
+Backends: ``"torch"`` (torch.fft + einsum + conv2d, the numerics oracle), ``"contrib"`` (the same
+layer written the reference's way: ONNX-contrib ``OnnxRfft2`` / ``OnnxIrfft2`` + real/imaginary
+einsums + zero padding, /root/reference/tests/test_dft.py:35-60, exportable to a stock ONNX graph
+that the engine's rewrite pass maps back onto the kernels below) and ``"amd"``.
 """
 from __future__ import annotations
 
@@ -30,7 +33,7 @@ import torch.nn.functional as F
 from ..ops import dft as D
 from ..ops import spectral as S
 
-__all__ = ["FNOConfig", "SpectralConv2d", "FNOBlock", "FNO2d", "spectral_conv2d_reference"]
+__all__ = ["FNOConfig", "SpectralConv2d", "FNOBlock", "FNO2d", "spectral_conv2d_reference", "spectral_conv2d_contrib"]
 
 
 @dataclass
@@ -61,6 +64,27 @@ def spectral_conv2d_reference(x: torch.Tensor, weight: torch.Tensor, m1: int, m2
     return torch.fft.irfft2(out, s=(H, W))
 
 
+def spectral_conv2d_contrib(x: torch.Tensor, weight: torch.Tensor, m1: int, m2: int) -> torch.Tensor:
+    """Classic FNO SpectralConv2d with the ONNX-contrib DFT ops: Rfft -> two mode windows ->
+    complex channel mixing as real einsums -> zero padding -> Irfft (all "backward" norm)."""
+    from ..onnx.exporter import OnnxIrfft2, OnnxRfft2
+
+    B, _, H, W = (int(d) for d in x.shape)
+    wf = W // 2 + 1
+    X = OnnxRfft2.apply(x.float())  # [B, Cin, H, wf, 2]
+    wr, wi = weight[..., 0].float(), weight[..., 1].float()
+
+    def mix(xs, lo, hi):
+        a, b = xs[..., 0], xs[..., 1]
+        re = torch.einsum("bixy,ioxy->boxy", a, wr[:, :, lo:hi]) - torch.einsum("bixy,ioxy->boxy", b, wi[:, :, lo:hi])
+        im = torch.einsum("bixy,ioxy->boxy", a, wi[:, :, lo:hi]) + torch.einsum("bixy,ioxy->boxy", b, wr[:, :, lo:hi])
+        return torch.stack([re, im], dim=-1)
+
+    top = F.pad(mix(X[:, :, :m1, :m2], 0, m1), (0, 0, 0, wf - m2, 0, H - m1))
+    bot = F.pad(mix(X[:, :, H - m1:, :m2], m1, 2 * m1), (0, 0, 0, wf - m2, H - m1, 0))
+    return OnnxIrfft2.apply(top + bot)
+
+
 class SpectralConv2d(nn.Module):
     def __init__(self, in_ch: int, out_ch: int, modes1: int, modes2: int, backend: str = "torch"):
         super().__init__()
@@ -80,6 +104,8 @@ class SpectralConv2d(nn.Module):
         m1, m2 = self.modes1, self.modes2
         if self.backend == "torch":
             return spectral_conv2d_reference(x, self.weight, m1, m2)
+        if self.backend == "contrib":
+            return spectral_conv2d_contrib(x, self.weight, m1, m2)
         keep = [(m1, m1), (m2, 0)]
         xm = D.rfftn_pruned(x, [2, 3], keep)  # [B, Cin, 2*m1, m2, 2] fp32
         ym = S.fno_spectral_mix(xm.reshape(B, C, 2 * m1 * m2, 2), self._packed_weight())

@@ -351,19 +351,29 @@ def _slice(attrs, x, starts=None, ends=None, axes=None, steps=None):
     axes = attrs.get("axes", list(range(len(starts)))) if axes is None else _ints(axes)
     steps = [1] * len(starts) if steps is None else _ints(steps)
     idx = [slice(None)] * x.dim()
+    rev = []
     for s, e, a, st in zip(starts, ends, axes, steps):
         n = x.shape[a]
         if st < 0:
-            raise NotImplementedError("negative Slice steps")
+            # ONNX: start clamped to [0, n-1], end to [-1, n-1], walking down (e.g. torch's F.pad
+            # export reverses its pads list this way)
+            s = max(0, min(n - 1, s + n if s < 0 else s))
+            e = max(-1, min(n - 1, e + n if e < -1 else e)) if e >= -n else -1
+            rev.append((a % x.dim(), list(range(s, e, st))))
+            continue
         s = max(0, min(n, s + n if s < 0 else s))
         e = max(0, min(n, e + n if e < 0 else e))
         idx[a % x.dim()] = slice(s, e, st)
-    return x[tuple(idx)]
+    x = x[tuple(idx)]
+    for a, ix in rev:
+        x = torch.index_select(x, a, torch.tensor(ix, dtype=torch.long, device=x.device))
+    return x
 
 
 @op("Gather")
 def _gather(attrs, x, idx):
     axis = attrs.get("axis", 0) % x.dim()
+    ishape = list(idx.shape)  # a 0-d index drops the axis (kept even when moved to the device as [1])
     if _is_host(idx) and not _is_host(x):
         idx = _to_dev(idx, x.device) if idx.dim() else idx.reshape(1).to(x.device)
     if _is_host(x) and not _is_host(idx):
@@ -371,7 +381,30 @@ def _gather(attrs, x, idx):
     n = x.shape[axis]
     idx = torch.where(idx < 0, idx + n, idx)
     out = torch.index_select(x, axis, idx.reshape(-1))
-    return out.reshape(list(x.shape[:axis]) + list(idx.shape) + list(x.shape[axis + 1:]))
+    return out.reshape(list(x.shape[:axis]) + ishape + list(x.shape[axis + 1:]))
+
+
+@op("ScatterND")
+def _scatter_nd(attrs, x, idx, upd):
+    """ONNX ScatterND (torch exports in-place slice assignment, e.g. the classic FNO's
+    ``out_ft[:, :, :m1, :m2] = ...``, this way)."""
+    if _is_host(idx) and not _is_host(x):
+        idx = idx.to(x.device)
+    if _is_host(upd) and not _is_host(x):
+        upd = _to_dev(upd, x.device)
+    k = idx.shape[-1]
+    key = tuple(idx[..., i].long() for i in range(k))
+    red = attrs.get("reduction", "none")
+    out = x.clone()
+    if red == "none":
+        out[key] = upd.to(out.dtype)
+    elif red == "add":
+        out.index_put_(key, upd.to(out.dtype), accumulate=True)
+    elif red == "mul":
+        out[key] = out[key] * upd.to(out.dtype)
+    else:
+        raise NotImplementedError(f"ScatterND reduction {red}")
+    return out
 
 
 @op("Expand")
