@@ -65,6 +65,9 @@ def rccl_choices(text: str) -> dict:
     if rings:
         out["ring_channels"] = int(rings[0][1])
         out["ring0"] = rings[0][2].strip()
+    nr = sorted({int(v) for v in re.findall(r"\bnranks (\d+)", text)})
+    if nr:
+        out["nranks"] = nr[0] if len(nr) == 1 else nr
     m = re.search(r"[RN]CCL version ([\d.]+\S*)", text)
     if m:
         out["version"] = m.group(1)
@@ -182,6 +185,8 @@ def run_steps(runner, steps: int, warmup: int, world: int, dev, cuda: bool) -> f
     sync()
     barrier()
     sync()
+    if world > 1 and hasattr(runner, "time_comm"):
+        runner.time_comm(True)  # event pair around each timed gather (comm-stream busy time)
     t0 = time.perf_counter()
     for _ in range(steps):
         runner.step()
@@ -235,23 +240,60 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None):
     return info, runner
 
 
+def multi_gpu_diagnostics(runner, steps: int, world: int, dev, cuda: bool) -> dict:
+    """Self-checks of a multi-GPU run: the rank count every collective actually spans (an all-reduce
+    of ones, which must equal WORLD_SIZE), the comm stream's busy time per timed step (gathers
+    only, not their wait for compute) and the cost of one gather with no compute in flight.
+    Times are the max over ranks."""
+    t = torch.ones(1, device=dev if cuda else "cpu")
+    dist.all_reduce(t)
+    ranks = int(round(float(t.item())))
+    if ranks != world:
+        raise SystemExit(f"collective spans {ranks} ranks, WORLD_SIZE is {world}")
+    busy = runner.comm_busy_ms()
+    g_only = runner.gather_only_ms(5)
+    vals = torch.tensor([busy / steps if busy is not None else -1.0, g_only if g_only is not None else -1.0],
+                        dtype=torch.float64, device=dev if cuda else "cpu")
+    dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+    out = {"collective_ranks": ranks}
+    if vals[0] >= 0:
+        out["comm_busy_ms_per_step"] = round(float(vals[0]), 3)
+    if vals[1] >= 0:
+        out["gather_only_ms"] = round(float(vals[1]), 3)
+    return out
+
+
 def _ensure_library(rank: int, world: int, cuda: bool) -> dict:
-    """The benchmarked library must be built from exactly these sources: check the digest the
-    library carries (tensorrt_dft_plugins_amd/_build.py) and rebuild here if it does not match
-    (local rank 0 builds, the others wait).  Recorded in the JSON line."""
+    """The benchmarked library must be compiled from exactly these sources ON THIS HOST (the
+    reference builds and tests in one command, /root/reference/build_with_docker.sh:39): rebuild
+    from source here when the library's embedded digest does not match the sources or when it was
+    linked on another host (local rank 0 builds, the others wait).  Recorded in the JSON line."""
+    import socket
+
     from tensorrt_dft_plugins_amd import _build
 
     st = _build.library_status()
-    rebuilt = False
-    if not st["digest_ok"] and not os.environ.get("MI_DFT_LIB"):
-        if int(os.environ.get("LOCAL_RANK", "0")) == 0:
-            log("native library does not match the sources: rebuilding from source")
-            _build.build(from_source=True)
-        rebuilt = True
-        if world > 1:
-            dist.barrier()
-        st = _build.library_status()
-    return {"source_digest_ok": st["digest_ok"], "rebuilt_here": rebuilt}
+    rebuilt, err = False, None
+    if not os.environ.get("MI_DFT_LIB"):
+        info = _build.embedded_info(st["path"]) or ""
+        other_host = f"host={socket.gethostname()} " not in info + " "
+        if (not st["digest_ok"] or (cuda and other_host)) and os.environ.get("MI_DFT_BENCH_BUILD", "1") != "0":
+            if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+                log("native library " + ("does not match the sources" if not st["digest_ok"] else
+                                         "was built on another host") + ": compiling from source here")
+                try:
+                    _build.build(from_source=True)
+                except Exception as e:  # noqa: BLE001 -- keep the shipped library, record why
+                    err = str(e)[-300:]
+                    log(f"rebuild failed, timing the shipped library: {err}")
+            rebuilt = err is None
+            if world > 1:
+                dist.barrier()
+            st = _build.library_status()
+    out = {"source_digest_ok": st["digest_ok"], "rebuilt_here": rebuilt}
+    if err:
+        out["rebuild_error"] = err
+    return out
 
 
 def main(argv=None) -> int:
@@ -315,6 +357,7 @@ def main(argv=None) -> int:
     log(f"world={world} batch/GPU={B} dtype={head_dt}")
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
+    comm_diag = multi_gpu_diagnostics(runner, a.steps, world, dev, cuda) if world > 1 else {}
     runner.close()
     del runner
     if cuda:
@@ -334,6 +377,8 @@ def main(argv=None) -> int:
         del r2
 
     rccl = _rccl_log_read(rccl_dir) if rank == 0 else {}
+    if "nranks" in rccl and rccl["nranks"] != world:
+        raise SystemExit(f"RCCL communicator reports nranks {rccl['nranks']}, WORLD_SIZE is {world}")
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -371,6 +416,8 @@ def main(argv=None) -> int:
                                  **({"rccl": rccl} if rccl else {})),
             },
             "model_tflops_per_s": round(tflops, 2),
+            **({"multi_gpu": dict(comm_diag, **({"rccl_nranks": rccl["nranks"]} if "nranks" in rccl else {}))}
+               if comm_diag else {}),
             "library": dict(lib_note, build_info=tdp.build_info()),
         }
         out.update(extra)

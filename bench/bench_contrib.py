@@ -33,13 +33,20 @@ from tensorrt_dft_plugins_amd.onnx import exporter as ex  # noqa: E402
 
 
 def dftexec(args, timeout=1200):
+    """Run the CLI in a fresh process; its stdout is collected and, like its stderr (--verbose
+    progress), echoed as it arrives."""
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     t0 = time.time()
-    r = subprocess.run([sys.executable, "-m", "tensorrt_dft_plugins_amd.engine.cli"] + args, capture_output=True,
-                       text=True, env=env, cwd=ROOT, timeout=timeout)
-    if r.returncode != 0:
-        raise RuntimeError(f"dftexec {' '.join(args)} failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
-    return r.stdout, time.time() - t0
+    pr = subprocess.Popen([sys.executable, "-m", "tensorrt_dft_plugins_amd.engine.cli", "--verbose"] + args,
+                          stdout=subprocess.PIPE, stderr=None, text=True, env=env, cwd=ROOT)
+    out = []
+    for ln in pr.stdout:
+        out.append(ln)
+        print(ln.rstrip(), file=sys.stderr, flush=True)
+    rc = pr.wait(timeout=timeout)
+    if rc != 0:
+        raise RuntimeError(f"dftexec {' '.join(args)} failed ({rc})")
+    return "".join(out), time.time() - t0
 
 
 def main() -> None:

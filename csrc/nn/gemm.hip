@@ -125,8 +125,10 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
     // operands as a wave-uniform 64-bit base + a 32-bit lane offset (the SGPR-base form of
     // global_load_lds: two fewer VGPRs per piece while the DMA issues inside an MFMA cluster)
     if constexpr (REG == 0 || REG == 3) {
+      // feature rows past N (the ragged last panel of an N % 256 != 0 GEMM) read row N - 1: their
+      // outputs are never stored; for full panels the clamp is a no-op
       const uint16_t* base = W + static_cast<int64_t>(f0) * ld + kt * kBK;  // uniform
-      g = base + static_cast<uint32_t>(tr * static_cast<int>(ld) + chunk * 8);
+      g = base + static_cast<uint32_t>(min(tr, p.N - 1 - f0) * static_cast<int>(ld) + chunk * 8);
     } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
       if constexpr (SPLIT) {  // channel kt / 2, patch rows (kt & 1) * 4 + c % 4 of the hi / lo plane
         const int py = (kt & 1) * 4 + (chunk & 3);
@@ -298,9 +300,13 @@ __device__ __forceinline__ float row_sum16(float x) {
 // grid of one tile per workgroup -- and measured 4-12 % SLOWER (profiles/gemm_persistent_r4.txt: the
 // GEMMs run power-limited, the turnaround gaps were the cheap part), so it stays opt-in
 // (MI_DFT_GEMM_PERSIST=1, bit-exact: tests/test_gemm_variants.py).
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false>
+// NT: N % 256 != 0 -- the last feature panel is ragged (N % 64 == 0): its W rows past N are clamped in
+// the DMA, its bias / c1 loads clamped, and the epilogue halves past N store nothing (wave-uniform).
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false,
+          bool NT = false>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   static_assert(!PERSIST || MODE == 0, "persistent tiles: token-major operands and outputs only");
+  static_assert(!NT || (!PERSIST && MODE != 2), "ragged feature panels: token-major, one tile per workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][4 regions]
   const uint16_t* __restrict__ W = p.w;
   const uint16_t* __restrict__ X = p.x;
@@ -314,7 +320,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   GEMM_STAMP(1, __builtin_amdgcn_s_memtime());
   // ---- XCD-aware tile order (bijective for any tile count).  PERSIST: virtual workgroup
   // v = blockIdx + k grid (grid % 8 == 0, so v stays on blockIdx's XCD)
-  const int tiles_f = N / kBF;
+  const int tiles_f = NT ? (N + kBF - 1) / kBF : N / kBF;
   const int ntl = PERSIST ? p.ntiles : static_cast<int>(gridDim.x);
   auto tile_of = [&](int v, int& f0_, int& t0_) {
     const int q8 = ntl / 8, r8 = ntl % 8, xcd = v % 8;
@@ -326,7 +332,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   int vb = blockIdx.x, f0, t0;
   tile_of(vb, f0, t0);
   const int KT = SPLIT ? K / 32 : K / kBK;  // SPLIT: 32-deep logical K-tiles (hi | lo = 64 elements)
-  AMD_DFT_DEV_CHECK(f0 + kBF <= N && t0 < M && (SPLIT ? (K / 32) * 32 : (K / kBK) * kBK) == K && KT > 0,
+  AMD_DFT_DEV_CHECK((NT ? f0 < N && N % 64 == 0 : f0 + kBF <= N) && t0 < M && (SPLIT ? (K / 32) * 32 : (K / kBK) * kBK) == K && KT > 0,
                     "gemm_bf16_kernel");
   f32x4 acc[8][4];
 #pragma unroll
@@ -556,7 +562,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     float4 bias4[8], c14[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int f = f0 + wr * 128 + i * 16 + 4 * kq;
+      const int f = NT ? min(f0 + wr * 128 + i * 16 + 4 * kq, N - 4) : f0 + wr * 128 + i * 16 + 4 * kq;
       bias4[i] = BIAS ? *reinterpret_cast<const float4*>(p.bias + f) : make_float4(0.f, 0.f, 0.f, 0.f);
       c14[i] = LN ? *reinterpret_cast<const float4*>(p.ln_c1 + f) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -612,6 +618,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
+          if constexpr (NT) {
+            if (fh >= N) continue;  // past the ragged panel's last feature: wave-uniform, nothing to store
+          }
           RT rr[RES ? NIT : 1];
           // residual rows are prefetched PD passes ahead of their use: all NIT before the half is
           // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
@@ -936,9 +945,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   }  // tile loop
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST>
-void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
-  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, PERSIST>;
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST, bool NT>
+void launch_kernel_nt(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, PERSIST, NT>;
   // the dynamic-LDS limit is a per-device function attribute: set it once per (instance, device)
   static std::atomic<uint64_t> attr_done{0};
   int dev = 0;
@@ -949,6 +958,18 @@ void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
     attr_done.fetch_or(uint64_t(1) << dev, std::memory_order_acq_rel);
   }
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
+}
+
+template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST>
+void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
+  if constexpr (!PERSIST && MODE != 2) {
+    if (p.N % kBF != 0) {  // ragged last feature panel (launch_gemm: staged epilogue, one tile per workgroup)
+      launch_kernel_nt<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, false, true>(p, st, grid);
+      return;
+    }
+  }
+  if (p.N % kBF != 0) throw std::runtime_error("amd_dft: gemm: N % 256 != 0 needs a token-major, non-persistent GEMM");
+  launch_kernel_nt<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, PERSIST, false>(p, st, grid);
 }
 
 // CAN_PERSIST: the instance has a persistent variant (the fp32 block's GEMMs); p.ntiles > 0 (set by
@@ -1033,8 +1054,11 @@ void throw_last(const char* what) {
 
 }  // namespace
 
+// N: whole 256-feature panels, or a ragged last panel of 64-feature halves (N % 64 == 0; token-major
+// outputs); K: whole 64-deep K-tiles
 bool gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return M >= 1 && N % kBF == 0 && K % kBK == 0 && K >= kBK && M < (int64_t(1) << 31) && N * K < (int64_t(1) << 31);
+  return M >= 1 && N >= 64 && N % 64 == 0 && K % kBK == 0 && K >= kBK && M < (int64_t(1) << 31) &&
+         N * K < (int64_t(1) << 31);
 }
 // logical K of a split (bf16x3) GEMM: 32-deep K-tiles, at least 2 (the pipeline prologue)
 static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
@@ -1072,19 +1096,21 @@ static int persist_grid() {
 }
 
 void launch_gemm(const GemmLaunch& p_, void* stream) {
-  if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 256 == 0, K % 64 == 0");
+  if (!gemm_supported(p_.M, p_.N, p_.K)) throw std::runtime_error("amd_dft: gemm: needs N % 64 == 0, K % 64 == 0");
   if (p_.ln_stats && !p_.ln_c1) throw std::runtime_error("amd_dft: gemm: LayerNorm fold needs c1");
   if (p_.out < 0 || p_.out > 2 || (p_.out != 0) != (p_.split != 0))
     throw std::runtime_error("amd_dft: gemm: fp32 / split-pair outputs come with split (bf16x3) operands only");
   if (p_.split && !split_k_ok(p_.K)) throw std::runtime_error("amd_dft: gemm: split mode needs K % 32 == 0, K >= 64");
   GemmLaunch p = p_;
-  p.direct_epi = gemm_direct_epi();
-  const int64_t nwg = ((p.M + kBT - 1) / kBT) * (p.N / kBF);
+  const bool ragged = p.N % kBF != 0;
+  if (ragged && p.sC > 0) throw std::runtime_error("amd_dft: gemm: the un-patchify scatter needs N % 256 == 0");
+  p.direct_epi = ragged ? 0 : gemm_direct_epi();  // the ragged panel's epilogue is the staged one
+  const int64_t nwg = ((p.M + kBT - 1) / kBT) * ((p.N + kBF - 1) / kBF);
   dim3 grid(static_cast<uint32_t>(nwg));
   p.ntiles = 0;
   // persistent variant: token-major GEMMs with an even K-tile count (the next tile's K-tile 0 lands
   // in stage 0) and more tiles than workgroups; instances without one fall back to a full grid
-  if (gemm_persist() && !p.direct_epi && p.gC == 0 && p.sC == 0 && (p.split ? p.K / 32 : p.K / kBK) % 2 == 0 &&
+  if (gemm_persist() && !ragged && !p.direct_epi && p.gC == 0 && p.sC == 0 && (p.split ? p.K / 32 : p.K / kBK) % 2 == 0 &&
       nwg > persist_grid()) {
     p.ntiles = static_cast<int>(nwg);
     grid = dim3(static_cast<uint32_t>(persist_grid()));

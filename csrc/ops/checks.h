@@ -15,13 +15,21 @@
 
 namespace amd_dft {
 
-inline bool finite_check_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("MI_DFT_CHECK_FINITE");
-    return e && std::string(e) != "0";
-  }();
+// Both switches start from their environment variable and can be flipped at run time
+// (torch.ops.amd_dft.set_finite_check / set_strict; utils.runtime.finite_checks / strict_mode).
+inline bool env_flag(const char* name) {
+  const char* e = std::getenv(name);
+  return e && std::string(e) != "0";
+}
+inline std::atomic<bool>& finite_check_flag() {
+  static std::atomic<bool> on{env_flag("MI_DFT_CHECK_FINITE")};
   return on;
 }
+inline std::atomic<bool>& strict_flag() {
+  static std::atomic<bool> on{env_flag("MI_DFT_STRICT")};
+  return on;
+}
+inline bool finite_check_enabled() { return finite_check_flag().load(std::memory_order_relaxed); }
 
 inline const at::Tensor& checked(const at::Tensor& out, const char* op) {
   if (finite_check_enabled() && out.defined() && out.numel() > 0 &&
@@ -45,11 +53,7 @@ inline FallbackRegistry& fallback_registry() {
   return r;
 }
 inline void fallback_note(const char* op, const char* why) {
-  static const bool strict = [] {
-    const char* e = std::getenv("MI_DFT_STRICT");
-    return e && std::string(e) != "0";
-  }();
-  TORCH_CHECK(!strict, "amd_dft.", op, ": no hand kernel for this call (", why, ") and MI_DFT_STRICT=1");
+  TORCH_CHECK(!strict_flag().load(std::memory_order_relaxed), "amd_dft.", op, ": no hand kernel for this call (", why, ") and MI_DFT_STRICT=1");
   auto& r = fallback_registry();
   bool first = false;
   {

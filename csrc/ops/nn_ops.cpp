@@ -13,7 +13,8 @@
 #include "checks.h"
 
 namespace amd_dft {
-void launch_patch_remap(const void* src, void* dst, int64_t B, int C, int h, int w, bool to_tokens, void* stream);
+void launch_patch_remap(const void* src, void* dst, int64_t B, int C, int h, int w, bool to_tokens, void* stream,
+                        int elem_bytes);
 
 namespace {
 
@@ -30,7 +31,7 @@ at::Tensor unpatchify_cpu(const at::Tensor& t, int64_t C, int64_t h, int64_t w, 
 }
 
 bool vec_ok(const at::Tensor& x, int64_t p) {
-  return x.scalar_type() == at::kBFloat16 && p == 8 && x.is_contiguous() &&
+  return (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) && p == 8 && x.is_contiguous() &&
          reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0;
 }
 
@@ -39,13 +40,13 @@ at::Tensor patchify_cuda(const at::Tensor& x_, int64_t p) {
   const c10::DeviceGuard guard(x_.device());
   at::Tensor x = x_.contiguous();
   if (!vec_ok(x, p)) {
-    fallback_note("patchify", "needs bf16, p == 8, 16-byte aligned");
+    fallback_note("patchify", "needs bf16 / fp32, p == 8, 16-byte aligned");
     return patchify_cpu(x, p);
   }
   const int64_t B = x.size(0), C = x.size(1), h = x.size(2) / p, w = x.size(3) / p;
   at::Tensor out = at::empty({B * h * w, C * p * p}, x.options());
   launch_patch_remap(x.data_ptr(), out.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(w), true,
-                     c10::hip::getCurrentHIPStream(x.device().index()).stream());
+                     c10::hip::getCurrentHIPStream(x.device().index()).stream(), static_cast<int>(x.element_size()));
   return out;
 }
 
@@ -54,13 +55,13 @@ at::Tensor unpatchify_cuda(const at::Tensor& t_, int64_t C, int64_t h, int64_t w
   const c10::DeviceGuard guard(t_.device());
   at::Tensor t = t_.contiguous();
   if (!vec_ok(t, p)) {
-    fallback_note("unpatchify", "needs bf16, p == 8, 16-byte aligned");
+    fallback_note("unpatchify", "needs bf16 / fp32, p == 8, 16-byte aligned");
     return unpatchify_cpu(t, C, h, w, p);
   }
   const int64_t B = t.numel() / (h * w * C * p * p);
   at::Tensor out = at::empty({B, C, h * p, w * p}, t.options());
   launch_patch_remap(t.data_ptr(), out.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(w), false,
-                     c10::hip::getCurrentHIPStream(t.device().index()).stream());
+                     c10::hip::getCurrentHIPStream(t.device().index()).stream(), static_cast<int>(t.element_size()));
   return out;
 }
 
@@ -76,7 +77,8 @@ at::Tensor unpatchify_meta(const at::Tensor& t, int64_t C, int64_t h, int64_t w,
 // ------------------------------------------------------------------ fused-epilogue linear
 // y = act(x @ w^T + bias) (+ residual); x [..., K] bf16, w [N, K] bf16, y [..., N] bf16.
 // act: 0 none, 1 GELU (erf).  CUDA: the hand-written MFMA GEMM (csrc/nn/gemm.hip) when
-// N % 256 == 0 and K % 64 == 0, otherwise hipBLASLt through at::linear.
+// N % 64 == 0 and K % 64 == 0 (a ragged last 256-feature panel is masked in the kernel), otherwise
+// hipBLASLt through at::linear (counted: fallback_counts / MI_DFT_STRICT).
 at::Tensor linear_ref(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
                       const c10::optional<at::Tensor>& residual) {
   at::Tensor y = at::linear(x.to(at::kFloat), w.to(at::kFloat),
@@ -103,7 +105,7 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
   TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "amd_dft.linear: bias must have N entries");
   if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K))
   {
-    fallback_note("linear", "needs bf16 operands, N % 256 == 0, K % 64 == 0 (fp32: use linear3)");
+    fallback_note("linear", "needs bf16 operands, N % 64 == 0, K % 64 == 0 (fp32: use linear3)");
     return linear_ref(x_, w_, bias, act, residual);
   }
   at::Tensor x = x_.contiguous(), w = w_.contiguous();
@@ -172,7 +174,7 @@ at::Tensor linear_ln_cuda(const at::Tensor& x_, const at::Tensor& w_, const at::
   check_linear_ln(x_, w_, c1_, bias, stats_, act);
   const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
   if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K)) {
-    fallback_note("linear_ln", "needs bf16 operands, N % 256 == 0, K % 64 == 0");
+    fallback_note("linear_ln", "needs bf16 operands, N % 64 == 0, K % 64 == 0");
     return linear_ln_ref(x_, w_, c1_, bias, stats_, act);
   }
   at::Tensor x = x_.contiguous(), w = w_.contiguous();
@@ -233,7 +235,7 @@ at::Tensor patch_linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c
   const bool native = p == 8 && x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
                       gemm_supported(M, N, K) && x_.numel() < (int64_t(1) << 31);
   if (!native) {  // ATen ops on the device tensors
-    fallback_note("patch_linear", "needs bf16, p == 8, N % 256 == 0 (fp32: use patch_linear3)");
+    fallback_note("patch_linear", "needs bf16, p == 8, N % 64 == 0 (fp32: use patch_linear3)");
     return patch_linear_cpu(x_, w_, bias, pos, p);
   }
   at::Tensor x = x_.contiguous(), wc = w_.contiguous();
@@ -283,7 +285,7 @@ at::Tensor linear_unpatch_cuda(const at::Tensor& t_, const at::Tensor& w_, const
   const bool native = p == 8 && t_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16 &&
                       gemm_supported(M, N, K) && M * N < (int64_t(1) << 31);
   if (!native) {
-    fallback_note("linear_unpatch", "needs bf16, p == 8, N % 256 == 0 (fp32: use linear_unpatch3)");
+    fallback_note("linear_unpatch", "needs bf16, p == 8, N % 64 == 0 (fp32: use linear_unpatch3)");
     return linear_unpatch_cpu(t_, w_, bias, C, h, wd, p);
   }
   at::Tensor t = t_.contiguous(), wc = w_.contiguous();
@@ -291,18 +293,27 @@ at::Tensor linear_unpatch_cuda(const at::Tensor& t_, const at::Tensor& w_, const
   at::Tensor y = at::empty({B, C, h * p, wd * p}, t.options());
   at::Tensor b;
   if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  // N % 256 != 0 (C % 4 != 0): token-major GEMM with a ragged last panel, then the remap kernel
+  const bool ragged = N % 256 != 0;
+  at::Tensor yt = ragged ? at::empty({M, N}, t.options()) : at::Tensor();
   GemmLaunch g;
   g.x = reinterpret_cast<const uint16_t*>(t.data_ptr());
   g.w = reinterpret_cast<const uint16_t*>(wc.data_ptr());
   g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
-  g.y = y.data_ptr();
+  g.y = ragged ? yt.data_ptr() : y.data_ptr();
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.K = static_cast<int>(K);
-  g.sC = static_cast<int>(C);
-  g.sh = static_cast<int>(h);
-  g.sw = static_cast<int>(wd);
-  launch_gemm(g, c10::hip::getCurrentHIPStream(t.device().index()).stream());
+  if (!ragged) {
+    g.sC = static_cast<int>(C);
+    g.sh = static_cast<int>(h);
+    g.sw = static_cast<int>(wd);
+  }
+  auto stream = c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  launch_gemm(g, stream);
+  if (ragged)
+    launch_patch_remap(yt.data_ptr(), y.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(wd),
+                       false, stream, 2);
   return y;
 }
 
@@ -403,7 +414,7 @@ at::Tensor linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10:
   TORCH_CHECK(act == 0 || act == 1, "amd_dft.linear3: act must be 0 (none) or 1 (gelu)");
   TORCH_CHECK(xs_.size(-1) == ws_.size(1), "amd_dft.linear3: xs [..., 2K], ws [N, 2K]");
   const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
-  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0 (got N=",
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3: the bf16x3 GEMM needs N % 64 == 0 and K % 64 == 0 (got N=",
               N, ", K=", K, ")");
   TORCH_CHECK(!(split_out && residual.has_value() && residual->defined() &&
                 (act != 0 || (bias.has_value() && bias->defined()))),
@@ -456,7 +467,7 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_cuda(const at::Tensor& xs_, con
   check_split_linear(xs_, ws_, c10::nullopt, "linear3_stats");
   TORCH_CHECK(xs_.size(-1) == ws_.size(1), "amd_dft.linear3_stats: xs [..., 2K], ws [N, 2K]");
   const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
-  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_stats: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0");
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_stats: the bf16x3 GEMM needs N % 64 == 0 and K % 64 == 0");
   TORCH_CHECK(residual.numel() == M * N, "amd_dft.linear3_stats: residual must have the output's shape");
   at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous(), r = residual.to(at::kFloat).contiguous();
   // the kernel always reads pre (zeros when absent): an optional load behind a branch made the compiler
@@ -527,7 +538,7 @@ std::tuple<at::Tensor, at::Tensor> linear_stats_cuda(const at::Tensor& x_, const
   TORCH_CHECK(residual.numel() == M * N, "amd_dft.linear_stats: residual must have the output's shape");
   TORCH_CHECK(!pre_.has_value() || !pre_->defined() || pre_->numel() == N, "amd_dft.linear_stats: pre must have N entries");
   if (x_.scalar_type() != at::kBFloat16 || w_.scalar_type() != at::kBFloat16 || !gemm_supported(M, N, K)) {
-    fallback_note("linear_stats", "needs bf16 operands, N % 256 == 0, K % 64 == 0");
+    fallback_note("linear_stats", "needs bf16 operands, N % 64 == 0, K % 64 == 0");
     return chunk_partials(linear_ref(x_, w_, c10::nullopt, 0, residual), pre_, N);
   }
   at::Tensor x = x_.contiguous(), w = w_.contiguous(), r = residual.to(at::kBFloat16).contiguous();
@@ -587,7 +598,7 @@ at::Tensor linear3_ln_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const a
   const c10::DeviceGuard guard(xs_.device());
   check_linear3_ln(xs_, ws_, c1_, bias, stats_, act);
   const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
-  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_ln: the bf16x3 GEMM needs N % 256 == 0 and K % 64 == 0 (got N=",
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_ln: the bf16x3 GEMM needs N % 64 == 0 and K % 64 == 0 (got N=",
               N, ", K=", K, ")");
   at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
   at::Tensor c1 = c1_.to(at::kFloat).contiguous(), stats = stats_.to(at::kFloat).contiguous();
@@ -653,7 +664,7 @@ at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, cons
   const int64_t B = xs_.size(1), C = xs_.size(2), h = xs_.size(3) / p, w = xs_.size(4) / p, N = ws_.size(0);
   const int64_t M = B * h * w, K = C * p * p;
   TORCH_CHECK(p == 8 && ws_.size(1) == 2 * K && gemm_supported(M, N, K) && xs_.numel() < (int64_t(1) << 31),
-              "amd_dft.patch_linear3: needs p == 8, ws [N, 2*C*64], N % 256 == 0 and < 2^31 image elements");
+              "amd_dft.patch_linear3: needs p == 8, ws [N, 2*C*64], N % 64 == 0 and < 2^31 image elements");
   at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
   at::Tensor y = at::empty({M, N}, xs.options().dtype(at::kFloat));
   at::Tensor b, r;
@@ -708,20 +719,28 @@ at::Tensor linear_unpatch3_cuda(const at::Tensor& ts_, const at::Tensor& ws_, co
   at::Tensor y = at::empty({B, C, h * p, wd * p}, ts.options().dtype(at::kFloat));
   at::Tensor b;
   if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  const bool ragged = N % 256 != 0;  // see linear_unpatch_cuda
+  at::Tensor yt = ragged ? at::empty({M, N}, ts.options().dtype(at::kFloat)) : at::Tensor();
   GemmLaunch g;
   g.x = reinterpret_cast<const uint16_t*>(ts.data_ptr());
   g.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
   g.bias = b.defined() ? b.data_ptr<float>() : nullptr;
-  g.y = y.data_ptr();
+  g.y = ragged ? yt.data_ptr() : y.data_ptr();
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.K = static_cast<int>(K);
-  g.sC = static_cast<int>(C);
-  g.sh = static_cast<int>(h);
-  g.sw = static_cast<int>(wd);
+  if (!ragged) {
+    g.sC = static_cast<int>(C);
+    g.sh = static_cast<int>(h);
+    g.sw = static_cast<int>(wd);
+  }
   g.split = 1;
   g.out = 1;
-  launch_gemm(g, c10::hip::getCurrentHIPStream(ts.device().index()).stream());
+  auto stream = c10::hip::getCurrentHIPStream(ts.device().index()).stream();
+  launch_gemm(g, stream);
+  if (ragged)
+    launch_patch_remap(yt.data_ptr(), y.data_ptr(), B, static_cast<int>(C), static_cast<int>(h), static_cast<int>(wd),
+                       false, stream, 4);
   return y;
 }
 

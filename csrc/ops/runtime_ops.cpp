@@ -47,6 +47,10 @@ void fallback_reset() {
   r.total.store(0);
 }
 
+// run-time switches (checks.h): return the previous setting
+bool set_finite_check(bool on) { return finite_check_flag().exchange(on); }
+bool set_strict(bool on) { return strict_flag().exchange(on); }
+
 }  // namespace
 }  // namespace amd_dft
 
@@ -57,4 +61,6 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("fallback_counts() -> (str[], int[])", &amd_dft::fallback_counts);
   m.def("fallback_reset() -> ()", &amd_dft::fallback_reset);
   m.def("fallback_note(str op, str why) -> ()", &amd_dft::fallback_note_op);
+  m.def("set_finite_check(bool on) -> bool", &amd_dft::set_finite_check);
+  m.def("set_strict(bool on) -> bool", &amd_dft::set_strict);
 }

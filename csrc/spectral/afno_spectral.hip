@@ -41,9 +41,10 @@
 // trips through HBM.
 //
 // Instances (AFNO_SHAPES below): H in {45 = 9x5, 64 = 16x4, 90 = 9x10} (FourCastNet at patch
-// 16 / square 512-pixel grids / patch 8) x block size in {64, 96, 128}.  The GEMMs are
-// [16 MT x 2BS] = A . W' with MT = ceil(H / 16) row tiles (rows >= H are padding whose outputs
-// are discarded) and 2BS / 16 column tiles over the 4 waves.
+// 16 / square 512-pixel grids / patch 8) x block size in {48, 64, 96, 128} (48: embed 384 at 8
+// blocks).  The GEMMs are [16 MT x 2BS] = A . W' with MT = ceil(H / 16) row tiles (rows >= H are
+// padding whose outputs are discarded) and 2BS / 16 column tiles over the 4 waves (BS = 48: 6 tiles,
+// the fourth wave's slots repeat the last tile and store nothing).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -89,7 +90,13 @@ struct AfnoShape {
   static constexpr int K = 2 * BS;        // real-block GEMM K = N
   static constexpr int APitch = K + 8;    // bf16 elements per A row (+16 B: ds_read_b128 spread)
   static constexpr int MT = (L + 15) / 16;  // GEMM row tiles (rows >= L are padding)
-  static constexpr int NTW = BS / 32;     // 16-wide column tiles per wave (2BS / 16 over 4 waves)
+  static constexpr int NCT = BS / 8;      // 16-wide column tiles of the 2BS-wide GEMM output
+  static constexpr int NTW = (NCT + 3) / 4;  // column tiles per wave (4 waves)
+  static constexpr bool CT_EXACT = NCT % 4 == 0;  // BS % 32 == 0: every wave owns NTW real tiles
+  // column tile of (wave w, slot nj); BS % 32 != 0 (e.g. 48): the last wave's extra slots repeat the
+  // last tile (their MFMAs are discarded, their stores skipped: ct_live)
+  __device__ static constexpr int ct(int w, int nj) { return CT_EXACT ? NTW * w + nj : min(NTW * w + nj, NCT - 1); }
+  __device__ static constexpr bool ct_live(int w, int nj) { return CT_EXACT || NTW * w + nj < NCT; }
   static constexpr int KS = BS / 16;      // 32-deep k-steps
   static constexpr int OCC = BS <= 96 ? 3 : 2;  // workgroups per SIMD the bf16 register budget targets
   // dynamic LDS: the FFT staging / GEMM A tile(s) (bf16 kernel: fp16 staging | one bf16 plane;
@@ -99,7 +106,7 @@ struct AfnoShape {
   static constexpr int64_t MAIN16 = L * BS * 4 > 32 * MT * APitch ? L * BS * 4 : 32 * MT * APitch;
   static constexpr int64_t MAIN32 = 2 * L * BS * 4 > 64 * MT * APitch ? 2 * L * BS * 4 : 64 * MT * APitch;
   static constexpr int64_t LDS16 = MAIN16 + TWN * 8, LDS32 = MAIN32 + TWN * 8;
-  static_assert(R0 * R1 == L && BS % 32 == 0 && L <= 128, "AFNO instance geometry");
+  static_assert(R0 * R1 == L && BS % 16 == 0 && L <= 128, "AFNO instance geometry");
 };
 
 __device__ __forceinline__ uint16_t f2bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
@@ -209,14 +216,14 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
   for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj)
-      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + ((S::NTW * w + nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
+      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + (S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
     if (ks + D < S::KS) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj)
         bq[(ks + D) % NQ][nj] =
-            *reinterpret_cast<const bf16x8*>(Bt + ((S::NTW * w + nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
+            *reinterpret_cast<const bf16x8*>(Bt + (S::ct(w, nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of its use (see gemm_tile_x3)
     bf16x8 afr[S::MT];
@@ -323,6 +330,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   __syncthreads();
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
     if constexpr (AFNO_X3_T) {  // lane: columns n0 .. n0 + 3 of row m -> one 8-byte write
       const int n0 = (S::NTW * w + nj) * 16 + 4 * (lane >> 4);
       const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
@@ -355,6 +363,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   const float lam = a.lambda;
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
     const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b2[n];
     const int c = n < BS ? n : n - BS;
@@ -498,7 +507,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
   for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) {
-      const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
+      const uint16_t* row = Bt + (S::ct(w, nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
       bh[s2][nj] = *reinterpret_cast<const bf16x8*>(row);
       bl[s2][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
     }
@@ -507,7 +516,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
     if (ks + D < S::KS) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
-        const uint16_t* row = Bt + ((S::NTW * w + nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
+        const uint16_t* row = Bt + (S::ct(w, nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
         bh[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row);
         bl[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
       }
@@ -632,6 +641,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   AFNO_STAMP(5, __builtin_amdgcn_s_memtime());
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
     if constexpr (AFNO_X3_T) {  // lane: columns n0 .. n0 + 3 of row m -> one 8-byte piece per plane
       const int n0 = (S::NTW * w + nj) * 16 + 4 * (lane >> 4);
       const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
@@ -662,6 +672,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   const float lam = a.lambda;
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
     const int n = (S::NTW * w + nj) * 16 + (lane & 15);
     const float bias = b2[n];
     const int c = n < BS ? n : n - BS;
@@ -746,12 +757,15 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   X(90, 9, 10, 96)     \
   X(90, 9, 10, 64)     \
   X(90, 9, 10, 128)    \
+  X(90, 9, 10, 48)     \
   X(45, 9, 5, 96)      \
   X(45, 9, 5, 64)      \
   X(45, 9, 5, 128)     \
+  X(45, 9, 5, 48)      \
   X(64, 16, 4, 64)     \
   X(64, 16, 4, 96)     \
-  X(64, 16, 4, 128)
+  X(64, 16, 4, 128)    \
+  X(64, 16, 4, 48)
 
 using KernFn = void (*)(AfnoArgs);
 struct AfnoInstance {

@@ -110,6 +110,20 @@ def embedded_digest(lib: str) -> str | None:
     return data[j:j + 64].decode(errors="replace")
 
 
+def embedded_info(lib: str) -> str | None:
+    """The whole provenance string (digest, host, time) a built library carries."""
+    try:
+        with open(lib, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(_DIGEST_MARK)
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i:j if j > 0 else i + 200].decode(errors="replace")
+
+
 def library_status(lib: str | None = None) -> dict:
     """{"path", "exists", "digest_ok"}: does the library match the current sources?"""
     lib = lib or os.environ.get("MI_DFT_LIB") or LIB

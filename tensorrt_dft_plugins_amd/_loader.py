@@ -59,7 +59,9 @@ def build_info() -> str:
     import ctypes
 
     load_plugins()
-    fn = ctypes.CDLL(_LIB_PATH).amd_dft_build_info
+    fn = getattr(ctypes.CDLL(_LIB_PATH), "amd_dft_build_info", None)
+    if fn is None:  # an older / diagnostic library (MI_DFT_LIB) without the provenance symbol
+        return "unknown (no provenance symbol)"
     fn.restype = ctypes.c_char_p
     return fn().decode()
 

@@ -46,6 +46,12 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
+    if a.verbose:  # engine build / optimizer progress on stderr
+        import logging
+
+        from ..utils.trace import get_logger
+
+        get_logger().setLevel(logging.INFO)
     from .. import load_plugins
     from .engine import Engine
 

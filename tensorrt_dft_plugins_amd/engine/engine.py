@@ -120,7 +120,8 @@ class Engine:
 
             t0 = time.perf_counter()
             shp = [list(map(int, s)) for s in input_shapes]
-            onnx_bytes, rep = _optimize(onnx_bytes, shp, input_dtypes, self.device)
+            onnx_bytes, rep = _optimize(onnx_bytes, shp, input_dtypes, self.device,
+                                        progress=lambda m: _log.info("graph optimizer: %s", m))
             counts: Dict[str, int] = {}
             for a in rep.applied:
                 counts[a["pattern"]] = counts.get(a["pattern"], 0) + 1
@@ -216,8 +217,9 @@ class Engine:
         self.static_outputs = outs
 
     def enqueue(self) -> None:
-        """Run one step on the current stream with whatever is in ``static_inputs``."""
-        if self._cuda_graph is not None:
+        """Run one step on the current stream with whatever is in ``static_inputs``.  Under a
+        caller's stream capture the nodes are recorded into that capture (no nested replay)."""
+        if self._cuda_graph is not None and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
             self._cuda_graph.replay()
         else:
             outs = self._run_eager()
@@ -288,8 +290,12 @@ class Engine:
         out on the stream the first time; a pointer set used again gets a hipGraph captured on
         those pointers (inputs read in place, no copy launches; ``BOUND_GRAPH_MAX`` kept, LRU), as
         a TensorRT context binds the caller's pointers directly (reference test_dft.py:112-114).
-        The pointers must stay valid while the engine may replay on them.  Returns without waiting."""
-        if self._bound and all(type(b) is int for b in bindings):
+        The pointers must stay valid while the engine may replay on them.  Returns without waiting,
+        except on the call that captures a new bound graph: hipGraph capture synchronises the
+        device once.  Inside a caller's own stream capture no graph is bound (a capture cannot
+        nest): the copy path is recorded into the caller's graph instead."""
+        capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        if self._bound and not capturing and all(type(b) is int for b in bindings):
             # hot path: an already bound pointer set needs no tensor wrappers or checks
             g = self._bound.get(tuple(bindings))
             if g is not None:
@@ -300,7 +306,7 @@ class Engine:
         views = self._views(bindings)
         n_in = len(self.static_inputs)
         own = [v.data_ptr() == t.data_ptr() for v, t in zip(views, self.binding_tensors)]
-        if self._cuda_graph is not None and not all(own) and self._bindable(views):
+        if self._cuda_graph is not None and not all(own) and not capturing and self._bindable(views):
             key = tuple(v.data_ptr() for v in views)
             g = self._bound.get(key)
             if g is None:

@@ -303,10 +303,11 @@ class AFNONet(nn.Module):
         return t.reshape(B, cfg.out_chans, cfg.h * p, cfg.w * p)
 
     def _f32_native(self) -> bool:
-        """fp32 on the hand kernels (bf16x3 GEMMs) needs the embed/MLP/head widths in 256-tiles."""
+        """fp32 on the hand kernels (bf16x3 GEMMs) needs the embed/MLP/head widths in 64-feature
+        halves (ragged 256-feature panels are masked in the GEMM) and 8x8 patches."""
         cfg = self.cfg
         hid = int(cfg.embed_dim * cfg.mlp_ratio)
-        return (cfg.embed_dim % 256 == 0 and hid % 256 == 0 and (cfg.out_chans * cfg.patch_size ** 2) % 256 == 0
+        return (cfg.embed_dim % 64 == 0 and hid % 64 == 0 and (cfg.out_chans * cfg.patch_size ** 2) % 64 == 0
                 and cfg.patch_size == 8)
 
     def _head_bias_cpp(self, pre: torch.Tensor) -> torch.Tensor:

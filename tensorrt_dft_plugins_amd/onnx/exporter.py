@@ -29,6 +29,25 @@ DEFAULT_OPSET = 15
 
 
 # ----------------------------------------------------------------- autograd Functions
+def _contrib_node(g, kind: str, x, signal_ndim: int):
+    """The contrib node, with its output type stamped (static shape inference of §2.9 items 4-5),
+    so the exporter does not warn that ``com.microsoft::Rfft`` has no shape inference."""
+    out = g.op(f"{CONTRIB_DOMAIN}::{kind}", x, normalized_i=0, onesided_i=1, signal_ndim_i=signal_ndim)
+    try:
+        from torch.onnx import symbolic_helper as sh
+
+        sizes = sh._get_tensor_sizes(x)
+        if sizes is not None and all(d is not None for d in sizes):
+            if kind == "Rfft":
+                sizes = list(sizes[:-1]) + [sizes[-1] // 2 + 1, 2]
+            else:
+                sizes = list(sizes[:-2]) + [2 * (sizes[-2] - 1)]
+            out.setType(x.type().with_sizes(sizes))
+    except Exception:  # noqa: BLE001 -- best effort: the importer infers shapes anyway
+        pass
+    return out
+
+
 class Rfft(torch.autograd.Function):
     """``com.microsoft::Rfft`` over the last ``signal_ndim`` dims."""
 
@@ -39,7 +58,7 @@ class Rfft(torch.autograd.Function):
 
     @staticmethod
     def symbolic(g, x, signal_ndim: int = 2):
-        return g.op(f"{CONTRIB_DOMAIN}::Rfft", x, normalized_i=0, onesided_i=1, signal_ndim_i=signal_ndim)
+        return _contrib_node(g, "Rfft", x, signal_ndim)
 
 
 class Irfft(torch.autograd.Function):
@@ -52,7 +71,7 @@ class Irfft(torch.autograd.Function):
 
     @staticmethod
     def symbolic(g, x, signal_ndim: int = 2):
-        return g.op(f"{CONTRIB_DOMAIN}::Irfft", x, normalized_i=0, onesided_i=1, signal_ndim_i=signal_ndim)
+        return _contrib_node(g, "Irfft", x, signal_ndim)
 
 
 class OnnxRfft2(torch.autograd.Function):
@@ -65,7 +84,7 @@ class OnnxRfft2(torch.autograd.Function):
 
     @staticmethod
     def symbolic(g, x):
-        return g.op(f"{CONTRIB_DOMAIN}::Rfft", x, normalized_i=0, onesided_i=1, signal_ndim_i=2)
+        return _contrib_node(g, "Rfft", x, 2)
 
 
 class OnnxIrfft2(torch.autograd.Function):
@@ -78,7 +97,7 @@ class OnnxIrfft2(torch.autograd.Function):
 
     @staticmethod
     def symbolic(g, x):
-        return g.op(f"{CONTRIB_DOMAIN}::Irfft", x, normalized_i=0, onesided_i=1, signal_ndim_i=2)
+        return _contrib_node(g, "Irfft", x, 2)
 
 
 def rfft(x: torch.Tensor, signal_ndim: int = 2) -> torch.Tensor:
@@ -100,11 +119,15 @@ def _const_int(v) -> int:
 
 
 def _sym_rfft(g, x, normalized, onesided, signal_ndim):
+    if (_const_int(normalized), _const_int(onesided)) == (0, 1):
+        return _contrib_node(g, "Rfft", x, _const_int(signal_ndim))
     return g.op(f"{CONTRIB_DOMAIN}::Rfft", x, normalized_i=_const_int(normalized),
                 onesided_i=_const_int(onesided), signal_ndim_i=_const_int(signal_ndim))
 
 
 def _sym_irfft(g, x, normalized, onesided, signal_ndim):
+    if (_const_int(normalized), _const_int(onesided)) == (0, 1):
+        return _contrib_node(g, "Irfft", x, _const_int(signal_ndim))
     return g.op(f"{CONTRIB_DOMAIN}::Irfft", x, normalized_i=_const_int(normalized),
                 onesided_i=_const_int(onesided), signal_ndim_i=_const_int(signal_ndim))
 

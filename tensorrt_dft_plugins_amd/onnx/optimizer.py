@@ -359,8 +359,9 @@ def amd_node(g: IRGraph, opname: str, tensors: Sequence[Optional[str]], outputs:
 
 
 class Ctx:
-    def __init__(self, g: IRGraph, device: torch.device, report: OptimizeReport, verify: bool = True):
+    def __init__(self, g: IRGraph, device: torch.device, report: OptimizeReport, verify: bool = True, progress=None):
         self.g, self.device, self.report, self.verify = g, device, report, verify
+        self.progress = progress
         self.refresh()
 
     def refresh(self) -> None:
@@ -437,9 +438,14 @@ def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
+def _gen(device, seed: int) -> torch.Generator:
+    """A generator on the build device: full-size probes are drawn there, not on the host."""
+    return torch.Generator(device=device).manual_seed(seed)
+
+
 def _rand_for(g: IRGraph, name: str, device, gen: torch.Generator, scale: float = 1.0) -> torch.Tensor:
     s, dt = g.meta[name]
-    return (torch.randn(s, generator=gen, dtype=torch.float32) * scale).to(device=device, dtype=dt)
+    return (torch.randn(s, generator=gen, dtype=torch.float32, device=device) * scale).to(dtype=dt)
 
 
 def _verify(ctx: Ctx, old: Sequence[Node], new: Sequence[Node], ins: Sequence[str], outs_old: Sequence[str],
@@ -451,7 +457,7 @@ def _verify(ctx: Ctx, old: Sequence[Node], new: Sequence[Node], ins: Sequence[st
     g = ctx.g
     worst = 0.0
     for si, sc in enumerate(scales):
-        gen = torch.Generator().manual_seed(1234 + si)
+        gen = _gen(ctx.device, 1234 + si)
         env = {i: _rand_for(g, i, ctx.device, gen, sc) for i in ins}
         e1 = g.run_nodes(old, env, ctx.device)
         e2 = g.run_nodes(new, env, ctx.device)
@@ -564,7 +570,7 @@ def rewrite_layernorm(ctx: Ctx) -> None:
 
 
 def _gemm_ok(N: int, K: int, split: bool) -> bool:
-    return N % 256 == 0 and (K % 32 == 0 and K >= 64 if split else K % 64 == 0)
+    return N % 64 == 0 and N >= 64 and (K % 32 == 0 and K >= 64 if split else K % 64 == 0)
 
 
 def rewrite_linear(ctx: Ctx) -> None:
@@ -722,8 +728,8 @@ def rewrite_patch_embed(ctx: Ctx) -> None:
             B, Cin, Hh, Ww = g.shape(x)
             N = W.shape[0]
             h, w = Hh // p, Ww // p
-            if N % 256:
-                raise RewriteRejected(f"patch embedding width {N} not a multiple of 256")
+            if N % 64:
+                raise RewriteRejected(f"patch embedding width {N} not a multiple of 64")
             rs = ctx.only_consumer(cv.outputs[0], "Reshape")
             if rs is None or g.shape(rs.outputs[0]) != [B, N, h * w]:
                 raise RewriteRejected("conv output is not flattened to [B, C, h*w]")
@@ -788,7 +794,7 @@ def rewrite_unpatch_head(ctx: Ctx) -> None:
             if rs2 is None or g.shape(rs2.outputs[0]) != [B, Co, h * p, w * p]:
                 raise RewriteRejected("un-patchify does not end in [B, C, h*p, w*p]")
             dt = g.dtype(t)
-            if dt not in (torch.float32, torch.bfloat16) or p != 8 or (Co * p * p) % 256 or C % 64:
+            if dt not in (torch.float32, torch.bfloat16) or p != 8 or C % 64:
                 raise RewriteRejected("head GEMM tile constraints")
             out = rs2.outputs[0]
             # weight rows reordered from (p1, p2, c_out) to (c_out, p1, p2)
@@ -993,8 +999,8 @@ def rewrite_afno(ctx: Ctx) -> None:
                 raise RewriteRejected("block sizes do not tile the channels")
             F = _region_fn(ctx, reg)
             # --- probe on a realistic spectrum: Rfft of a random channel-last field
-            gen = torch.Generator().manual_seed(7)
-            hp = torch.randn([B, H, W, C], generator=gen).to(ctx.device, dt)
+            gen = _gen(ctx.device, 7)
+            hp = torch.randn([B, H, W, C], generator=gen, device=ctx.device).to(dt)
             pre_env = g.run_nodes(pre[::-1] + [rf], {h: hp}, ctx.device)
             X = pre_env[rf.outputs[0]]
             Y = F(X)
@@ -1014,7 +1020,7 @@ def rewrite_afno(ctx: Ctx) -> None:
             # --- roles: which constant is w_re / w_im / b_re / b_im of each layer, the input scale
             # and the softshrink threshold: checked on sampled modes of the probe
             scal = _scalar_consts(ctx, reg.nodes)
-            sel = torch.randint(0, B * (r1 - r0) * km, (8,), generator=gen)
+            sel = torch.randint(0, B * (r1 - r0) * km, (8,), generator=_gen("cpu", 8))
             Xs = X.float().permute(0, 2, 3, 1, 4)[:, r0:r1, :km].reshape(-1, C, 2)[sel.to(X.device)].cpu().double()
             Ys = Yc.permute(0, 2, 3, 1, 4)[:, r0:r1, :km].reshape(-1, C, 2)[sel.to(Y.device)].cpu().double()
             best = None
@@ -1136,7 +1142,7 @@ def rewrite_fno(ctx: Ctx) -> None:
             keep_rows = list(range(m1)) + list(range(H - m1, H))
             Wk = Wt[:, :, keep_rows, :m2]  # [Cin, Cout, 2*m1, m2, 2] (complex-as-pair)
             # --- the map must be complex-linear, batch- and mode-diagonal: check on random spectra
-            gen = torch.Generator().manual_seed(11)
+            gen = _gen("cpu", 11)
             Xr = torch.randn(B, Cin, H, wf, 2, generator=gen, dtype=torch.float64)
             Yr = F(Xr.float().to(dev)).double().cpu()
             wc = torch.view_as_complex(Wk.contiguous())
@@ -1197,9 +1203,10 @@ PASSES = (("afno_filter", rewrite_afno), ("fno_spectral", rewrite_fno), ("layer_
 
 
 def optimize(onnx_bytes: bytes, input_shapes: Sequence[Sequence[int]], input_dtypes=None, device=None,
-             verify: bool = True, passes: Optional[Sequence[str]] = None) -> Tuple[bytes, OptimizeReport]:
+             verify: bool = True, passes: Optional[Sequence[str]] = None, progress=None) -> Tuple[bytes, OptimizeReport]:
     """Rewrite ``onnx_bytes`` for this library's kernels.  Returns (model bytes, report); the
-    input bytes are returned unchanged when no rewrite applies."""
+    input bytes are returned unchanged when no rewrite applies.  ``progress(msg)`` is called after
+    every pass (engine builds log it)."""
     device = torch.device(device) if device is not None else (
         torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
     model = P.load_model(onnx_bytes)
@@ -1212,14 +1219,17 @@ def optimize(onnx_bytes: bytes, input_shapes: Sequence[Sequence[int]], input_dty
         g.infer_shapes()
     g.eliminate_noops()
     g.dead_code()
-    ctx = Ctx(g, device, rep, verify)
+    ctx = Ctx(g, device, rep, verify, progress)
     for name, fn in PASSES:
         if passes is not None and name not in passes:
             continue
+        n0 = len(rep.applied)
         fn(ctx)
         ctx.topo_fix()
         g.dead_code()
         ctx.refresh()
+        if progress is not None:
+            progress(f"pass {name}: {len(rep.applied) - n0} rewrites, {len(g.nodes)} nodes")
     rep.nodes_after = len(g.nodes)
     if not rep.applied:
         return onnx_bytes, rep

@@ -85,12 +85,15 @@ def _to_dev(t: torch.Tensor, device: torch.device) -> torch.Tensor:
         return t
     if t.numel() <= 4096:
         key = (str(device), t.dtype, tuple(t.shape), tuple(t.reshape(-1).tolist()))
-        v = _DEV_CONSTS.get(key)
-        if v is None:
-            v = t.to(device)
-            _DEV_CONSTS[key] = v
-        return v
-    return t.to(device)
+    else:  # a large host constant (e.g. ScatterND indices): memoised by storage; it lives in the graph
+        key = (str(device), t.dtype, tuple(t.shape), t.data_ptr(), t._version)
+    v = _DEV_CONSTS.get(key)
+    if v is None:
+        # the entry keeps the host tensor alive too, so a storage-keyed entry can never be
+        # matched by another tensor reusing a freed address
+        v = (t.to(device), t)
+        _DEV_CONSTS[key] = v
+    return v[0]
 
 
 def _align(a, b):
@@ -375,7 +378,7 @@ def _gather(attrs, x, idx):
     axis = attrs.get("axis", 0) % x.dim()
     ishape = list(idx.shape)  # a 0-d index drops the axis (kept even when moved to the device as [1])
     if _is_host(idx) and not _is_host(x):
-        idx = _to_dev(idx, x.device) if idx.dim() else idx.reshape(1).to(x.device)
+        idx = _to_dev(idx if idx.dim() else idx.reshape(1), x.device)  # memoised: no copy under capture
     if _is_host(x) and not _is_host(idx):
         x = _to_dev(x, idx.device)
     n = x.shape[axis]
@@ -389,7 +392,7 @@ def _scatter_nd(attrs, x, idx, upd):
     """ONNX ScatterND (torch exports in-place slice assignment, e.g. the classic FNO's
     ``out_ft[:, :, :m1, :m2] = ...``, this way)."""
     if _is_host(idx) and not _is_host(x):
-        idx = idx.to(x.device)
+        idx = _to_dev(idx, x.device)
     if _is_host(upd) and not _is_host(x):
         upd = _to_dev(upd, x.device)
     k = idx.shape[-1]

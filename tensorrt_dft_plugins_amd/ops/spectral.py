@@ -118,7 +118,7 @@ def pack_afno_weights(w1, b1, w2, b2, split: bool = False) -> Tuple[torch.Tensor
 # (H, block size) instances of the fused AFNO kernel; mirrors afno_spectral_supported() in
 # csrc/spectral/afno_spectral.hip (checked equal in tests/test_models.py).  Kept in Python so
 # the check stays a constant under ONNX/TorchScript tracing (an op returning bool cannot be traced).
-AFNO_FUSED_SHAPES = frozenset({(H, bs) for H in (45, 64, 90) for bs in (64, 96, 128)})
+AFNO_FUSED_SHAPES = frozenset({(H, bs) for H in (45, 64, 90) for bs in (48, 64, 96, 128)})
 
 
 def afno_fused_available(x: torch.Tensor, num_blocks: int) -> bool:
@@ -228,13 +228,14 @@ def _ln_fused_ok(blk, x: torch.Tensor) -> bool:
 
 
 def _mlp_gemm_ok(m, split: bool) -> bool:
-    """Both MLP GEMMs fit the hand kernel (csrc/nn/gemm.hip): output features in 256-tiles and
-    the reduction depth in 64-tiles (bf16) or 32-tiles of at least 64 (bf16x3 split)."""
+    """Both MLP GEMMs fit the hand kernel (csrc/nn/gemm.hip): output features in 64-feature
+    halves (a ragged last 256-feature panel is masked in the kernel) and the reduction depth in
+    64-tiles (bf16) or 32-tiles of at least 64 (bf16x3 split)."""
     def k_ok(k: int) -> bool:
         return k % 32 == 0 and k >= 64 if split else k % 64 == 0
 
     f1, f2 = m.fc1, m.fc2
-    return (f1.out_features % 256 == 0 and f2.out_features % 256 == 0 and k_ok(f1.in_features)
+    return (f1.out_features % 64 == 0 and f2.out_features % 64 == 0 and k_ok(f1.in_features)
             and k_ok(f2.in_features))
 
 

@@ -116,6 +116,53 @@ class DataParallelInference:
                     self.full[i] = torch.empty((self.world * o.shape[0],) + tuple(o.shape[1:]), dtype=o.dtype,
                                                device=o.device)
         self.k = 0
+        self._comm_marks: Optional[List[tuple]] = None  # (start, end) events per gather when timing
+
+    # ------------------------------------------------------------------ diagnostics
+    def time_comm(self, on: bool = True) -> None:
+        """Record a (start, end) event pair around every gather on the comm stream (GPU)."""
+        self._comm_marks = [] if on and self.cuda and self.gather else None
+
+    def comm_busy_ms(self) -> Optional[float]:
+        """Total comm-stream time spent inside gathers since ``time_comm()`` (call after ``drain``
+        + synchronize).  The start event sits after the wait for the step's compute, so this is
+        the gathers' own duration, not their queueing behind compute."""
+        if self._comm_marks is None:
+            return None
+        return float(sum(a.elapsed_time(b) for a, b in self._comm_marks))
+
+    def gather_only_ms(self, iters: int = 5) -> Optional[float]:
+        """Milliseconds per gather with no compute in flight: ``iters`` back-to-back gathers of
+        the current output shard (the xGMI / RCCL cost the overlapped step hides)."""
+        if not self.gather:
+            return None
+        self.drain()
+        out = self.cap.outputs[0][0]
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+                a.record(self.comm_stream)
+                for j in range(iters):
+                    if self.ipc is not None:
+                        self.ipc.gather(out, j)
+                    else:
+                        all_gather_batch(out, self.full[0], async_op=False)
+                b.record(self.comm_stream)
+            torch.cuda.synchronize(self.device)
+            return a.elapsed_time(b) / iters
+        import time as _t
+
+        t0 = _t.perf_counter()
+        for j in range(iters):
+            if self.ipc is not None:
+                self.ipc.gather(out, j)
+            else:
+                all_gather_batch(out, self.full[0], async_op=False)
+        if self.ipc is not None:
+            self.ipc.synchronize()
+        return (_t.perf_counter() - t0) * 1e3 / iters
 
     @property
     def inputs(self) -> torch.Tensor:
@@ -139,12 +186,20 @@ class DataParallelInference:
         out = self.cap.replay(i)[0]
         if not self.gather:
             return out
+        marks = None
+        if self._comm_marks is not None:
+            marks = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self._comm_marks.append(marks)
         if self.ipc is not None:
             if self.cuda:
                 self.events[i].record()
                 with torch.cuda.stream(self.comm_stream):
                     self.comm_stream.wait_event(self.events[i])
+                    if marks:
+                        marks[0].record(self.comm_stream)
                     self.ipc.gather(out, i)
+                    if marks:
+                        marks[1].record(self.comm_stream)
                     self.done[i].record(self.comm_stream)
                 self.done_pending[i] = True
             else:
@@ -154,7 +209,14 @@ class DataParallelInference:
             self.events[i].record()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(self.events[i])
+                if marks:
+                    marks[0].record(self.comm_stream)
                 _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
+                if marks:
+                    # RCCL runs on its own stream: join it (stream-ordered, no host wait) so the
+                    # end mark is recorded when the collective has finished
+                    self.works[i].wait()
+                    marks[1].record(self.comm_stream)
         else:
             _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
         return self.full[i]

@@ -2,8 +2,10 @@
 
 * ``finite_checks(True)`` / ``MI_DFT_CHECK_FINITE=1``: every native op validates that its
   output is finite (SURVEY §2.9 item 11 -- the reference's enqueue always returns 0,
-  /root/reference/src/dft_plugins/dft_plugins.cpp:198); the C++ side reads the variable once
-  at first use, so set it before the first op runs.
+  /root/reference/src/dft_plugins/dft_plugins.cpp:198).  The variable sets the initial state;
+  ``finite_checks`` switches the loaded library at any time (and exports the variable for
+  child processes).
+* ``strict_mode(True)`` / ``MI_DFT_STRICT=1``: a device op that would leave its hand kernel raises.
 * ``time_fn``: device time of a callable, eager or captured into one hipGraph.
 * ``env_report``: the versions / devices a benchmark line should be read against.
 """
@@ -16,8 +18,25 @@ from typing import Callable, Dict
 import torch
 
 
-def finite_checks(enable: bool = True) -> None:
+def finite_checks(enable: bool = True) -> bool:
+    """Turn the native ops' output NaN/Inf check on or off; returns the previous setting."""
+    from .._loader import load_plugins
+
+    load_plugins()
+    prev = bool(torch.ops.amd_dft.set_finite_check(bool(enable)))
     os.environ["MI_DFT_CHECK_FINITE"] = "1" if enable else "0"
+    return prev
+
+
+def strict_mode(enable: bool = True) -> bool:
+    """Make ATen / vendor fallbacks of the device ops raise (True) or warn + count (False);
+    returns the previous setting."""
+    from .._loader import load_plugins
+
+    load_plugins()
+    prev = bool(torch.ops.amd_dft.set_strict(bool(enable)))
+    os.environ["MI_DFT_STRICT"] = "1" if enable else "0"
+    return prev
 
 
 def check_finite(t: torch.Tensor, what: str = "tensor") -> torch.Tensor:

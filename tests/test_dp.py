@@ -214,6 +214,12 @@ def test_bench_harness_torchrun_gloo(nproc, extra, scaling, gather_dtype):
         assert d["config"]["gather_backend"] == extra[extra.index("--gather") + 1]
     if gather_dtype:
         assert d["config"]["gather_dtype"] == gather_dtype
+    # self-diagnosis of a multi-GPU run: the collective's rank count, the
+    # gather-only cost and the comm stream's busy time per step
+    mg = d["multi_gpu"]
+    assert mg["collective_ranks"] == nproc
+    assert mg["gather_only_ms"] > 0
+    print(json.dumps(mg))
 
 
 def test_rccl_choices_parser():
@@ -232,8 +238,10 @@ def test_rccl_choices_parser():
         "host:1:1 [0] NCCL INFO 32 coll channels, 32 collnet channels, 0 nvls channels, 32 p2p channels, 4 p2p channels per peer",
         "host:1:1 [0] NCCL INFO AllGather: algo Ring proto Simple nchannels 32 nthreads 256",
         "host:1:1 [0] NCCL INFO AllGather: algo Ring proto Simple nchannels 32 nthreads 256",
+        "host:1:1 [0] NCCL INFO comm 0x5f0c rank 0 nranks 8 cudaDev 0 busId 5000 commId 0x1 - Init COMPLETE",
     ])
     r = rccl_choices(log)
+    assert r["nranks"] == 8
     assert r["coll_channels"] == 32 and r["p2p_channels"] == 32 and r["ring_channels"] == 32
     assert r["ring0"] == "0 1 2 3 4 5 6 7" and r["version"].startswith("2.26.6")
     assert r["tuning"] == ["AllGather: algo Ring proto Simple nchannels 32 nthreads 256"]

@@ -201,6 +201,29 @@ def test_engine_execute_v2_bound_graphs_gpu(device):
 
 
 @pytest.mark.gpu
+def test_engine_execute_async_v2_inside_caller_capture_gpu(device):
+    """execute_async_v2 on caller pointers while the CALLER is capturing a hipGraph: no nested
+    capture / replay, the engine's nodes are recorded into the caller's graph."""
+    torch.manual_seed(4)
+    eng = Engine.build(Rfft2Model(), (torch.randn(1, 2, 720, 1440),), device=device)
+    x = torch.randn(1, 2, 720, 1440, device=device)
+    y = torch.empty(1, 2, 720, 721, 2, device=device)
+    for _ in range(2):  # the same pointer set twice outside capture: bound graph, then replay
+        eng.execute_async_v2([x.data_ptr(), y.data_ptr()])
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g):
+        eng.execute_async_v2([x.data_ptr(), y.data_ptr()])
+    x.copy_(torch.randn(1, 2, 720, 1440))
+    y.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    ref = torch.view_as_real(torch.fft.rfft2(x.cpu().double()))
+    assert ((y.cpu().double() - ref).norm() / ref.norm()).item() < 1e-6
+
+
+@pytest.mark.gpu
 def test_engine_from_fast_models_gpu(device, tmp_path):
     """Engines built from the MI355X model paths (com.amd.dft nodes) replay under hipGraph and
     match the eager model."""

@@ -447,17 +447,19 @@ def test_generic_afno_shape_counts_fallbacks(device):
 
 
 def test_fp32_block_gate_checks_real_mlp_width():
-    """the fp32 fused-block gate must look at the real MLP widths (mlp_ratio != 4):
-    embed 256 x 2.5 = hidden 640 is not a 256-multiple, so the block stays on the generic path
-    instead of hard-failing inside linear3."""
+    """the fp32 fused-block gate must look at the real MLP widths (mlp_ratio != 4).
+    Round 5: the hand GEMM masks a ragged last 256-feature panel, so widths in 64-feature halves
+    (embed 256 x 2.5 = hidden 640, embed 384) stay on it; others keep the generic path instead of
+    hard-failing inside linear3."""
     from tensorrt_dft_plugins_amd.models.afno import Mlp
 
     assert S._mlp_gemm_ok(Mlp(768, 3072), split=True)
     assert S._mlp_gemm_ok(Mlp(256, 1024), split=False)
-    assert not S._mlp_gemm_ok(Mlp(256, 640), split=True)
-    assert not S._mlp_gemm_ok(Mlp(320, 1280), split=False)
-    assert S._mlp_gemm_ok(Mlp(256, 1280), split=False)
-    assert not S._mlp_gemm_ok(Mlp(256, 1056), split=True)  # fc2 K = 1056: 32-tiles ok, fc1 out 1056 % 256 != 0
+    assert S._mlp_gemm_ok(Mlp(256, 640), split=True)      # ragged fc1 panel (640 = 2 x 256 + 128)
+    assert S._mlp_gemm_ok(Mlp(384, 1536), split=True)     # FourCastNet embed 384: fc2 N = 384
+    assert S._mlp_gemm_ok(Mlp(320, 1280), split=False)
+    assert not S._mlp_gemm_ok(Mlp(256, 1056), split=True)  # fc1 out 1056 % 64 != 0
+    assert not S._mlp_gemm_ok(Mlp(256, 600), split=False)
 
 
 def test_fused_fp32_block_composition_and_export_cpu(monkeypatch):
