@@ -331,7 +331,7 @@ def main(argv=None) -> int:
         torch.cuda.set_device(dev)
     lib_note = _ensure_library(rank, world, cuda)
     tdp.load_plugins()
-    gemm_table = None  # hipBLASLt solution tables: bench/experimental/gemm_tables.py (comparator only)
+    gemm_table = None  # (hipBLASLt solution tables were a round-1 comparator, removed round 5)
     from tensorrt_dft_plugins_amd.ops.spectral import mlp_on_hand_gemm
 
     if a.tiny:

@@ -48,4 +48,8 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import note_tuning_build
+
+    note_tuning_build("MI_DFT_FIXED_CFG")
     main()

@@ -1,5 +1,6 @@
 """rfft2 / irfft2 720x1440 latency per column-pass tile config (MI_DFT_FIXED_CFG) and XCD-aware
-tile order (MI_DFT_FFT_XCD), one process, interleaved."""
+tile order (MI_DFT_FFT_XCD), one process, interleaved.
+(Tuning build only: the switches are read by a library built with -DAMD_DFT_TUNING=1, csrc/ops/tuning.h.)"""
 import json
 import os
 import sys

@@ -43,4 +43,8 @@ def main():
 
 
 if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import note_tuning_build
+
+    note_tuning_build("MI_DFT_LN_SPLIT")
     main()

@@ -1,5 +1,6 @@
 """A/B the specialised column-pass configurations (MI_DFT_FIXED_CFG) and the generic kernel
-for rfft2/irfft2 720x1440 (interleaved rounds, hipGraph timing)."""
+for rfft2/irfft2 720x1440 (interleaved rounds, hipGraph timing).
+(Tuning build only: the switches are read by a library built with -DAMD_DFT_TUNING=1, csrc/ops/tuning.h.)"""
 import os
 import statistics
 import sys

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "fft_fixed_impl.h"
+#include "../ops/tuning.h"
 
 namespace amd_dft {
 namespace fixed_detail {
@@ -34,7 +35,7 @@ const std::vector<FixedCfg>& fixed_configs() { return table(); }
 // when the plan of L is first built).
 std::vector<int32_t> fixed_radices(int32_t L) {
   static const std::string spec = [] {
-    const char* e = std::getenv("MI_DFT_FFT_RADICES");
+    const char* e = tuning_env("MI_DFT_FFT_RADICES");
     return std::string(e ? e : "");
   }();
   if (!spec.empty()) {
@@ -77,9 +78,9 @@ struct FixedKnobs {
 const FixedKnobs& knobs() {
   static const FixedKnobs k = [] {
     FixedKnobs r;
-    if (const char* fe = std::getenv("MI_DFT_FIXED")) r.enabled = std::atoi(fe) != 0;
-    if (const char* fc = std::getenv("MI_DFT_FIXED_CFG")) std::sscanf(fc, "%d,%d", &r.force_tp, &r.force_t);
-    if (const char* xe = std::getenv("MI_DFT_FFT_XCD")) r.xcd = std::atoi(xe) != 0 ? 1 : 0;
+    if (const char* fe = tuning_env("MI_DFT_FIXED")) r.enabled = std::atoi(fe) != 0;
+    if (const char* fc = tuning_env("MI_DFT_FIXED_CFG")) std::sscanf(fc, "%d,%d", &r.force_tp, &r.force_t);
+    if (const char* xe = tuning_env("MI_DFT_FFT_XCD")) r.xcd = std::atoi(xe) != 0 ? 1 : 0;
     return r;
   }();
   return k;

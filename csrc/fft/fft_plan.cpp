@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <map>
 #include <sstream>
+#include "../ops/tuning.h"
 
 namespace amd_dft {
 
@@ -221,7 +222,7 @@ bool choose_tiling(PassDesc& d) {
     break;
   }
   // Tuning overrides (experiments only): MI_DFT_LOGT_ROW / MI_DFT_LOGT_COL force log2(T).
-  if (const char* e = std::getenv(col_like ? "MI_DFT_LOGT_COL" : "MI_DFT_LOGT_ROW")) {
+  if (const char* e = tuning_env(col_like ? "MI_DFT_LOGT_COL" : "MI_DFT_LOGT_ROW")) {
     const int f = std::atoi(e);
     if (f >= 0 && f <= 6 && lds_of(f) <= kMaxLdsBytes) logT = f;
   }
@@ -232,7 +233,7 @@ bool choose_tiling(PassDesc& d) {
   for (int p = 0; p < d.npass; ++p) work = std::max<int64_t>(work, (static_cast<int64_t>(d.L) << logT) / d.radix[p]);
   int64_t nt = ((work + 63) / 64) * 64;
   d.nthreads = static_cast<int32_t>(std::min<int64_t>(256, std::max<int64_t>(64, nt)));
-  if (const char* e = std::getenv("MI_DFT_THREADS")) {
+  if (const char* e = tuning_env("MI_DFT_THREADS")) {
     const int f = std::atoi(e);
     if (f >= 64 && f <= 256 && f % 64 == 0) d.nthreads = f;
   }

@@ -52,6 +52,7 @@
 #include "../fft/dev_check.h"
 #include "gelu.h"
 #include "gemm.h"
+#include "../ops/tuning.h"
 
 namespace amd_dft {
 namespace {
@@ -1066,7 +1067,7 @@ static bool split_k_ok(int64_t K) { return K % 32 == 0 && K >= 64; }
 // MI_DFT_GEMM_EPI=direct: the token-major (MODE 0 / 1) epilogue stores straight from the MFMA layout (A/B only)
 static int gemm_direct_epi() {
   static const int v = [] {
-    const char* e = std::getenv("MI_DFT_GEMM_EPI");
+    const char* e = tuning_env("MI_DFT_GEMM_EPI");
     return (e && std::string(e) == "direct") ? 1 : 0;
   }();
   return v;
@@ -1075,7 +1076,7 @@ static int gemm_direct_epi() {
 // MI_DFT_GEMM_PERSIST=1: the FourCastNet block GEMMs on a persistent grid (gemm_bf16_kernel PERSIST; A/B)
 static int gemm_persist() {
   static const int v = [] {
-    const char* e = std::getenv("MI_DFT_GEMM_PERSIST");
+    const char* e = tuning_env("MI_DFT_GEMM_PERSIST");
     return (e && std::string(e) == "1") ? 1 : 0;
   }();
   return v;

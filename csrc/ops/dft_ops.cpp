@@ -37,6 +37,7 @@
 #include "../spectral/spectral.h"
 #include "checks.h"
 #include "plan_cache.h"
+#include "tuning.h"
 
 namespace amd_dft {
 namespace {
@@ -360,7 +361,7 @@ C2RShape c2r_shape(at::IntArrayRef sizes_with_2, at::IntArrayRef dim, at::IntArr
 // (csrc/spectral/dft_gemm.hip) instead of a full Stockham FFT.  MI_DFT_GEMM=0 disables it.
 bool use_dftw(const at::Tensor& in, const DimSpec& s, at::ScalarType out_t) {
   static const bool enabled = [] {
-    const char* e = std::getenv("MI_DFT_GEMM");
+    const char* e = tuning_env("MI_DFT_GEMM");
     return !(e && std::string(e) == "0");
   }();
   if (!enabled || out_t != at::kFloat || !in.is_contiguous()) return false;
@@ -711,7 +712,7 @@ void check_ln_args(const at::Tensor& x, int64_t dim, const at::Tensor& stats, co
 // MI_DFT_NO_AFNO_W=1 (A/B, read once): LayerNorm-fused AFNO W-transforms on the generic fixed
 // Stockham kernels instead of afno_wfft.hip (same results)
 bool afno_w_enabled() {
-  static const bool on = std::getenv("MI_DFT_NO_AFNO_W") == nullptr;
+  static const bool on = tuning_env("MI_DFT_NO_AFNO_W") == nullptr;
   return on;
 }
 

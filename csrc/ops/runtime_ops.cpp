@@ -7,6 +7,7 @@
 #include <torch/library.h>
 
 #include "checks.h"
+#include "tuning.h"
 
 namespace amd_dft {
 namespace {
@@ -50,6 +51,7 @@ void fallback_reset() {
 // run-time switches (checks.h): return the previous setting
 bool set_finite_check(bool on) { return finite_check_flag().exchange(on); }
 bool set_strict(bool on) { return strict_flag().exchange(on); }
+bool is_tuning_build() { return tuning_build(); }
 
 }  // namespace
 }  // namespace amd_dft
@@ -63,4 +65,5 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("fallback_note(str op, str why) -> ()", &amd_dft::fallback_note_op);
   m.def("set_finite_check(bool on) -> bool", &amd_dft::set_finite_check);
   m.def("set_strict(bool on) -> bool", &amd_dft::set_strict);
+  m.def("tuning_build() -> bool", &amd_dft::is_tuning_build);
 }

@@ -14,6 +14,7 @@
 #include <string>
 
 #include "spectral.h"
+#include "../ops/tuning.h"
 
 namespace amd_dft {
 namespace {
@@ -589,7 +590,7 @@ void launch_layernorm(const LayerNormLaunch& p, void* stream) {
       auto* y = static_cast<uint16_t*>(p.y);
       hipStream_t s = static_cast<hipStream_t>(stream);
       static const bool dup = [] {  // MI_DFT_LN_SPLIT=dup: the duplicated-load kernel (A/B only)
-        const char* e = std::getenv("MI_DFT_LN_SPLIT");
+        const char* e = tuning_env("MI_DFT_LN_SPLIT");
         return e && std::string(e) == "dup";
       }();
       if (dup) {

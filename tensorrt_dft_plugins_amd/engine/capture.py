@@ -3,9 +3,14 @@
 Used by the benchmark and the data-parallel runner: the whole per-step forward (hundreds of
 kernels: FFT passes, fused spectral kernels, GEMMs, LayerNorms) is replayed as one graph, so
 launch overhead disappears (MI355X_MICROARCH.md: graph replay is one host call per step).
-``n_graphs > 1`` captures several copies that write distinct output buffers but share one
-memory pool, so an output can be consumed (e.g. all-gathered on another stream) while the
-next step computes into the other buffer.
+``n_graphs > 1`` captures several copies that write distinct output buffers, so an output can be
+consumed (e.g. all-gathered on another stream) while the next step computes into the other
+buffer.  Each copy has its OWN memory pool: with a shared pool, the second graph's output could be
+placed in blocks the first graph uses for its intermediates (freed to the pool when its capture
+ends, rewritten on every replay), so replaying graph 0 while graph 1's output is still being read
+on the comm stream corrupted that output (seen as a wrong self-slot in the IPC gather test, round 5).
+The price is one set of intermediates per graph -- a few GB for FourCastNet at batch 32, next to
+288 GB of HBM.
 """
 from __future__ import annotations
 
@@ -34,12 +39,10 @@ class CapturedModule:
                     module(*self.inputs)
             torch.cuda.current_stream(dev).wait_stream(s)
             torch.cuda.synchronize(dev)
-            pool = None
             for _ in range(n_graphs):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g):  # private pool per graph (see the module docstring)
                     out = self._as_list(module(*self.inputs))
-                pool = g.pool()
                 self.graphs.append(g)
                 self.outputs.append(out)
 

@@ -172,3 +172,40 @@ def test_fno2d_width64_strict(device):
         finally:
             strict_mode(prev)
     assert rel_l2(y.double().cpu(), ref.double().cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N", [64, 384])
+def test_patch_embed_ragged(device, dtype, N):
+    """Patch-embedding GEMM (the image gathered in the operand DMA) with a ragged feature panel,
+    + bias + position embedding; deterministic across calls and under hipGraph replay."""
+    from tensorrt_dft_plugins_amd.ops.spectral import split_bf16
+
+    torch.manual_seed(N)
+    B, C, h, w, p = 2, 4, 6, 12, 8
+    x = torch.randn(B, C, h * p, w * p, device=device)
+    W = torch.randn(N, C * p * p, device=device) / (C * p * p) ** 0.5
+    bias = torch.randn(N, device=device) * 0.1
+    pos = torch.randn(h * w, N, device=device) * 0.1
+    patches = x.double().reshape(B, C, h, p, w, p).permute(0, 2, 4, 1, 3, 5).reshape(B * h * w, C * p * p)
+    ref = (patches @ W.double().t() + bias.double()).reshape(B, h * w, N) + pos.double()
+
+    def run():
+        if dtype == torch.float32:
+            return torch.ops.amd_dft.patch_linear3(split_bf16(x, rows=False), split_bf16(W), bias, pos, p)
+        return torch.ops.amd_dft.patch_linear(x.to(dtype), W.to(dtype), bias, pos, p)
+
+    y = run()
+    assert rel_l2(y.double().reshape(B, h * w, N).cpu(), ref.cpu()) < (2e-5 if dtype == torch.float32 else 8e-3)
+    assert torch.equal(run(), y)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run()
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        yg = run()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(yg, y)

@@ -119,13 +119,10 @@ def test_fused_block_matches_unfused_cpu_math():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("impl", ["afno_w", "fixed"])
 @pytest.mark.parametrize("with_pre", [False, True])
-def test_ln_fused_kernels_gpu(device, with_pre, impl, recwarn, monkeypatch):
-    """Specialised-kernel paths on [B, 90, 180, 768] bf16 (the FourCastNet AFNO W-transforms):
-    the 16-byte-lane afno_wfft kernels and the generic fixed Stockham kernels (NADD = 3)."""
-    if impl == "fixed":
-        monkeypatch.setenv("MI_DFT_NO_AFNO_W", "1")
+def test_ln_fused_kernels_gpu(device, with_pre, recwarn):
+    """Specialised-kernel paths on [B, 90, 180, 768] bf16 (the FourCastNet AFNO W-transforms, the
+    16-byte-lane afno_wfft kernels; the fixed-Stockham NADD = 3 alternative is a tuning-build A/B)."""
     x, pre, g, b = _inputs(B=2, H=90, W=180, C=768, seed=2)
     xb = x.to(torch.bfloat16)
     p = pre if with_pre else None
