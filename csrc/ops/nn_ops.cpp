@@ -639,11 +639,19 @@ at::Tensor linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::o
 }
 
 // xs = split planes [2, B, C, h*p, w*p] of the fp32 image; ws [N, 2*C*p*p]; fp32 tokens [B*h*w, N]
+// patch_linear3 takes the image either as bf16 split planes [2, B, C, H, W] or as the raw fp32 image
+// [B, C, H, W] (split inside the GEMM's fragment reads: no split pass, gemm.hip MODE 3)
+bool raw_f32_image(const at::Tensor& xs) { return xs.dim() == 4 && xs.scalar_type() == at::kFloat; }
+
 at::Tensor patch_linear3_cpu(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,
                              const c10::optional<at::Tensor>& pos, int64_t p) {
-  check_split_linear(xs, ws, bias, "patch_linear3");
-  TORCH_CHECK(xs.dim() == 5 && xs.size(0) == 2, "amd_dft.patch_linear3: xs must be split planes [2, B, C, H, W]");
-  at::Tensor x = xs.select(0, 0).to(at::kFloat) + xs.select(0, 1).to(at::kFloat);
+  const bool raw = raw_f32_image(xs);
+  check_split_linear(raw ? ws : xs, ws, bias, "patch_linear3");
+  TORCH_CHECK(raw || (xs.dim() == 5 && xs.size(0) == 2),
+              "amd_dft.patch_linear3: xs must be split planes [2, B, C, H, W] or the fp32 image [B, C, H, W]");
+  // the split pair of the raw image is exactly what the GEMM multiplies (hi + lo of each value)
+  at::Tensor planes = raw ? split_ref(xs, false) : xs;
+  at::Tensor x = planes.select(0, 0).to(at::kFloat) + planes.select(0, 1).to(at::kFloat);
   at::Tensor t = patchify_cpu(x, p);
   at::Tensor y = at::linear(t, unsplit_rows(ws),
                             bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
@@ -658,10 +666,12 @@ at::Tensor patch_linear3_cpu(const at::Tensor& xs, const at::Tensor& ws, const c
 at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const c10::optional<at::Tensor>& bias,
                               const c10::optional<at::Tensor>& pos, int64_t p) {
   const c10::DeviceGuard guard(xs_.device());
-  check_split_linear(xs_, ws_, bias, "patch_linear3");
-  TORCH_CHECK(xs_.dim() == 5 && xs_.size(0) == 2 && xs_.size(3) % p == 0 && xs_.size(4) % p == 0,
-              "amd_dft.patch_linear3: xs must be split planes [2, B, C, h*p, w*p]");
-  const int64_t B = xs_.size(1), C = xs_.size(2), h = xs_.size(3) / p, w = xs_.size(4) / p, N = ws_.size(0);
+  const bool raw = raw_f32_image(xs_);
+  check_split_linear(raw ? ws_ : xs_, ws_, bias, "patch_linear3");
+  const int o = raw ? 0 : 1;  // leading plane dim of the split form
+  TORCH_CHECK((raw || (xs_.dim() == 5 && xs_.size(0) == 2)) && xs_.size(2 + o) % p == 0 && xs_.size(3 + o) % p == 0,
+              "amd_dft.patch_linear3: xs must be split planes [2, B, C, h*p, w*p] or the fp32 image [B, C, h*p, w*p]");
+  const int64_t B = xs_.size(o), C = xs_.size(1 + o), h = xs_.size(2 + o) / p, w = xs_.size(3 + o) / p, N = ws_.size(0);
   const int64_t M = B * h * w, K = C * p * p;
   TORCH_CHECK(p == 8 && ws_.size(1) == 2 * K && gemm_supported(M, N, K) && xs_.numel() < (int64_t(1) << 31),
               "amd_dft.patch_linear3: needs p == 8, ws [N, 2*C*64], N % 64 == 0 and < 2^31 image elements");
@@ -688,14 +698,16 @@ at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, cons
   g.gw = static_cast<int>(w);
   g.split = 1;
   g.out = 1;
-  g.x_lo = xs.numel() / 2;
+  g.x_lo = raw ? 0 : xs.numel() / 2;
+  g.x_f32 = raw ? 1 : 0;
   launch_gemm(g, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
   return y;
 }
 
 at::Tensor patch_linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>&,
                               const c10::optional<at::Tensor>&, int64_t p) {
-  return at::empty({xs.size(1) * (xs.size(3) / p) * (xs.size(4) / p), ws.size(0)}, xs.options().dtype(at::kFloat));
+  const int o = raw_f32_image(xs) ? 0 : 1;
+  return at::empty({xs.size(o) * (xs.size(2 + o) / p) * (xs.size(3 + o) / p), ws.size(0)}, xs.options().dtype(at::kFloat));
 }
 
 at::Tensor linear_unpatch3_cpu(const at::Tensor& ts, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,

@@ -259,11 +259,11 @@ class AFNONet(nn.Module):
             # gathers the 8x8 patches straight from the image, bias + position embedding in its
             # epilogue (no patchified copy, no separate add)
             pos = self.pos_embed.reshape(cfg.h * cfg.w, cfg.embed_dim)
-            if f32:  # bf16x3: the image as (hi, lo) planes, split weights, fp32 tokens
+            if f32:  # bf16x3: the raw fp32 image (split inside the GEMM's fragment reads), split weights
                 pe = self.patch_embed
                 ws = S.module_cached(self, "embed_split", (pe.weight,),
                                      lambda: S.split_bf16(pe.weight.reshape(cfg.embed_dim, -1)))
-                t = torch.ops.amd_dft.patch_linear3(S.split_bf16(x, rows=False), ws, pe.bias, pos, p)
+                t = torch.ops.amd_dft.patch_linear3(x.contiguous(), ws, pe.bias, pos, p)
             else:
                 wmat = self.patch_embed.weight.reshape(cfg.embed_dim, -1)
                 t = torch.ops.amd_dft.patch_linear(x, wmat, self.patch_embed.bias, pos, p)

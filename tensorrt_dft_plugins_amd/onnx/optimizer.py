@@ -116,6 +116,9 @@ class IRGraph:
             self.nodes.append(Node(n.op_type, n.domain or "", list(n.input), list(n.output), attrs,
                                    n.name or f"n{i}"))
         self.meta: Dict[str, Tuple[List[int], torch.dtype]] = {}
+        # fp32 originals of the split-pair weight constants the rewrites create (build-time only,
+        # never serialised): later passes re-derive operands from them without the split's rounding
+        self.orig: Dict[str, torch.Tensor] = {}
         self._uid = 0
 
     # ------------------------------------------------------------------ bookkeeping
@@ -428,7 +431,8 @@ class Ctx:
                     rest.append(n)
             pending = rest
             if not progress:
-                raise RuntimeError("graph has a cycle after rewriting")
+                miss = sorted({i for n in pending for i in n.inputs if i and i not in have})[:8]
+                raise RuntimeError(f"graph has a cycle after rewriting (unresolved inputs {miss})")
         self.g.nodes = out
         self.refresh()
 
@@ -631,6 +635,7 @@ def rewrite_linear(ctx: Ctx) -> None:
                 g.meta[xs] = (g.shape(x)[:-1] + [2 * K], torch.bfloat16)
                 from ..ops.spectral import split_bf16
                 ws = g.add_const("lin_ws", split_bf16(wt))
+                g.orig[ws] = wt
                 new.append(amd_node(g, "linear3", [xs, ws, bname, residual], [y], act=act, split_out=False))
             else:
                 wb = g.add_const("lin_w", wt.to(torch.bfloat16))
@@ -749,13 +754,10 @@ def rewrite_patch_embed(ctx: Ctx) -> None:
             y2 = g.fresh("pe_out")
             new = []
             wm = W.reshape(N, -1).float()
-            if dt == torch.float32:
+            if dt == torch.float32:  # the raw fp32 image: split inside the GEMM's operand reads
                 from ..ops.spectral import split_bf16
-                xs = g.fresh("pe_planes")
-                new.append(amd_node(g, "split_bf16", [x], [xs], rows=False))
-                g.meta[xs] = ([2] + g.shape(x), torch.bfloat16)
                 ws = g.add_const("pe_ws", split_bf16(wm))
-                new.append(amd_node(g, "patch_linear3", [xs, ws, bname, posn], [y], p=p))
+                new.append(amd_node(g, "patch_linear3", [x, ws, bname, posn], [y], p=p))
             else:
                 wb = g.add_const("pe_w", wm.to(torch.bfloat16))
                 new.append(amd_node(g, "patch_linear", [x, wb, bname, posn], [y], p=p))
@@ -807,6 +809,7 @@ def rewrite_unpatch_head(ctx: Ctx) -> None:
                 new.append(amd_node(g, "split_bf16", [t], [ts], rows=True))
                 g.meta[ts] = ([B, h, w, 2 * C], torch.bfloat16)
                 ws = g.add_const("head_ws", split_bf16(wcpp))
+                g.orig[ws] = wcpp
                 new.append(amd_node(g, "linear_unpatch3", [ts, ws, None], [y], C=Co, h=h, w=w, p=p))
             else:
                 wb = g.add_const("head_w", wcpp.to(torch.bfloat16))
@@ -1196,10 +1199,189 @@ def rewrite_fno(ctx: Ctx) -> None:
             ctx.report.rejected.append({"pattern": "fno_spectral", "at": rf.name, "why": str(e)})
 
 
+# ----------------------------------------------------------------------------------------- whole blocks
+def _amd(n: Optional[Node], op: str) -> bool:
+    return n is not None and n.domain == AMD_DOMAIN and n.op == op
+
+
+def _mask(n: Node) -> List[int]:
+    return list(n.attrs.get("tensor_mask", []))
+
+
+def _users(ctx: Ctx, v: str) -> List[Node]:
+    return [] if v in ctx.g.output_names else ctx.cons.get(v, [])
+
+
+def _weight_f32(g: IRGraph, ws: str) -> torch.Tensor:
+    """fp32 [N, K] weight behind a split-pair constant (the original when a rewrite recorded it)."""
+    if ws in g.orig:
+        return g.orig[ws].float()
+    from ..ops.spectral import unsplit_bf16
+    return unsplit_bf16(g.consts[ws]).float()
+
+
+def _block_nodes(ctx: Ctx, c2r: Node):
+    """The fp32 FourCastNet block around an AFNO ``c2r_add`` as the earlier passes leave it:
+    h = layer_norm(x); xw = r2c(h); yw = afno_spectral(xw); x1 = c2r_add(yw, h, x);
+    x1s = layer_norm_split(x1); hid = linear3(x1s, GELU, split out); y = linear3(hid, + b2, + x1).
+    Returns the nodes or None."""
+    g = ctx.g
+    if _mask(c2r)[:3] != [1, 1, 1] or c2r.attrs.get("out_dtype") != _SCALARTYPE[torch.float32]:
+        return None
+    yw, h, x = c2r.inputs[:3]
+    ln1, sp = ctx.producer(h), ctx.producer(yw)
+    if not _amd(ln1, "layer_norm") or ln1.outputs[0] != h or ln1.inputs[0] != x or _mask(ln1) != [1, 1, 1, 0] \
+            or _users(ctx, ln1.outputs[1]) or not _amd(sp, "afno_spectral") or _users(ctx, yw) != [c2r]:
+        return None
+    r2c = ctx.producer(sp.inputs[0])
+    if not _amd(r2c, "r2c") or r2c.inputs[0] != h or r2c.attrs.get("dim") != [2] or \
+            _users(ctx, sp.inputs[0]) != [sp] or sorted(map(id, _users(ctx, h))) != sorted([id(r2c), id(c2r)]):
+        return None
+    if r2c.attrs.get("out_dtype") != _SCALARTYPE[torch.float32] or g.dtype(x) != torch.float32 or \
+            len(g.shape(x) or []) != 4:
+        return None
+    x1 = c2r.outputs[0]
+    us = _users(ctx, x1)
+    lns = next((u for u in us if _amd(u, "layer_norm_split")), None)
+    if lns is None or len(us) != 2 or lns.inputs[0] != x1 or _mask(lns) != [1, 1, 1, 0]:
+        return None
+    fc1 = ctx.only_consumer(lns.outputs[0])
+    if not _amd(fc1, "linear3") or _mask(fc1) != [1, 1, 1, 0] or fc1.attrs.get("act") != 1 or \
+            not fc1.attrs.get("split_out"):
+        return None
+    fc2 = ctx.only_consumer(fc1.outputs[0])
+    if not _amd(fc2, "linear3") or fc2 not in us or _mask(fc2) != [1, 1, 1, 1] or fc2.inputs[3] != x1 or \
+            fc2.attrs.get("act", 0) != 0 or fc2.attrs.get("split_out"):
+        return None
+    return ln1, r2c, sp, c2r, lns, fc1, fc2
+
+
+def fuse_afno_blocks(ctx: Ctx) -> None:
+    """fp32 FourCastNet blocks -> the native block sequence (ops/spectral.py afno_block_fused_f32):
+    LN1 applied inside the W-transform's loads (``r2c_ln``; the normalised copy of x is never
+    stored), the C2R epilogue adding both skips, writing fc1's centred split pairs and LN2's
+    partial statistics (``c2r_ln_add_split``), and LN2 folded into fc1's epilogue (``linear3_ln``):
+    two full-tensor passes fewer per block.  Then, across blocks, fc2 emits the next block's LN1
+    partial statistics (``linear3_stats``) with its bias carried as the next block's ``pre``, and
+    the last fc2 writes the head's split pairs itself with its bias folded into the head's."""
+    from ..ops.spectral import split_bf16, unsplit_bf16
+
+    g = ctx.g
+    for c2r in [n for n in g.nodes if _amd(n, "c2r_add")]:
+        blk = _block_nodes(ctx, c2r)
+        if blk is None:
+            continue
+        ln1, r2c, sp, c2r, lns, fc1, fc2 = blk
+        try:
+            x, g1, b1 = ln1.inputs[:3]
+            g2, b2 = lns.inputs[1:3]
+            B, H, W, C = g.shape(x)
+            if C % 64 or C > 64 * 64:
+                raise RewriteRejected("LN partial statistics need C % 64 == 0 and C <= 4096")
+            km = r2c.attrs["keep"][0]
+            w1 = _weight_f32(g, fc1.inputs[1]).double()
+            gam, bet = g.consts[g2].double().reshape(C), g.consts[b2].double().reshape(C)
+            w1s = split_bf16((w1 * gam[None, :]).float())
+            c1 = unsplit_bf16(w1s).double().sum(1).float()
+            c2 = (w1 @ bet + g.consts[fc1.inputs[2]].double()).float()
+            n_w1s, n_c1, n_c2 = g.add_const("blk_w1s", w1s), g.add_const("blk_c1", c1), g.add_const("blk_c2", c2)
+            st, xw, yw = g.fresh("blk_st"), g.fresh("blk_xw"), g.fresh("blk_yw")
+            x1, x1s2, part2 = g.fresh("blk_x1"), g.fresh("blk_x1s2d"), g.fresh("blk_part2")
+            x1s, st2, hid, y = g.fresh("blk_x1s"), g.fresh("blk_st2"), g.fresh("blk_hid"), g.fresh("blk_y")
+            shp = g.add_const("blk_shape", torch.tensor([B, H, W, 2 * C], dtype=torch.int64))
+            new = [amd_node(g, "ln_stats", [x, None], [st], eps=ln1.attrs["eps"]),
+                   amd_node(g, "r2c_ln", [x, st, g1, b1, None], [xw], dim=2, scale=r2c.attrs["scale"], keep=km,
+                            out_dtype=torch.float32),
+                   Node(sp.op, sp.domain, [xw] + sp.inputs[1:], [yw], dict(sp.attrs), g.fresh("afno_spectral")),
+                   amd_node(g, "c2r_ln_add_split", [yw, x, st, g1, b1, None], [x1, x1s2, part2], dim=2, n=W,
+                            scale=c2r.attrs["scale"]),
+                   Node("Reshape", "", [x1s2, shp], [x1s], {}, g.fresh("reshape")),
+                   amd_node(g, "ln_stats_merge", [part2, st], [st2], eps=lns.attrs["eps"]),
+                   amd_node(g, "linear3_ln", [x1s, n_w1s, n_c1, n_c2, st2], [hid], act=1),
+                   Node(fc2.op, fc2.domain, [hid, fc2.inputs[1], fc2.inputs[2], x1], [y], dict(fc2.attrs),
+                        g.fresh("linear3"))]
+            M = B * H * W
+            for k, v in ((st, ([M, 2], torch.float32)), (xw, (g.shape(sp.inputs[0]), torch.float32)),
+                         (yw, (g.shape(sp.inputs[0]), torch.float32)), (x1, ([B, H, W, C], torch.float32)),
+                         (x1s2, ([M, 2 * C], torch.bfloat16)), (part2, ([M, C // 64, 2], torch.float32)),
+                         (x1s, ([B, H, W, 2 * C], torch.bfloat16)), (st2, ([M, 2], torch.float32)),
+                         (hid, (g.shape(fc1.outputs[0]), torch.bfloat16)), (y, g.meta[fc2.outputs[0]])):
+                g.meta[k] = v
+            old = list(blk)
+            err = _verify(ctx, old, new, [x], [fc2.outputs[0]], [y], 2e-4, scales=(1.0, 4.0))
+            ctx.replace(old, new, {fc2.outputs[0]: y})
+            ctx.report.applied.append({"pattern": "afno_block", "at": c2r.name, "rel_l2": err})
+        except RewriteRejected as e:
+            ctx.report.rejected.append({"pattern": "afno_block", "at": c2r.name, "why": str(e)})
+    _chain_afno_blocks(ctx)
+
+
+def _chain_afno_blocks(ctx: Ctx) -> None:
+    from ..ops.spectral import split_bf16
+
+    g = ctx.g
+    for fc2 in [n for n in g.nodes if _amd(n, "linear3")]:
+        if fc2 not in g.nodes or _mask(fc2) != [1, 1, 1, 1] or fc2.attrs.get("act", 0) or fc2.attrs.get("split_out"):
+            continue
+        hid, w2s, b2, res = fc2.inputs
+        v = fc2.outputs[0]
+        us = _users(ctx, v)
+        try:
+            st = next((u for u in us if _amd(u, "ln_stats")), None)
+            r2 = next((u for u in us if _amd(u, "r2c_ln")), None)
+            cs = next((u for u in us if _amd(u, "c2r_ln_add_split")), None)
+            if st is not None and r2 is not None and cs is not None and len(us) == 3 and \
+                    _mask(st) == [1, 0] and _mask(r2)[4] == 0 and _mask(cs)[5] == 0:
+                # fc2 -> next block: statistics from fc2's epilogue, bias carried as `pre`
+                sp = ctx.producer(cs.inputs[0])
+                C = g.shape(v)[-1]
+                M = math.prod(g.shape(v)) // C
+                y, part, stn = g.fresh("blk_y"), g.fresh("blk_part"), g.fresh("blk_st")
+                xw, yw = g.fresh("blk_xw"), g.fresh("blk_yw")
+                outs_cs = [g.fresh("blk_x1"), g.fresh("blk_x1s2d"), g.fresh("blk_part2")]
+                new = [amd_node(g, "linear3_stats", [hid, w2s, res, b2], [y, part]),
+                       amd_node(g, "ln_stats_merge", [part, None], [stn], eps=st.attrs["eps"]),
+                       amd_node(g, "r2c_ln", [y, stn] + r2.inputs[2:4] + [b2], [xw], dim=r2.attrs["dim"],
+                                scale=r2.attrs["scale"], keep=r2.attrs["keep"], out_dtype=torch.float32),
+                       Node(sp.op, sp.domain, [xw] + sp.inputs[1:], [yw], dict(sp.attrs), g.fresh("afno_spectral")),
+                       amd_node(g, "c2r_ln_add_split", [yw, y, stn] + cs.inputs[3:5] + [b2], outs_cs,
+                                dim=cs.attrs["dim"], n=cs.attrs["n"], scale=cs.attrs["scale"])]
+                for k, m in ((y, g.meta[v]), (part, ([M, C // 64, 2], torch.float32)), (stn, ([M, 2], torch.float32)),
+                             (xw, g.meta[r2.outputs[0]]), (yw, g.meta[sp.outputs[0]])):
+                    g.meta[k] = m
+                for a, b in zip(cs.outputs, outs_cs):
+                    g.meta[b] = g.meta[a]
+                old = [fc2, st, r2, sp, cs]
+                err = _verify(ctx, old, new, [hid, res], cs.outputs, outs_cs, 2e-4)
+                ctx.replace(old, new, dict(zip(cs.outputs, outs_cs), **{st.outputs[0]: stn}))
+                ctx.report.applied.append({"pattern": "afno_block_chain", "at": fc2.name, "rel_l2": err})
+                continue
+            sp_ = us[0] if len(us) == 1 and _amd(us[0], "split_bf16") and us[0].attrs.get("rows", True) else None
+            head = ctx.only_consumer(sp_.outputs[0]) if sp_ is not None else None
+            if _amd(head, "linear_unpatch3"):
+                # last fc2 -> head: split pairs straight from fc2, its bias folded into the head's
+                hws = head.inputs[1]
+                hb = g.consts[head.inputs[2]].double() if _mask(head)[2] else 0.0
+                bias = (_weight_f32(g, hws).double() @ g.consts[b2].double() + hb).float()
+                ys, hy = g.fresh("blk_ys"), g.fresh("head_out")
+                new = [amd_node(g, "linear3", [hid, w2s, None, res], [ys], act=0, split_out=True),
+                       Node(head.op, head.domain, [ys, hws, g.add_const("head_b", bias)], [hy],
+                            dict(head.attrs, tensor_mask=[1, 1, 1]), g.fresh("linear_unpatch3"))]
+                g.meta[ys] = g.meta[sp_.outputs[0]]
+                g.meta[hy] = g.meta[head.outputs[0]]
+                old = [fc2, sp_, head]
+                err = _verify(ctx, old, new, [hid, res], [head.outputs[0]], [hy], 2e-4)
+                ctx.replace(old, new, {head.outputs[0]: hy})
+                ctx.report.applied.append({"pattern": "afno_block_head", "at": fc2.name, "rel_l2": err})
+        except RewriteRejected as e:
+            ctx.report.rejected.append({"pattern": "afno_block_chain", "at": fc2.name, "why": str(e)})
+
+
 # ----------------------------------------------------------------------------------------- driver
 PASSES = (("afno_filter", rewrite_afno), ("fno_spectral", rewrite_fno), ("layer_norm", rewrite_layernorm),
           ("patch_embed", rewrite_patch_embed), ("unpatch_head", rewrite_unpatch_head), ("linear", rewrite_linear),
-          ("pointwise_conv", rewrite_pointwise_conv), ("split_fusion", fuse_split_chains))
+          ("pointwise_conv", rewrite_pointwise_conv), ("split_fusion", fuse_split_chains),
+          ("afno_block", fuse_afno_blocks))
 
 
 def optimize(onnx_bytes: bytes, input_shapes: Sequence[Sequence[int]], input_dtypes=None, device=None,

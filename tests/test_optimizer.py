@@ -86,9 +86,14 @@ def test_optimizer_rewrites_contrib_fourcastnet():
     assert rep.count("split_fused_layer_norm_split") == 2 and rep.count("split_fused_linear3") == 2
     # both AFNO skips (filter input and block residual) fused into the C2R store
     assert all(a["skips"] == 2 for a in rep.applied if a["pattern"] == "afno_filter")
+    # whole blocks in the native fp32 sequence: LN1 inside the W-transform, both skips + fc1's split
+    # pairs + LN2 partials in the C2R epilogue, LN2 folded into fc1, LN1 statistics from fc2
+    assert rep.count("afno_block") == 2 and rep.count("afno_block_chain") == 1 and rep.count("afno_block_head") == 1
     ops = [o for d, o in _ops(od)]
     assert "Rfft" not in ops and "Einsum" not in ops and "MatMul" not in ops
-    assert ops.count("afno_spectral") == 2 and ops.count("linear3") == 4
+    assert ops.count("afno_spectral") == 2 and ops.count("r2c_ln") == 2 and ops.count("c2r_ln_add_split") == 2
+    assert ops.count("linear3_ln") == 2 and ops.count("linear3_stats") == 1 and ops.count("linear3") == 1
+    assert "layer_norm" not in ops and "layer_norm_split" not in ops and "split_bf16" not in ops
     assert rep.nodes_after < rep.nodes_before // 5
     (y,) = OnnxGraph(od, device="cpu").run(x)
     assert _rel(y, want) < 2e-5

@@ -46,6 +46,8 @@ def test_contrib_fourcastnet_engine_full_size(fcn_pair, tmp_path):
     assert opt["applied"].get("afno_filter") == 2 and opt["applied"].get("layer_norm") == 4, opt
     assert opt["applied"].get("linear_gelu") == 2 and opt["applied"].get("linear_residual") == 2, opt
     assert opt["applied"].get("patch_embed") == 1 and opt["applied"].get("unpatch_head") == 1, opt
+    assert opt["applied"].get("afno_block") == 2 and opt["applied"].get("afno_block_chain") == 1, opt
+    assert opt["applied"].get("afno_block_head") == 1, opt
     assert not opt["rejected"], opt["rejected"]
     p = str(tmp_path / "fcn_contrib.engine")
     eng.save(p)

@@ -77,3 +77,19 @@ def test_linear_unpatch_kernel_gpu(device, B, h, w, with_bias):
     y = ops.linear_unpatch(t.to(device), wt.to(device), None if bias is None else bias.to(device), C, h, w, p)
     assert y.dtype == torch.bfloat16 and y.shape == (B, C, h * p, w * p)
     assert rel_l2(y, _head_ref(t, wt, bias, C, h, w, p)) < 1e-2
+
+
+def test_patch_linear3_raw_image_cpu_semantics():
+    """patch_linear3 on the raw fp32 image equals the split-planes form (CPU reference ops)."""
+    import torch
+
+    from tensorrt_dft_plugins_amd.ops.spectral import split_bf16
+
+    torch.manual_seed(3)
+    x = torch.randn(2, 3, 16, 24)
+    W = torch.randn(64, 3 * 64) * 0.1
+    b, pos = torch.randn(64), torch.randn(2 * 3, 64)
+    y_raw = torch.ops.amd_dft.patch_linear3(x, split_bf16(W), b, pos, 8)
+    y_split = torch.ops.amd_dft.patch_linear3(split_bf16(x, rows=False), split_bf16(W), b, pos, 8)
+    assert torch.allclose(y_raw, y_split, atol=1e-6)
+    assert y_raw.shape == (2 * 2 * 3, 64)
