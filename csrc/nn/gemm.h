@@ -20,7 +20,6 @@ struct GemmLaunch {
   int split = 0;
   int out = 0;               // 0 bf16, 1 fp32, 2 split pair [hi(N) | lo(N)] (split mode only)
   int64_t x_lo = 0;
-  int x_f32 = 0;             // patch gather + split: x is the RAW fp32 image, split on the fragment read
   // Patch-embedding gather (x is an image [B, gC, gh*8, gw*8]; token t = (b, i, j) reads its
   // 8x8 patch of every channel, feature order (c, py, px): one 16-byte chunk per (c, py)).
   int gC = 0, gh = 0, gw = 0;

@@ -106,18 +106,11 @@ __device__ __forceinline__ int region_row(int r) {
 #define GEMM_DMA_DWORD 0  // timing-only ablation: bit R = region R's DMA moves 4 instead of 16 bytes per lane
 #endif                    // (same instructions and vmcnt counts, a quarter of the bytes: power vs operand traffic)
 // NPC: pieces (8-row instructions) per calling wave; wave = the caller's slot (rows 8 NPC wave ..)
-// MODE 3 (fp32 patch embedding, SPLIT only): the token operand is gathered from the RAW fp32 image
-// -- a 32-deep K-tile kt is channel kt / 2, patch rows (kt & 1) * 4 .. + 3, i.e. 32 fp32 = the same
-// 128 bytes per token row as the [hi | lo] pair row of MODE 1; 16-byte chunk c = half a patch row
-// (py = (kt & 1) * 4 + c / 2, px = 4 (c & 1) ..).  read_b_f32 splits the fp32 values into the hi /
-// lo bf16 fragments when it reads them, so no split copy of the image is ever written (round 5:
-// the separate split pass was 0.9 ms of the fp32 step).
 template <int REG, int MODE, bool SPLIT, bool OPQ = false, bool ASM = false, int NPC = 2>
 __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, const uint16_t* __restrict__ X,
                                              int64_t K, int f0, int t0, int M, int kt, char* stage, int wave,
                                              int lane, const GemmLaunch& p, const int (&gb)[2][2]) {
-  static_assert(NPC == 2 || (MODE != 1 && MODE != 3), "gathered token rows: 2 pieces per wave");
-  static_assert(MODE != 3 || SPLIT, "the raw fp32 image gather feeds the split (bf16x3) GEMM");
+  static_assert(NPC == 2 || MODE != 1, "gathered token rows: 2 pieces per wave");
   if constexpr (OPQ) asm volatile("" : "+v"(lane));
   char* dst = stage + REG * kRegion;
   // SPLIT: K-tile kt = logical k [32 kt, 32 kt + 32); its hi and lo halves are adjacent in the
@@ -137,10 +130,6 @@ __device__ __forceinline__ void stage_region(const uint16_t* __restrict__ W, con
       // outputs are never stored; for full panels the clamp is a no-op
       const uint16_t* base = W + static_cast<int64_t>(f0) * ld + kt * kBK;  // uniform
       g = base + static_cast<uint32_t>(min(tr, p.N - 1 - f0) * static_cast<int>(ld) + chunk * 8);
-    } else if constexpr (MODE == 3) {  // raw fp32 image, element offsets (gb as for MODE 1)
-      const int py = (kt & 1) * 4 + (chunk >> 1);
-      g = reinterpret_cast<const uint16_t*>(reinterpret_cast<const float*>(X) +
-                                            (gb[REG - 1][i] + ((kt >> 1) * (p.gh * 8) + py) * (p.gw * 8) + (chunk & 1) * 4));
     } else if constexpr (MODE == 1) {  // gb: this lane's token base offsets (32-bit, host-checked)
       if constexpr (SPLIT) {  // channel kt / 2, patch rows (kt & 1) * 4 + c % 4 of the hi / lo plane
         const int py = (kt & 1) * 4 + (chunk & 3);
@@ -184,34 +173,6 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       b[s * 2 + j] = *reinterpret_cast<const bf16x8*>(base + swz(wc * 32 + j * 16 + r16, s * 4 + kq));
-}
-
-// MODE 3: the region row holds 32 fp32 k-values of one token; lane kq needs k = 8 kq .. 8 kq + 7 =
-// chunks 2 kq, 2 kq + 1.  Returns them as the (hi, lo) bf16 fragments read_b delivers in SPLIT mode
-// (b[j] = hi, b[2 + j] = lo).
-template <int REG>
-__device__ __forceinline__ void read_b_f32(bf16x8 (&b)[4], const char* stage, int wc, int r16, int kq) {
-  const char* base = stage + REG * kRegion;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = wc * 32 + j * 16 + r16;
-    const float4 u0 = *reinterpret_cast<const float4*>(base + swz(row, 2 * kq));
-    const float4 u1 = *reinterpret_cast<const float4*>(base + swz(row, 2 * kq + 1));
-    const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      hi[q] = pk_bf16(v[2 * q], v[2 * q + 1]);
-      lo[q] = pk_bf16(v[2 * q] - __uint_as_float(hi[q] << 16), v[2 * q + 1] - __uint_as_float(hi[q] & 0xffff0000u));
-    }
-    b[j] = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
-    b[2 + j] = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
-  }
-}
-template <int MODE, int REG>
-__device__ __forceinline__ void read_b_any(bf16x8 (&b)[4], const char* stage, int wc, int r16, int kq) {
-  if constexpr (MODE == 3) read_b_f32<REG>(b, stage, wc, r16, kq);
-  else read_b<REG>(b, stage, wc, r16, kq);
 }
 
 // bf16: k-steps 0 and 1.  SPLIT: fragments [0..3] / [4..7] of A and [0..1] / [2..3] of B are
@@ -391,9 +352,9 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   constexpr int kEpiVm = 2 * kNitE * ((OUT == 2 ? 2 : 1) + (RES ? (OUT == 2 ? 2 : 1) : 0) + (STATS ? 1 : 0));
   constexpr int kRelaxed = kEpiVm + 4 < 63 ? kEpiVm + 4 : 63;
 
-  // MODE 1 / 3: per-lane token base offsets of the gathered image rows (regions 1, 2 x 2 pieces)
+  // MODE 1: per-lane token base offsets of the gathered image rows (regions 1, 2 x 2 pieces)
   int gb[2][2] = {{0, 0}, {0, 0}};
-  if constexpr (MODE == 1 || MODE == 3) {
+  if constexpr (MODE == 1) {
     const int hw = p.gh * p.gw, rowlen = p.gw * 8;
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -408,7 +369,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
       }
   }
   // HALF: two-phase K-tile schedule (see the main loop); wave group as a scalar for its branches
-  constexpr bool HALF = ((GEMM_HALF >> (SPLIT ? 1 : 0)) & 1) && !PERSIST && MODE != 1 && MODE != 3;
+  constexpr bool HALF = ((GEMM_HALF >> (SPLIT ? 1 : 0)) & 1) && !PERSIST && MODE != 1;
   const int wrs = __builtin_amdgcn_readfirstlane(wr);
   // HALF batch(kt): R0 (each group its own feature rows) + R1 / R2 (all token rows, wave group 1 only)
   auto half_batch = [&](int kt, char* st) {
@@ -480,7 +441,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
     };
     auto res_off = [&](int i, int j) -> int64_t {
       const int f = f0 + wr * 128 + i * 16 + 4 * kq;
-      if constexpr (MODE == 1 || MODE == 3) {
+      if constexpr (MODE == 1) {
         if (p.res_rows > 0) return static_cast<int64_t>(tokc(j) % p.res_rows) * N + f;
       }
       return out_off(i, j);
@@ -550,7 +511,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         if (!(GEMM_ABLATE & 1) && issued(P)) stage_region<1, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
       };
       if (!GEMM_DMA_MID) dma0();
-      if (!(GEMM_ABLATE & 2)) read_b_any<MODE, 1>(b0, cur, wc, r16, kq);
+      if (!(GEMM_ABLATE & 2)) read_b<1>(b0, cur, wc, r16, kq);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_quadrant<0, 0, SPLIT>(acc, a0, b0, dma0);
@@ -562,7 +523,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         if (!(GEMM_ABLATE & 1) && issued(P + 1)) stage_region<2, MODE, SPLIT, PERSIST>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
       };
       if (!GEMM_DMA_MID) dma1();
-      if (!(GEMM_ABLATE & 2)) read_b_any<MODE, 2>(b1, cur, wc, r16, kq);
+      if (!(GEMM_ABLATE & 2)) read_b<2>(b1, cur, wc, r16, kq);
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_quadrant<0, 1, SPLIT>(acc, a0, b1, dma1);
@@ -669,7 +630,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           constexpr int PD = (OUT == 2 || PERSIST) ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
           auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
             int rt = min(tbase + it * RPI + rsub, M - 1);
-            if constexpr (MODE == 1 || MODE == 3) {
+            if constexpr (MODE == 1) {
               if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
             }
             if constexpr (OUT == 2) {
@@ -1165,12 +1126,7 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
         throw std::runtime_error("amd_dft: gemm: patch gather needs K = C*64 and M = B*h*w");
       if (static_cast<int64_t>(p.M) * p.K >= (int64_t(1) << 31) || (p.split && p.x_lo + static_cast<int64_t>(p.M) * p.K >= (int64_t(1) << 31)))
         throw std::runtime_error("amd_dft: gemm: patch gather uses 32-bit offsets");
-      if (p.split && p.x_f32) {  // raw fp32 image, split on the fragment read (MODE 3)
-        if (bias && p.residual) launch_one<0, true, true, false, 3, true, 1>(p, st, grid);
-        else if (bias) launch_one<0, true, false, false, 3, true, 1>(p, st, grid);
-        else if (p.residual) launch_one<0, false, true, false, 3, true, 1>(p, st, grid);
-        else launch_one<0, false, false, false, 3, true, 1>(p, st, grid);
-      } else if (p.split) {
+      if (p.split) {
         if (bias && p.residual) launch_one<0, true, true, false, 1, true, 1>(p, st, grid);
         else if (bias) launch_one<0, true, false, false, 1, true, 1>(p, st, grid);
         else if (p.residual) launch_one<0, false, true, false, 1, true, 1>(p, st, grid);

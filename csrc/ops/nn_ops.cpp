@@ -640,7 +640,9 @@ at::Tensor linear3_meta(const at::Tensor& xs, const at::Tensor& ws, const c10::o
 
 // xs = split planes [2, B, C, h*p, w*p] of the fp32 image; ws [N, 2*C*p*p]; fp32 tokens [B*h*w, N]
 // patch_linear3 takes the image either as bf16 split planes [2, B, C, H, W] or as the raw fp32 image
-// [B, C, H, W] (split inside the GEMM's fragment reads: no split pass, gemm.hip MODE 3)
+// [B, C, H, W] (split here first).  Round 5 measured folding that split into the GEMM's fragment reads
+// (the raw fp32 gathered into LDS, split per read): the embed GEMM went from 2.32 to 4.69 ms, more
+// than the 0.90 ms split pass it removed (profiles/patch_embed_raw_f32_r5.txt), so the pass stays.
 bool raw_f32_image(const at::Tensor& xs) { return xs.dim() == 4 && xs.scalar_type() == at::kFloat; }
 
 at::Tensor patch_linear3_cpu(const at::Tensor& xs, const at::Tensor& ws, const c10::optional<at::Tensor>& bias,
@@ -675,7 +677,7 @@ at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, cons
   const int64_t M = B * h * w, K = C * p * p;
   TORCH_CHECK(p == 8 && ws_.size(1) == 2 * K && gemm_supported(M, N, K) && xs_.numel() < (int64_t(1) << 31),
               "amd_dft.patch_linear3: needs p == 8, ws [N, 2*C*64], N % 64 == 0 and < 2^31 image elements");
-  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous();
+  at::Tensor xs = raw ? split_bf16_cuda(xs_, false) : xs_.contiguous(), ws = ws_.contiguous();
   at::Tensor y = at::empty({M, N}, xs.options().dtype(at::kFloat));
   at::Tensor b, r;
   if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
@@ -698,8 +700,7 @@ at::Tensor patch_linear3_cuda(const at::Tensor& xs_, const at::Tensor& ws_, cons
   g.gw = static_cast<int>(w);
   g.split = 1;
   g.out = 1;
-  g.x_lo = raw ? 0 : xs.numel() / 2;
-  g.x_f32 = raw ? 1 : 0;
+  g.x_lo = xs.numel() / 2;
   launch_gemm(g, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
   return y;
 }

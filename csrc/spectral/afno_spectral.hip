@@ -103,8 +103,13 @@ struct AfnoShape {
   // x3: fp32 staging | hi + lo planes), then the pass-1 twiddles (TWN float2, copied from the plan
   // table at kernel start: an LDS read instead of an L2 round trip after each pass-1 barrier)
   static constexpr int TWN = (R1 - 1) * R0;
-  static constexpr int64_t MAIN16 = L * BS * 4 > 32 * MT * APitch ? L * BS * 4 : 32 * MT * APitch;
-  static constexpr int64_t MAIN32 = 2 * L * BS * 4 > 64 * MT * APitch ? 2 * L * BS * 4 : 64 * MT * APitch;
+  // row pitch (complex elements) of the GEMM-2 output staging X: the epilogue writes 4 consecutive
+  // values (two channels' re, im) of one row per lane, 16 lanes on 16 rows, so the pitch is padded
+  // off a multiple of the bank row (fp16 rows shift by 2 banks, fp32 rows by 4: conflict-free)
+  static constexpr int XP = BS + 2;
+  static constexpr int64_t cmax(int64_t a, int64_t b) { return a > b ? a : b; }
+  static constexpr int64_t MAIN16 = cmax(cmax(L * BS * 4, L * XP * 4), 32 * MT * APitch);
+  static constexpr int64_t MAIN32 = cmax(cmax(2 * L * BS * 4, 2 * L * XP * 4), 64 * MT * APitch);
   static constexpr int64_t LDS16 = MAIN16 + TWN * 8, LDS32 = MAIN32 + TWN * 8;
   static_assert(R0 * R1 == L && BS % 16 == 0 && L <= 128, "AFNO instance geometry");
 };
@@ -199,7 +204,13 @@ struct AfnoArgs {
 #ifndef AFNO_X3_T
 #define AFNO_X3_T 1
 #endif
-template <class S, bool TR = false>
+// PERM: output column n' of the tile computes weight row (n' & 1) BS + (n' >> 1), i.e. the
+// columns come out as interleaved (re, im) pairs of each channel (GEMM 2: with TR a lane then holds
+// two channels' complex values of one row, one 8 / 16-byte LDS write)
+template <class S, bool PERM>
+__device__ __forceinline__ int brow(int n) { return PERM ? (n & 1) * S::BS + (n >> 1) : n; }
+
+template <class S, bool TR = false, bool PERM = false>
 __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
                                           f32x4 (&acc)[S::MT][S::NTW]) {
   const int lane = threadIdx.x & 63;
@@ -216,14 +227,14 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
   for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj)
-      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + (S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
+      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
     if (ks + D < S::KS) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj)
         bq[(ks + D) % NQ][nj] =
-            *reinterpret_cast<const bf16x8*>(Bt + (S::ct(w, nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
+            *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of its use (see gemm_tile_x3)
     bf16x8 afr[S::MT];
@@ -356,33 +367,34 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
     }
   }
   __syncthreads();
-  // ---------------- GEMM2 + bias + softshrink -> X (fp16 complex, conjugated for the inverse)
-  gemm_tile<S>(A, w2t, acc);
+  // ---------------- GEMM2 + bias + softshrink -> X (fp16 complex, conjugated for the inverse):
+  // transposed tile with (re, im)-interleaved columns, so a lane holds channels c0, c0 + 1 of one
+  // row and writes them as one 8-byte piece (row pitch XP)
+  gemm_tile<S, true, true>(A, w2t, acc);
   __syncthreads();
-  _Float16* X = reinterpret_cast<_Float16*>(lds);
   const float lam = a.lambda;
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
     if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
-    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
-    const float bias = b2[n];
-    const int c = n < BS ? n : n - BS;
-    const int part = n < BS ? 0 : 1;
-    const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
+    const int c0 = ((S::NTW * w + nj) * 16 + 4 * (lane >> 4)) >> 1;
+    const float2 bre = *reinterpret_cast<const float2*>(b2 + c0), bim = *reinterpret_cast<const float2*>(b2 + BS + c0);
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mi * 16 + 4 * (lane >> 4) + i;
-        if (m < L) {
-          const float v = acc[mi][nj][i] + bias;
-          const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
-          X[(m * BS + c) * 2 + part] = static_cast<_Float16>(sgn * s);
-        }
+    for (int mi = 0; mi < S::MT; ++mi) {
+      const int m = mi * 16 + (lane & 15);
+      if (m < L) {
+        const float v0 = acc[mi][nj][0] + bre.x, v1 = acc[mi][nj][1] + bim.x;
+        const float v2 = acc[mi][nj][2] + bre.y, v3 = acc[mi][nj][3] + bim.y;
+        // softshrink; conj(Z) for the forward-FFT-as-inverse trick
+        *reinterpret_cast<h4_t*>(lds + m * S::XP + c0) =
+            h4_t{static_cast<_Float16>(v0 - __builtin_amdgcn_fmed3f(v0, -lam, lam)),
+                 static_cast<_Float16>(__builtin_amdgcn_fmed3f(v1, -lam, lam) - v1),
+                 static_cast<_Float16>(v2 - __builtin_amdgcn_fmed3f(v2, -lam, lam)),
+                 static_cast<_Float16>(__builtin_amdgcn_fmed3f(v3, -lam, lam) - v3)};
       }
+    }
   }
   __syncthreads();
-  // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
+  // ---------------- inverse FFT_H (conj trick): pass 0 LDS (pitch XP) -> LDS (pitch BS)
   {
     cpair v[P0::Q][R0];
 #pragma unroll
@@ -391,7 +403,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_hp(lds, (j + r * P0::LR) * BS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_hp(lds, (j + r * P0::LR) * S::XP + 2 * tp);
       }
     }
     __syncthreads();
@@ -486,7 +498,7 @@ __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx
 // TR: the same products with the MFMA operands swapped, so the accumulator tile is the transpose:
 // a lane holds 4 CONSECUTIVE output columns n of one row m (instead of 4 rows of one column) --
 // the epilogue then writes 8-byte bf16x4 pieces instead of single bf16 values.
-template <class S, bool TR = false>
+template <class S, bool TR = false, bool PERM = false>
 __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
                                              const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
   constexpr int K2 = 2 * S::K;  // split weight row: k32-interleaved [hi(32) | lo(32)] chunks
@@ -507,7 +519,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
   for (int s2 = 0; s2 < D; ++s2)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) {
-      const uint16_t* row = Bt + (S::ct(w, nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
+      const uint16_t* row = Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
       bh[s2][nj] = *reinterpret_cast<const bf16x8*>(row);
       bl[s2][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
     }
@@ -516,7 +528,7 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
     if (ks + D < S::KS) {
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
-        const uint16_t* row = Bt + (S::ct(w, nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
+        const uint16_t* row = Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * K2 + (ks + D) * 64 + kq * 8;
         bh[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row);
         bl[(ks + D) % NQ][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
       }
@@ -551,7 +563,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
   constexpr int plane = 16 * S::MT * AP;                         // bf16 elements per A plane
   constexpr int64_t LDSB = S::MAIN32;  // the staging / A-plane area (twiddles follow it)
-  static_assert(S::MAIN32 == ((2LL * L * BS * 4 > 4LL * plane) ? 2LL * L * BS * 4 : 4LL * plane), "x3 LDS layout");
+  static_assert(S::MAIN32 >= 2LL * L * S::XP * 4 && S::MAIN32 >= 4LL * plane, "x3 LDS layout");
   extern __shared__ __attribute__((aligned(16))) float2 ldsf[];  // [L][BS] complex fp32
   uint16_t* Ah = reinterpret_cast<uint16_t*>(ldsf);              // aliases: [16 MT][APitch] bf16 hi
   uint16_t* Al = Ah + plane;                                     //          [16 MT][APitch] bf16 lo
@@ -665,34 +677,33 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   }
   __syncthreads();
   AFNO_STAMP(6, __builtin_amdgcn_s_memtime());
-  gemm_tile_x3<S>(Ah, Al, w2t, acc);
+  // transposed tile, (re, im)-interleaved columns: one 16-byte write of two channels per lane and row
+  gemm_tile_x3<S, true, true>(Ah, Al, w2t, acc);
   __syncthreads();
   AFNO_STAMP(7, __builtin_amdgcn_s_memtime());
-  float* X = reinterpret_cast<float*>(ldsf);
   const float lam = a.lambda;
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
     if (!S::ct_live(w, nj)) continue;  // wave-uniform (BS % 32 != 0 only)
-    const int n = (S::NTW * w + nj) * 16 + (lane & 15);
-    const float bias = b2[n];
-    const int c = n < BS ? n : n - BS;
-    const int part = n < BS ? 0 : 1;
-    const float sgn = part ? -1.f : 1.f;  // conj(Z) for the forward-FFT-as-inverse trick
+    const int c0 = ((S::NTW * w + nj) * 16 + 4 * (lane >> 4)) >> 1;
+    const float2 bre = *reinterpret_cast<const float2*>(b2 + c0), bim = *reinterpret_cast<const float2*>(b2 + BS + c0);
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mi * 16 + 4 * (lane >> 4) + i;
-        if (m < L) {
-          const float v = acc[mi][nj][i] + bias;
-          const float s = v - __builtin_amdgcn_fmed3f(v, -lam, lam);  // softshrink
-          X[(m * BS + c) * 2 + part] = sgn * s;
-        }
+    for (int mi = 0; mi < S::MT; ++mi) {
+      const int m = mi * 16 + (lane & 15);
+      if (m < L) {
+        const float v0 = acc[mi][nj][0] + bre.x, v1 = acc[mi][nj][1] + bim.x;
+        const float v2 = acc[mi][nj][2] + bre.y, v3 = acc[mi][nj][3] + bim.y;
+        // softshrink; conj(Z) for the forward-FFT-as-inverse trick
+        AMD_DFT_DEV_LDS(static_cast<int64_t>(m * S::XP + c0) * 8, 16, LDSB, "afno x3 epilogue 2");
+        *reinterpret_cast<float4*>(ldsf + m * S::XP + c0) =
+            make_float4(v0 - __builtin_amdgcn_fmed3f(v0, -lam, lam), __builtin_amdgcn_fmed3f(v1, -lam, lam) - v1,
+                        v2 - __builtin_amdgcn_fmed3f(v2, -lam, lam), __builtin_amdgcn_fmed3f(v3, -lam, lam) - v3);
       }
+    }
   }
   __syncthreads();
   AFNO_STAMP(8, __builtin_amdgcn_s_memtime());
-  // ---------------- inverse FFT_H (conj trick): pass 0 LDS -> LDS
+  // ---------------- inverse FFT_H (conj trick): pass 0 LDS (pitch XP) -> LDS (pitch BS)
   {
     cpair v[P0::Q][R0];
 #pragma unroll
@@ -701,7 +712,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
       if (P0::NB % kNT == 0 || bb < P0::NB) {
         const int tp = bb % NP, j = bb / NP;
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * BS + 2 * tp);
+        for (int r = 0; r < R0; ++r) v[q][r] = ld_fp<LDSB>(ldsf, (j + r * P0::LR) * S::XP + 2 * tp);
       }
     }
     __syncthreads();

@@ -259,7 +259,7 @@ class AFNONet(nn.Module):
             # gathers the 8x8 patches straight from the image, bias + position embedding in its
             # epilogue (no patchified copy, no separate add)
             pos = self.pos_embed.reshape(cfg.h * cfg.w, cfg.embed_dim)
-            if f32:  # bf16x3: the raw fp32 image (split inside the GEMM's fragment reads), split weights
+            if f32:  # bf16x3: the raw fp32 image (split into bf16 planes by the op), split weights
                 pe = self.patch_embed
                 ws = S.module_cached(self, "embed_split", (pe.weight,),
                                      lambda: S.split_bf16(pe.weight.reshape(cfg.embed_dim, -1)))

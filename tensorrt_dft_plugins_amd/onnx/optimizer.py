@@ -754,7 +754,7 @@ def rewrite_patch_embed(ctx: Ctx) -> None:
             y2 = g.fresh("pe_out")
             new = []
             wm = W.reshape(N, -1).float()
-            if dt == torch.float32:  # the raw fp32 image: split inside the GEMM's operand reads
+            if dt == torch.float32:  # the raw fp32 image (the op splits it into bf16 planes)
                 from ..ops.spectral import split_bf16
                 ws = g.add_const("pe_ws", split_bf16(wm))
                 new.append(amd_node(g, "patch_linear3", [x, ws, bname, posn], [y], p=p))

@@ -191,7 +191,7 @@ def test_patch_embed_ragged(device, dtype, N):
     ref = (patches @ W.double().t() + bias.double()).reshape(B, h * w, N) + pos.double()
 
     def run():
-        if dtype == "raw32":  # the fp32 image split inside the GEMM's fragment reads (gemm.hip MODE 3)
+        if dtype == "raw32":  # the raw fp32 image (the op splits it)
             return torch.ops.amd_dft.patch_linear3(x, split_bf16(W), bias, pos, p)
         if dtype == torch.float32:
             return torch.ops.amd_dft.patch_linear3(split_bf16(x, rows=False), split_bf16(W), bias, pos, p)
