@@ -76,7 +76,7 @@ def sources():
 
 
 # bump when the compile / link command lines below change (part of the source digest)
-_FLAGS_VERSION = "r4-1"
+_FLAGS_VERSION = "r5-1"
 _DIGEST_MARK = b"amd_dft_source_digest="
 
 
@@ -214,6 +214,9 @@ def _compile(src: str, needs_torch: bool, tinc, abi: int, asan: bool = False, ob
         # host-only C++ that includes HIP runtime headers (torch's c10/hip)
         rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
         cmd += ["-x", "c++", "-I" + os.path.join(rocm, "include"), "-D__HIP_PLATFORM_AMD__=1"]
+        # the -D switches of MI_DFT_HIPCC_EXTRA (e.g. -DAMD_DFT_TUNING=1: the kernel-selection knobs
+        # in the host code, csrc/ops/tuning.h) reach the host objects too
+        cmd += [f for f in os.environ.get("MI_DFT_HIPCC_EXTRA", "").split() if f.startswith("-D")]
         if asan:
             cmd += ASAN_FLAGS
     if needs_torch:
