@@ -9,6 +9,7 @@
 //   _ipc_mem_handle / _ipc_open_mem / _ipc_close_mem      hipIpc{Get,Open,Close}MemHandle
 //   _ipc_event_*    inter-process events (hipEventInterprocess): record on the producer's
 //                   stream, hipStreamWaitEvent on the consumer's
+//   _ipc_write_value / _ipc_wait_value   stream-ordered flag words (hipStreamWrite/WaitValue32)
 //   _ipc_push       one kernel copying a source to N destination pointers concurrently on
 //                   the current stream (peer stores over xGMI, one link per destination)
 // Names start with '_' so they are never exported into ONNX graphs (raw device pointers).
@@ -109,6 +110,24 @@ void ipc_stream_wait(int64_t ev, int64_t device) {
 
 void ipc_event_destroy(int64_t ev) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)); }
 
+// Stream-ordered 32-bit flag write / wait (the counted gather protocol: no host handshake).  The
+// write runs on the command processor after everything enqueued before it on the current stream;
+// the wait blocks the stream (not the host, not a CU) until *ptr >= value.  ptr: a hipMalloc'd
+// flag word of this process or one mapped from a peer (hipIpcOpenMemHandle).
+void ipc_write_value(int64_t ptr, int64_t value, int64_t device) {
+  TORCH_CHECK(ptr != 0 && ptr % 4 == 0 && value >= 0 && value <= 0xffffffffLL, "amd_dft._ipc_write_value: bad flag");
+  auto st = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device)).stream();
+  hip_ok(hipStreamWriteValue32(st, reinterpret_cast<void*>(ptr), static_cast<uint32_t>(value), 0), "_ipc_write_value");
+}
+
+void ipc_wait_value(int64_t ptr, int64_t value, int64_t device) {
+  TORCH_CHECK(ptr != 0 && ptr % 4 == 0 && value >= 0 && value <= 0xffffffffLL, "amd_dft._ipc_wait_value: bad flag");
+  auto st = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device)).stream();
+  hip_ok(hipStreamWaitValue32(st, reinterpret_cast<void*>(ptr), static_cast<uint32_t>(value), hipStreamWaitValueGte,
+                              0xffffffffu),
+         "_ipc_wait_value");
+}
+
 // src -> every dst_ptrs[i] + offset (bytes), stream-ordered on the current stream: one kernel,
 // all destinations concurrently (csrc/parallel/ipc_push.hip); hipMemcpyAsync fallback for
 // unaligned sizes
@@ -148,5 +167,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("_ipc_event_record(int ev, int device) -> ()", &amd_dft::ipc_event_record);
   m.def("_ipc_stream_wait(int ev, int device) -> ()", &amd_dft::ipc_stream_wait);
   m.def("_ipc_event_destroy(int ev) -> ()", &amd_dft::ipc_event_destroy);
+  m.def("_ipc_write_value(int ptr, int value, int device) -> ()", &amd_dft::ipc_write_value);
+  m.def("_ipc_wait_value(int ptr, int value, int device) -> ()", &amd_dft::ipc_wait_value);
   m.def("_ipc_push(Tensor src, int[] dst_ptrs, int offset) -> ()", &amd_dft::ipc_push);
 }

@@ -10,7 +10,6 @@
 #include <unordered_map>
 
 #include "../spectral/dft_gemm.h"
-#include "../spectral/spectral.h"
 
 namespace amd_dft {
 namespace {
@@ -122,9 +121,7 @@ std::pair<at::Tensor, at::Tensor> get_dft_gemm_tables(DftTable kind, int W, int 
   std::vector<uint16_t> frag;
   std::vector<float> ph;
   if (kind == DftTable::R2C) dftw_r2c_tables(W, m, frag, ph);
-  else if (kind == DftTable::AFNO_H) afno_dft_tables(W, frag);
   else fno_c2r_tables(W, m, kind == DftTable::C2R_BF16 ? kFnoChunkBF : kFnoChunkF32, frag, ph);
-  if (ph.empty()) ph.push_back(0.f);
   auto f = at::from_blob(frag.data(), {static_cast<int64_t>(frag.size())}, at::TensorOptions().dtype(at::kShort))
                .to(dev);
   auto p = at::from_blob(ph.data(), {static_cast<int64_t>(ph.size())}, at::TensorOptions().dtype(at::kFloat)).to(dev);

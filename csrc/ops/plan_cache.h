@@ -21,7 +21,7 @@ size_t plan_cache_entries();
 size_t plan_cache_pinned();  // plans looked up during a hipGraph capture (never evicted)
 
 // Fragment-ordered twiddle tables of the DFT-as-GEMM kernels, (fragments, phases) on `dev`.
-enum class DftTable { R2C = 0, C2R_F32 = 1, C2R_BF16 = 2, AFNO_H = 3 };
+enum class DftTable { R2C = 0, C2R_F32 = 1, C2R_BF16 = 2 };
 std::pair<at::Tensor, at::Tensor> get_dft_gemm_tables(DftTable kind, int W, int m, const at::Device& dev);
 void plan_cache_reset();
 

@@ -12,7 +12,6 @@
 #include "../spectral/spectral.h"
 #include "checks.h"
 #include "plan_cache.h"
-#include "tuning.h"
 
 namespace amd_dft {
 namespace {
@@ -92,17 +91,6 @@ at::Tensor afno_spectral_cuda(const at::Tensor& xw_, const at::Tensor& w1t_, con
   p.C = static_cast<int>(C);
   p.NB = static_cast<int>(NB);
   p.lambda = static_cast<float>(lam);
-  // the H-transforms as MFMA GEMMs where an instance exists (AMD_DFT_TUNING builds: MI_DFT_AFNO_DFT=0
-  // selects the Stockham-FFT kernel for A/B runs)
-  static const bool dft_off = [] {  // measured slower (profiles/afno_dft_gemm_r5.txt): tuning builds only, opt-in
-    const char* e = tuning_env("MI_DFT_AFNO_DFT");
-    return e == nullptr || e[0] != '1';
-  }();
-  at::Tensor tab;
-  if (!dft_off && afno_dft_supported(static_cast<int>(H), static_cast<int>(C / NB), x3)) {
-    tab = get_dft_gemm_tables(DftTable::AFNO_H, static_cast<int>(H), 0, xw.device()).first;
-    p.dft = reinterpret_cast<const uint16_t*>(tab.data_ptr());
-  }
   launch_afno_spectral(p, c10::hip::getCurrentHIPStream(xw.device().index()).stream());
   return checked(y, "afno_spectral");
 }

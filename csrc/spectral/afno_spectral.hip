@@ -48,10 +48,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cmath>
 #include <cstdint>
 #include <cstdlib>
-#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -770,326 +768,6 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   AFNO_STAMP(11, __builtin_amdgcn_s_memrealtime());
 }
 
-// ================================================================== H-transforms on MFMA
-// The same filter with the two H-direction transforms computed as GEMMs against the DFT matrix
-// instead of Stockham FFT passes on the VALU (which left the FFT variant VALU-bound: ~3.7k of its
-// ~4k instructions per wave are FFT butterflies, staging conversions and index math).  With the
-// complex tile stacked as real rows (part, h), part in {re, im}, padded to HP = 16 ceil(H / 16):
-//   forward   A[k][part BS + c] = sum_(p', h) LF[(part, k)][(p', h)] X[(p', h)][c]
-//             LF = [[cos, sin], [-sin, cos]](2 pi h k / H)   (rows k >= H and columns h >= H zero)
-//   inverse   y[(part, h)][c]   = sum_(p', k) LG[(part, h)][(p', k)] Z[k][p' BS + c]
-//             LG = [[cos, -sin], [sin, cos]](2 pi h k / H)   (unnormalised, as the FFT variant)
-// M = K = 2 HP (192 at H = 90), N = BS: per tile 2 x 7.1 MFLOP next to the block MLP's 2 x 7.1, on the
-// matrix cores.  Both DFT GEMMs run transposed (the tile operand as MFMA A, read from LDS with
-// ds_read_b64_tr_b16; the DFT rows as MFMA B from L2), so a lane holds 4 consecutive channels of one
-// row: the forward epilogue writes 8-byte pieces of A, the inverse one holds re (part 0) and im
-// (part 1) of the same (h, c) and stores 4 complex values as one 16 / 32-byte piece.
-// Precision: bf16 spectra run the DFTs on fp16 MFMA operands (the bf16 input is exact in fp16, the
-// DFT matrix rounded to fp16: 2^-12, and Z staged in fp16 as in the FFT variant), fp32 spectra on
-// 3-product bf16 splits of both operands (LF_hi X_hi + LF_lo X_hi + LF_hi X_lo, ~2^-17).
-// Geometry: HP % 32 == 0 (a 32-deep k-step never straddles the two parts) -> H in {64, 90};
-// 4 waves = 2 parts x 2 k-tile halves, each over all channel tiles (every DFT-matrix fragment read
-// from L2 serves BS / 16 MFMAs); the inverse result goes through a planar LDS staging tile so the
-// global stores are whole interleaved rows.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4s lds_v4s;
-
-template <int L_, int R0_, int R1_, int BS_>
-struct AfnoDftShape : AfnoShape<L_, R0_, R1_, BS_> {
-  using Base = AfnoShape<L_, R0_, R1_, BS_>;
-  static constexpr int HP = 16 * Base::MT;   // padded H: rows of A and Z, half of the DFT K
-  static constexpr int KD = 2 * HP;          // DFT GEMM K (and M): (part, h)
-  static constexpr int KSD = KD / 32;        // 32-deep k-steps
-  static constexpr int CT = BS_ / 16;        // channel tiles
-  static constexpr int MTW = Base::MT / 2;   // k-tiles per wave (one part)
-  static constexpr int CP = BS_ + 8;         // X plane pitch (16-bit elements)
-  static constexpr int ZP = 2 * BS_ + 8;     // Z pitch
-  // one plane set (fp16 / bf16 hi); the x3 kernel's lo planes follow at + PLANE bytes
-  static constexpr int64_t PLANE = Base::cmax(Base::cmax(int64_t(KD) * CP * 2, int64_t(HP) * Base::APitch * 2),
-                                              int64_t(HP) * ZP * 2);
-  static_assert(HP % 32 == 0 && Base::MT % 2 == 0 && Base::CT_EXACT, "DFT-GEMM AFNO geometry");
-};
-
-struct AfnoDftArgs {
-  const void* x;        // [B, H, KM, C, 2] fp32 or bf16
-  void* y;
-  const uint16_t* w1t;  // as AfnoArgs
-  const uint16_t* w2t;
-  const float* b1;
-  const float* b2;
-  const uint16_t* dft;  // afno_dft_tables: [6][KD][KD]
-  int KM, C, NB;
-  float lambda;
-};
-
-__device__ __forceinline__ uint32_t pk_bf(float a, float b) {
-  return static_cast<uint32_t>(f2bf16(a)) | (static_cast<uint32_t>(f2bf16(b)) << 16);
-}
-__device__ __forceinline__ uint32_t pk_h(float a, float b) {
-  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(a))) |
-         (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(b))) << 16);
-}
-// two floats -> (hi, lo) packed bf16 pairs
-__device__ __forceinline__ void split_pk2(float a, float b, uint32_t& hi, uint32_t& lo) {
-  const uint16_t ha = f2bf16(a), hb = f2bf16(b);
-  hi = static_cast<uint32_t>(ha) | (static_cast<uint32_t>(hb) << 16);
-  lo = pk_bf(a - __uint_as_float(static_cast<uint32_t>(ha) << 16), b - __uint_as_float(static_cast<uint32_t>(hb) << 16));
-}
-
-// 8 consecutive K (rows) of one column of a 16-bit LDS matrix [rows][pitch]: the MFMA fragment of
-// lane (c = lane & 15, kq = lane >> 4) for rows r0 + 8 kq .., columns c0 + c (two transposed reads)
-template <int PITCH>
-__device__ __forceinline__ bf16x8 ld_col8(const uint16_t* m, int r0, int c0) {
-  const int lane = threadIdx.x & 63, l15 = lane & 15, lq = lane >> 4;
-  const int e0 = (r0 + 8 * lq + (l15 >> 2)) * PITCH + c0 + 4 * (l15 & 3);
-  const lds_v4s* t = (const lds_v4s*)(m);
-  const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_v4s*>(t + e0 / 4));
-  const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_v4s*>(t + (e0 + 4 * PITCH) / 4));
-  const uint2 u0 = __builtin_bit_cast(uint2, a0), u1 = __builtin_bit_cast(uint2, a1);
-  return __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
-}
-
-// One DFT GEMM for the wave's part p and k-tiles kt0 .. kt0 + MTW - 1 over all CT channel tiles:
-// acc[i][j] (TR: lane holds channels 16 j + 4 kq .. of row p HP + 16 (kt0 + i) + (lane & 15)).
-// Each DFT-matrix fragment (L2) is used CT times; it is prefetched two k-steps ahead.
-// F16: one fp16 product (Xh, Th fp16); else NPR bf16 products Xh.Th (+ Xh.Tl) (+ Xl.Th).
-// ZMODE (inverse): k-step ks reads rows (32 ks) % HP of the column block (32 ks / HP) BS of Z.
-template <class D, bool F16, int NPR, bool ZMODE, int PITCH>
-__device__ __forceinline__ void dft_gemm(const uint16_t* Xh, const uint16_t* Xl, const uint16_t* __restrict__ Th,
-                                         const uint16_t* __restrict__ Tl, int p, int kt0,
-                                         f32x4 (&acc)[D::MTW][D::CT]) {
-  const int lane = threadIdx.x & 63, l15 = lane & 15, lq = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < D::MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < D::CT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr bool TLO = !F16 && NPR >= 2;
-  constexpr int NQ = 3;  // prefetch slots (two k-steps ahead)
-  bf16x8 th[NQ][D::MTW], tl[TLO ? NQ : 1][D::MTW];
-  auto load_t = [&](int ks, int slot) {
-#pragma unroll
-    for (int i = 0; i < D::MTW; ++i) {
-      const int off = (p * D::HP + (kt0 + i) * 16 + l15) * D::KD + ks * 32 + lq * 8;
-      th[slot][i] = *reinterpret_cast<const bf16x8*>(Th + off);
-      if constexpr (TLO) tl[slot][i] = *reinterpret_cast<const bf16x8*>(Tl + off);
-    }
-  };
-  load_t(0, 0);
-  load_t(1, 1);
-#pragma unroll
-  for (int ks = 0; ks < D::KSD; ++ks) {
-    if (ks + 2 < D::KSD) load_t(ks + 2, (ks + 2) % NQ);
-    __builtin_amdgcn_sched_barrier(0);  // keep the table prefetch two k-steps ahead
-    const int r0 = ZMODE ? (ks * 32) % D::HP : ks * 32;
-    const int cb = ZMODE ? ((ks * 32) / D::HP) * D::BS : 0;
-    // tile fragments one channel tile ahead of their MFMAs (two live, not CT)
-    bf16x8 xh[2], xl[2];
-    xh[0] = ld_col8<PITCH>(Xh, r0, cb);
-    if constexpr (NPR >= 3) xl[0] = ld_col8<PITCH>(Xl, r0, cb);
-#pragma unroll
-    for (int j = 0; j < D::CT; ++j) {
-      if (j + 1 < D::CT) {
-        xh[(j + 1) & 1] = ld_col8<PITCH>(Xh, r0, cb + (j + 1) * 16);
-        if constexpr (NPR >= 3) xl[(j + 1) & 1] = ld_col8<PITCH>(Xl, r0, cb + (j + 1) * 16);
-      }
-#pragma unroll
-      for (int pr = 0; pr < (F16 ? 1 : NPR); ++pr)
-#pragma unroll
-        for (int i = 0; i < D::MTW; ++i) {
-          f32x4& c = acc[i][j];
-          if constexpr (F16) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, xh[j & 1]),
-                                                       __builtin_bit_cast(f16x8, th[ks % NQ][i]), c, 0, 0, 0);
-          } else {
-            const bf16x8 av = pr == 2 ? xl[j & 1] : xh[j & 1];
-            const bf16x8 bv = pr == 1 ? tl[TLO ? ks % NQ : 0][i] : th[ks % NQ][i];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
-          }
-        }
-    }
-  }
-}
-
-template <class D, bool BFI, bool BFO, bool X3>
-__global__ void __launch_bounds__(kNT, X3 ? 2 : D::OCC) afno_dft_kernel(const AfnoDftArgs a) {
-  constexpr int L = D::L, BS = D::BS, HP = D::HP, KD = D::KD, AP = D::APitch, CP = D::CP, ZP = D::ZP;
-  extern __shared__ __attribute__((aligned(16))) uint16_t ldsu[];
-  uint16_t* P0 = ldsu;                        // X / A / Z (fp16 or bf16 hi), aliased in turn
-  uint16_t* P1 = ldsu + D::PLANE / 2;         // x3: the lo planes
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int blk = blockIdx.x % a.NB;
-  const int bk = blockIdx.x / a.NB;
-  const int kw = bk % a.KM;
-  const int b = bk / a.KM;
-  AMD_DFT_DEV_CHECK((blk + 1) * BS <= a.C && kw < a.KM, "afno_dft_kernel");
-  const int row_stride = a.KM * a.C * 2;
-  const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * BS) * 2;
-  // ---------------- x -> X planes [part HP + h][c] (16-byte chunks, one row per CPR lanes)
-  {
-    constexpr int CPR = BFI ? BS / 4 : BS / 2;  // chunks per row (4 / 2 complex each)
-    constexpr int NCH = L * CPR, NQ = (NCH + kNT - 1) / kNT;
-    uint4 u[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {  // every load issued before the first LDS write
-      const int t = min(tid + q * kNT, NCH - 1);
-      const int h = t / CPR, cc = t - h * CPR;
-      const char* src = static_cast<const char*>(a.x) + (base + static_cast<int64_t>(h) * row_stride) * (BFI ? 2 : 4);
-      u[q] = *reinterpret_cast<const uint4*>(src + cc * 16);
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int t = tid + q * kNT;
-      if (NCH % kNT == 0 || t < NCH) {
-        const int h = t / CPR, cc = t - h * CPR;
-        if constexpr (BFI) {  // 4 complex bf16 -> fp16 re / im (exact: bf16 values well inside fp16 range)
-          const float2 c0 = make_float2(__uint_as_float(u[q].x << 16), __uint_as_float(u[q].x & 0xffff0000u));
-          const float2 c1 = make_float2(__uint_as_float(u[q].y << 16), __uint_as_float(u[q].y & 0xffff0000u));
-          const float2 c2 = make_float2(__uint_as_float(u[q].z << 16), __uint_as_float(u[q].z & 0xffff0000u));
-          const float2 c3 = make_float2(__uint_as_float(u[q].w << 16), __uint_as_float(u[q].w & 0xffff0000u));
-          *reinterpret_cast<uint2*>(P0 + h * CP + cc * 4) = make_uint2(pk_h(c0.x, c1.x), pk_h(c2.x, c3.x));
-          *reinterpret_cast<uint2*>(P0 + (HP + h) * CP + cc * 4) = make_uint2(pk_h(c0.y, c1.y), pk_h(c2.y, c3.y));
-        } else {
-          const float4 f = __builtin_bit_cast(float4, u[q]);  // (re, im) of channels 2 cc, 2 cc + 1
-          if constexpr (X3) {
-            uint32_t hr, lr, hi_, li;
-            split_pk2(f.x, f.z, hr, lr);
-            split_pk2(f.y, f.w, hi_, li);
-            *reinterpret_cast<uint32_t*>(P0 + h * CP + cc * 2) = hr;
-            *reinterpret_cast<uint32_t*>(P1 + h * CP + cc * 2) = lr;
-            *reinterpret_cast<uint32_t*>(P0 + (HP + h) * CP + cc * 2) = hi_;
-            *reinterpret_cast<uint32_t*>(P1 + (HP + h) * CP + cc * 2) = li;
-          } else {
-            *reinterpret_cast<uint32_t*>(P0 + h * CP + cc * 2) = pk_h(f.x, f.z);
-            *reinterpret_cast<uint32_t*>(P0 + (HP + h) * CP + cc * 2) = pk_h(f.y, f.w);
-          }
-        }
-      }
-    }
-    // rows h in [L, HP) of both parts: zero (their DFT-matrix columns are zero, but 0 x stale NaN is not)
-    constexpr int PADW = (HP - L) * 2 * (BS / 8);  // 16-byte words
-#pragma unroll
-    for (int q = 0; q < (PADW + kNT - 1) / kNT; ++q) {
-      const int t = tid + q * kNT;
-      if (t < PADW) {
-        const int r = t / (BS / 8), cw = t - r * (BS / 8);
-        const int row = (r < HP - L ? L + r : HP + L + (r - (HP - L)));
-        *reinterpret_cast<uint4*>(P0 + row * CP + cw * 8) = make_uint4(0, 0, 0, 0);
-        if constexpr (X3) *reinterpret_cast<uint4*>(P1 + row * CP + cw * 8) = make_uint4(0, 0, 0, 0);
-      }
-    }
-  }
-  __syncthreads();
-  // wave w: part p = w & 1 (re / im rows of the stacked transform), k-tiles kt0 .. kt0 + MTW - 1
-  const int pw = w & 1, kt0 = (w >> 1) * D::MTW;
-  constexpr int64_t KK = static_cast<int64_t>(KD) * KD;
-  f32x4 accd[D::MTW][D::CT];
-  // ---------------- forward DFT -> A ([k][re c | im c]; bf16, x3: hi / lo planes)
-  if constexpr (X3) dft_gemm<D, false, 3, false, CP>(P0, P1, a.dft, a.dft + KK, pw, kt0, accd);
-  else dft_gemm<D, true, 1, false, CP>(P0, P0, a.dft + 4 * KK, a.dft + 4 * KK, pw, kt0, accd);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < D::MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < D::CT; ++j) {
-      const int k = (kt0 + i) * 16 + (lane & 15);
-      const int idx = k * AP + pw * BS + j * 16 + 4 * (lane >> 4);
-      const f32x4 v = accd[i][j];
-      if constexpr (X3) put_split4(P0, P1, idx, v[0], v[1], v[2], v[3]);
-      else *reinterpret_cast<uint2*>(P0 + idx) = make_uint2(pk_bf(v[0], v[1]), pk_bf(v[2], v[3]));
-    }
-  __syncthreads();
-  // ---------------- block MLP: GEMM1 + bias + ReLU (in place), GEMM2 (+ bias + softshrink -> Z)
-  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * D::K * D::K * (X3 ? 2 : 1);
-  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * D::K * D::K * (X3 ? 2 : 1);
-  const float* b1 = a.b1 + blk * D::K;
-  const float* b2 = a.b2 + blk * D::K;
-  f32x4 acc[D::MT][D::NTW];
-  if constexpr (X3) gemm_tile_x3<D, true>(P0, P1, w1t, acc);
-  else gemm_tile<D, true>(P0, w1t, acc);
-  __syncthreads();
-#pragma unroll
-  for (int nj = 0; nj < D::NTW; ++nj) {
-    const int n0 = (D::NTW * w + nj) * 16 + 4 * (lane >> 4);
-    const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
-#pragma unroll
-    for (int mi = 0; mi < D::MT; ++mi) {
-      const int idx = (mi * 16 + (lane & 15)) * AP + n0;
-      const float r0 = fmaxf(acc[mi][nj][0] + bias.x, 0.f), r1 = fmaxf(acc[mi][nj][1] + bias.y, 0.f);
-      const float r2 = fmaxf(acc[mi][nj][2] + bias.z, 0.f), r3 = fmaxf(acc[mi][nj][3] + bias.w, 0.f);
-      if constexpr (X3) put_split4(P0, P1, idx, r0, r1, r2, r3);
-      else *reinterpret_cast<uint2*>(P0 + idx) = make_uint2(pk_bf(r0, r1), pk_bf(r2, r3));
-    }
-  }
-  __syncthreads();
-  if constexpr (X3) gemm_tile_x3<D, true>(P0, P1, w2t, acc);
-  else gemm_tile<D, true>(P0, w2t, acc);
-  __syncthreads();
-  const float lam = a.lambda;
-#pragma unroll
-  for (int nj = 0; nj < D::NTW; ++nj) {
-    const int n0 = (D::NTW * w + nj) * 16 + 4 * (lane >> 4);
-    const float4 bias = *reinterpret_cast<const float4*>(b2 + n0);
-#pragma unroll
-    for (int mi = 0; mi < D::MT; ++mi) {
-      const int idx = (mi * 16 + (lane & 15)) * ZP + n0;
-      const float v0 = acc[mi][nj][0] + bias.x, v1 = acc[mi][nj][1] + bias.y;
-      const float v2 = acc[mi][nj][2] + bias.z, v3 = acc[mi][nj][3] + bias.w;
-      const float s0 = v0 - __builtin_amdgcn_fmed3f(v0, -lam, lam), s1 = v1 - __builtin_amdgcn_fmed3f(v1, -lam, lam);
-      const float s2 = v2 - __builtin_amdgcn_fmed3f(v2, -lam, lam), s3 = v3 - __builtin_amdgcn_fmed3f(v3, -lam, lam);
-      if constexpr (X3) put_split4(P0, P1, idx, s0, s1, s2, s3);
-      else *reinterpret_cast<uint2*>(P0 + idx) = make_uint2(pk_h(s0, s1), pk_h(s2, s3));
-    }
-  }
-  __syncthreads();
-  // ---------------- inverse DFT -> planar y staging [part][h][c] (pitch CP) -> interleaved global rows
-  if constexpr (X3) dft_gemm<D, false, 3, true, ZP>(P0, P1, a.dft + 2 * KK, a.dft + 3 * KK, pw, kt0, accd);
-  else dft_gemm<D, true, 1, true, ZP>(P0, P0, a.dft + 5 * KK, a.dft + 5 * KK, pw, kt0, accd);
-  __syncthreads();
-  float* Yf = reinterpret_cast<float*>(ldsu);  // x3 / fp32 out: fp32 planes (2 PLANE bytes)
-#pragma unroll
-  for (int i = 0; i < D::MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < D::CT; ++j) {
-      const int h = (kt0 + i) * 16 + (lane & 15);
-      const int idx = (pw * HP + h) * CP + j * 16 + 4 * (lane >> 4);
-      const f32x4 v = accd[i][j];
-      if constexpr (BFO) *reinterpret_cast<uint2*>(P0 + idx) = make_uint2(pk_bf(v[0], v[1]), pk_bf(v[2], v[3]));
-      else *reinterpret_cast<float4*>(Yf + idx) = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  __syncthreads();
-  {
-    // one 16-byte global piece per thread and step: 4 complex bf16 / 2 complex fp32 of one row
-    constexpr int CPC = BFO ? 4 : 2;  // complex values per piece
-    constexpr int PPR = BS / CPC, NP_ = L * PPR;
-    int tid2 = tid;
-    asm volatile("" : "+v"(tid2));  // (see below: no index shared with the input phase)
-#pragma unroll
-    for (int q = 0; q < (NP_ + kNT - 1) / kNT; ++q) {
-      const int t = tid2 + q * kNT;
-      if (NP_ % kNT == 0 || t < NP_) {
-        int h = t / PPR;
-        const int c = (t - h * PPR) * CPC;
-        // opaque: otherwise the row offsets are shared with the input phase's and held (spilled)
-        // across the whole kernel
-        asm volatile("" : "+v"(h));
-        char* dst = static_cast<char*>(a.y) + (base + static_cast<int64_t>(h) * row_stride + 2 * c) * (BFO ? 2 : 4);
-        if constexpr (BFO) {
-          const uint2 re = *reinterpret_cast<const uint2*>(P0 + h * CP + c);
-          const uint2 im = *reinterpret_cast<const uint2*>(P0 + (HP + h) * CP + c);
-          *reinterpret_cast<uint4*>(dst) =
-              make_uint4((re.x & 0xffffu) | (im.x << 16), (re.x >> 16) | (im.x & 0xffff0000u),
-                         (re.y & 0xffffu) | (im.y << 16), (re.y >> 16) | (im.y & 0xffff0000u));
-        } else {
-          const float2 re = *reinterpret_cast<const float2*>(Yf + h * CP + c);
-          const float2 im = *reinterpret_cast<const float2*>(Yf + (HP + h) * CP + c);
-          *reinterpret_cast<float4*>(dst) = make_float4(re.x, im.x, re.y, im.y);
-        }
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ instance table
 // (H, R0, R1, block size): (R0, R1) must be the FFT plan's radix order for H (plan_info),
 // because the kernel reads the plan's twiddle table; launch_afno_spectral checks it.
@@ -1136,46 +814,6 @@ const AfnoInstance* find_instance(int H, int bs) {
   return nullptr;
 }
 
-// DFT-GEMM instances: (H, R0, R1, block size, bf16x3 variant too).  The x3 variant needs two
-// fp32-class plane sets (2 x PLANE bytes) and keeps 2 workgroups per CU up to block size 96.
-#define AFNO_DFT_SHAPES(X) \
-  X(90, 9, 10, 96, 1)      \
-  X(90, 9, 10, 64, 1)      \
-  X(90, 9, 10, 128, 0)     \
-  X(64, 16, 4, 96, 1)      \
-  X(64, 16, 4, 64, 1)      \
-  X(64, 16, 4, 128, 0)
-
-using DftFn = void (*)(AfnoDftArgs);
-struct AfnoDftInstance {
-  int H, BS, HP;
-  int64_t plane;         // dynamic LDS bytes of the bf16 kernel with bf16 output (x3 / fp32 output: twice)
-  DftFn bf16[2][2];      // [bf16_in][bf16_out]
-  DftFn x3;              // nullptr: no bf16x3 DFT-GEMM variant for this shape
-};
-
-template <class D, bool HAS_X3>
-AfnoDftInstance make_dft_instance() {
-  AfnoDftInstance r{D::L, D::BS, D::HP, D::PLANE,
-                    {{afno_dft_kernel<D, false, false, false>, afno_dft_kernel<D, false, true, false>},
-                     {afno_dft_kernel<D, true, false, false>, afno_dft_kernel<D, true, true, false>}},
-                    nullptr};
-  if constexpr (HAS_X3) r.x3 = afno_dft_kernel<D, false, false, true>;
-  return r;
-}
-
-#define AFNO_DFT_INSTANCE(H, R0, R1, BS, X3) make_dft_instance<AfnoDftShape<H, R0, R1, BS>, X3 != 0>(),
-const std::vector<AfnoDftInstance>& dft_instances() {
-  static const std::vector<AfnoDftInstance> v = {AFNO_DFT_SHAPES(AFNO_DFT_INSTANCE)};
-  return v;
-}
-
-const AfnoDftInstance* find_dft_instance(int H, int bs, bool x3) {
-  for (const auto& i : dft_instances())
-    if (i.H == H && i.BS == bs && (!x3 || i.x3 != nullptr)) return &i;
-  return nullptr;
-}
-
 void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a, void* stream) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(lds));
@@ -1189,51 +827,6 @@ void launch_kernel(KernFn kern, int64_t lds, int64_t nblocks, const AfnoArgs& a,
 }  // namespace
 
 bool afno_spectral_supported(int H, int block_size) { return find_instance(H, block_size) != nullptr; }
-
-bool afno_dft_supported(int H, int block_size, bool x3) { return find_dft_instance(H, block_size, x3) != nullptr; }
-
-void afno_dft_tables(int H, std::vector<uint16_t>& t) {
-  const int HP = 16 * ((H + 15) / 16), KD = 2 * HP;
-  const int64_t KK = static_cast<int64_t>(KD) * KD;
-  t.assign(6 * KK, 0);
-  const double two_pi = 6.283185307179586476925286766559;
-  auto bf = [](double v) {  // round-to-nearest-even bf16
-    const float f = static_cast<float>(v);
-    uint32_t u;
-    std::memcpy(&u, &f, 4);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return static_cast<uint16_t>(u >> 16);
-  };
-  auto bf_val = [](uint16_t h) {
-    const uint32_t u = static_cast<uint32_t>(h) << 16;
-    float f;
-    std::memcpy(&f, &u, 4);
-    return static_cast<double>(f);
-  };
-  auto f16 = [](double v) {
-    const _Float16 h = static_cast<_Float16>(static_cast<float>(v));
-    uint16_t u;
-    std::memcpy(&u, &h, 2);
-    return u;
-  };
-  // entry (row, col) of the 2 x 2 real block form; m: 0 forward (LF), 1 inverse (LG)
-  for (int m = 0; m < 2; ++m)
-    for (int p = 0; p < 2; ++p)
-      for (int r = 0; r < H; ++r)
-        for (int q = 0; q < 2; ++q)
-          for (int c = 0; c < H; ++c) {
-            const double th = two_pi * static_cast<double>((static_cast<int64_t>(r) * c) % H) / H;
-            const double cs = std::cos(th), sn = std::sin(th);
-            // LF rows (part, k), cols (part', h): [[cos, sin], [-sin, cos]]
-            // LG rows (part, h), cols (part', k): [[cos, -sin], [sin, cos]]
-            double v = p == q ? cs : (p == 0 ? 1.0 : -1.0) * (m == 0 ? sn : -sn);
-            const int64_t e = static_cast<int64_t>(p * HP + r) * KD + q * HP + c;
-            const uint16_t hi = bf(v);
-            t[(2 * m) * KK + e] = hi;
-            t[(2 * m + 1) * KK + e] = bf(v - bf_val(hi));
-            t[(4 + m) * KK + e] = f16(v);
-          }
-}
 
 std::vector<std::pair<int, int>> afno_spectral_shapes() {
   std::vector<std::pair<int, int>> v;
@@ -1269,31 +862,6 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   a.lambda = p.lambda;
   const int64_t nblocks = static_cast<int64_t>(p.B) * p.KM * p.NB;
   if (nblocks <= 0) return;
-  if (const AfnoDftInstance* d = p.dft ? find_dft_instance(p.H, p.C / p.NB, p.x3 != 0) : nullptr) {
-    AfnoDftArgs da;
-    da.x = p.x;
-    da.y = p.y;
-    da.w1t = p.w1t;
-    da.w2t = p.w2t;
-    da.b1 = p.b1;
-    da.b2 = p.b2;
-    da.dft = p.dft;
-    da.KM = p.KM;
-    da.C = p.C;
-    da.NB = p.NB;
-    da.lambda = p.lambda;
-    if (p.x3 && (p.bf16_in || p.bf16_out)) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
-    DftFn k = p.x3 ? d->x3 : d->bf16[p.bf16_in ? 1 : 0][p.bf16_out ? 1 : 0];
-    const int64_t lds = (p.x3 || !p.bf16_out) ? 2 * d->plane : d->plane;  // fp32 output staging: 2 planes
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(lds));
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_dft attr: ") + hipGetErrorString(e));
-    hipLaunchKernelGGL(k, dim3(static_cast<uint32_t>(nblocks)), dim3(kNT), static_cast<size_t>(lds),
-                       static_cast<hipStream_t>(stream), da);
-    e = hipGetLastError();
-    if (e != hipSuccess) throw std::runtime_error(std::string("amd_dft: afno_dft launch: ") + hipGetErrorString(e));
-    return;
-  }
   if (p.x3) {
     if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
     launch_kernel(in->x3, in->lds_x3, nblocks, a, stream);

@@ -21,15 +21,8 @@ struct AfnoLaunch {
   int r0 = 0, r1 = 0;   // the plan's radix order (must match the instance's two passes)
   int B, H, KM, C, NB;
   float lambda;
-  // H-transforms as MFMA GEMMs (afno_dft_tables(H)): used when non-null and an instance exists
-  const uint16_t* dft = nullptr;
 };
 bool afno_spectral_supported(int H, int block_size);
-// (H, block size) pairs with a DFT-GEMM instance (x3: of the bf16x3 variant)
-bool afno_dft_supported(int H, int block_size, bool x3);
-// the H-direction DFT matrices of the DFT-GEMM instances: [6][2 HP][2 HP] uint16 (HP = 16 ceil(H / 16)),
-// forward (hi, lo bf16), inverse (hi, lo bf16), forward fp16, inverse fp16 -- see afno_spectral.hip
-void afno_dft_tables(int H, std::vector<uint16_t>& t);
 std::vector<std::pair<int, int>> afno_spectral_shapes();  // instantiated (H, block size) pairs
 int64_t afno_spectral_lds_bytes(int H, int block_size, bool x3);
 void launch_afno_spectral(const AfnoLaunch& p, void* stream);

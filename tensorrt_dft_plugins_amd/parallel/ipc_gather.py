@@ -6,29 +6,37 @@ each rank can instead PUSH its shard straight into every peer's output buffer --
 concurrent copies, one per link, each moving one shard (ring: ~7 x shard / link bandwidth;
 mesh: ~1 x shard / link bandwidth, derived in SURVEY §5.8).
 
-Protocol per step (buffer slot ``i`` of ``nbuf``, all on the caller's current stream):
-  1. release: record this rank's inter-process event ``rel[i]``.  Everything this rank enqueued
-     before the call -- in particular every consumer of the slot's previous contents (step
-     ``k - nbuf``) -- is ordered before it;
-  2. host handshake #1: a barrier on a Gloo group (every rank has enqueued its release record);
-  3. the stream waits on every peer's ``rel[i]``: a push never overwrites a peer's slot while
-     that peer's GPU may still read the old contents (write-after-read across processes);
-  4. push: one kernel (csrc/parallel/ipc_push.hip) stores the local shard into slot ``i`` of every
+Protocol per step, ``protocol="flags"`` (default; buffer slot ``i`` of ``nbuf``, its ``n``-th use,
+all on the caller's current stream, no host handshake):
+  1. release: write ``n`` into flag word (slot i, REL, this rank) of every PEER's flag buffer
+     (``hipStreamWriteValue32``, stream-ordered after everything this rank enqueued before the
+     call -- in particular every consumer of the slot's previous contents);
+  2. the stream waits until this rank's own flag words (i, REL, p) >= n for every peer p
+     (``hipStreamWaitValue32``): a push never overwrites a peer's slot while that peer's GPU may
+     still read the old contents (write-after-read across processes);
+  3. push: one kernel (csrc/parallel/ipc_push.hip) stores the local shard into slot ``i`` of every
      rank's buffer at once (peer pointers from ``hipIpcOpenMemHandle``; one xGMI link per peer),
      at byte offset ``rank * shard_bytes``;
-  5. record this rank's inter-process event ``done[i]`` after the pushes;
-  6. host handshake #2: every producer has ENQUEUED its pushes and its ``done[i]`` record;
-  7. the stream waits on every peer's ``done[i]``: stream-ordered completion of all pushes.
-The host never waits for the GPU.  Contract: the gathered buffer of step ``k`` stays valid until
-the gather of step ``k + nbuf`` is called, and every read of it must be enqueued (in stream order
-on the calling stream, or joined into it) before that call.
+  4. write ``n`` into (i, DONE, this rank) of every peer's flags after the pushes;
+  5. the stream waits until its own (i, DONE, p) >= n for every peer: all pushes into this rank's
+     slot have completed.
+A wait on a counter value (not on "the latest record" of an event) is satisfied by exactly the
+peer's n-th release / push whenever the peer gets to it, so no rank has to know that the others
+have enqueued their records: the gather enqueues 4 (world - 1) stream packets and returns, and the
+host never blocks on a peer (no barriers on the enqueue path).
+``protocol="events"`` is the round-2 form: inter-process events, whose stream wait targets the
+latest record enqueued so far, so two Gloo host barriers per step ensure the peers' records are
+enqueued first.
+Contract (both): the gathered buffer of step ``k`` stays valid until the gather of step
+``k + nbuf`` is called, and every read of it must be enqueued (in stream order on the calling
+stream, or joined into it) before that call.
 
 Transports: ``HipIpcTransport`` (GPU: hipMalloc'd buffers, IPC memory/event handles) and
 ``ShmTransport`` (CPU: ``/dev/shm``-backed storages).  The CPU transport emulates a GPU stream
-with one worker thread per rank and inter-process events with shared ``(enqueued, completed)``
-counters, so the multi-process Gloo tests exercise the same ordering the GPU relies on -- a
-deliberately slow consumer on one rank shows whether a peer's push waits for it
-(tests/test_dp.py::test_ipc_gather_slow_consumer_*).
+with one worker thread per rank, inter-process events with shared ``(enqueued, completed)``
+counters and flag words as shared int32s written / polled by the workers, so the multi-process
+Gloo tests exercise the same ordering the GPU relies on -- a deliberately slow consumer on one
+rank shows whether a peer's push waits for it (tests/test_dp.py::test_ipc_gather_slow_consumer_*).
 """
 from __future__ import annotations
 
@@ -90,6 +98,12 @@ class HipIpcTransport:
 
     def wait(self, ev) -> None:
         self.ops._ipc_stream_wait(ev, self.dev)
+
+    def write_value(self, flags, idx: int, value: int) -> None:
+        self.ops._ipc_write_value(int(flags) + 4 * idx, value, self.dev)
+
+    def wait_value(self, flags, idx: int, value: int) -> None:
+        self.ops._ipc_wait_value(int(flags) + 4 * idx, value, self.dev)
 
     def enqueue(self, fn: Callable[[], None]) -> None:
         fn()  # device work is already stream-ordered: run the enqueueing code now
@@ -232,6 +246,27 @@ class ShmTransport:
 
         self.stream.submit(run)
 
+    def write_value(self, flags, idx: int, value: int) -> None:
+        f = flags.view(torch.int32)
+
+        def run():
+            f[idx] = value
+
+        self.stream.submit(run)
+
+    def wait_value(self, flags, idx: int, value: int) -> None:
+        f = flags.view(torch.int32)
+        deadline_s = self.spin_timeout_s
+
+        def run():
+            t0 = time.monotonic()
+            while int(f[idx]) < value:
+                if time.monotonic() - t0 > deadline_s:
+                    raise TimeoutError(f"amd_dft ShmTransport: flag wait {int(f[idx])} < {value}")
+                time.sleep(0.0005)
+
+        self.stream.submit(run)
+
     def enqueue(self, fn: Callable[[], None]) -> None:
         self.stream.submit(fn)
 
@@ -264,7 +299,10 @@ class IpcAllGather:
     """
 
     def __init__(self, shard_shape: Sequence[int], dtype: torch.dtype, device: torch.device, *, nbuf: int = 2,
-                 transport=None, group=None, release: bool = True):
+                 transport=None, group=None, release: bool = True, protocol: str = "flags"):
+        if protocol not in ("flags", "events"):
+            raise ValueError(f"protocol must be 'flags' or 'events', not {protocol!r}")
+        self.protocol = protocol
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.shard_shape = list(shard_shape)
         self.dtype = dtype
@@ -296,14 +334,45 @@ class IpcAllGather:
             self.peer_events.append([self.transport.open_event(h[1], ev, p == self.rank) for p, h in enumerate(handles)])
             self.rel.append(rel)
             self.peer_rel.append([self.transport.open_event(h[2], rel, p == self.rank) for p, h in enumerate(handles)])
+        # flag words [nbuf][REL, DONE][writer rank] (int32, zeroed), written by the peers
+        self.uses = [0] * nbuf
+        self.flags = None
+        self.peer_flags: List[object] = []
+        if protocol == "flags":
+            fbuf, fh = self.transport.alloc(nbuf * 2 * self.world * 4)
+            fbuf.zero_()
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            fhandles: List[Optional[object]] = [None] * self.world
+            dist.all_gather_object(fhandles, fh, group=self.host_group)
+            self.peer_flags = [self.transport.open(h, fbuf, p == self.rank) for p, h in enumerate(fhandles)]
+            self.flags = self.peer_flags[self.rank]
         dist.barrier(group=self.host_group)
         self._closed = False
+
+    def _fi(self, slot: int, kind: int, writer: int) -> int:
+        return (slot * 2 + kind) * self.world + writer
 
     def gather(self, local: torch.Tensor, i: int) -> torch.Tensor:
         if list(local.shape) != self.shard_shape or local.dtype != self.dtype:
             raise ValueError(f"shard {list(local.shape)} {local.dtype} != {self.shard_shape} {self.dtype}")
         i %= self.nbuf
         t = self.transport
+        if self.protocol == "flags":
+            self.uses[i] += 1
+            n = self.uses[i]
+            peers = [p for p in range(self.world) if p != self.rank]
+            if self.release:
+                for p in peers:
+                    t.write_value(self.peer_flags[p], self._fi(i, 0, self.rank), n)
+                for p in peers:
+                    t.wait_value(self.flags, self._fi(i, 0, p), n)
+            t.push(local, self.peers[i], self.rank * self.shard_bytes)
+            for p in peers:
+                t.write_value(self.peer_flags[p], self._fi(i, 1, self.rank), n)
+            for p in peers:
+                t.wait_value(self.flags, self._fi(i, 1, p), n)
+            return self.full[i]
         if self.release:
             t.record(self.rel[i])
             dist.barrier(group=self.host_group)
@@ -335,7 +404,7 @@ class IpcAllGather:
         self.transport.synchronize()
         dist.barrier(group=self.host_group)
         self.transport.close_imports()
-        self.peers, self.peer_events, self.peer_rel = [], [], []
+        self.peers, self.peer_events, self.peer_rel, self.peer_flags, self.flags = [], [], [], [], None
         dist.barrier(group=self.host_group)
         self.full, self.events, self.rel = [], [], []
         self.transport.close_own()

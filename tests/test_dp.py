@@ -104,7 +104,7 @@ def test_dp_allgather_gloo_world8(backend):
     _run_dp("cpu", backend, world=8)
 
 
-def _slow_consumer_worker(rank, world, port, q, release):
+def _slow_consumer_worker(rank, world, port, q, release, protocol="flags"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         sys.path.insert(0, ROOT)
@@ -115,7 +115,15 @@ def _slow_consumer_worker(rank, world, port, q, release):
         from tensorrt_dft_plugins_amd.parallel import IpcAllGather
 
         dist.init_process_group("gloo")
-        g = IpcAllGather([4, 8], torch.float32, torch.device("cpu"), nbuf=2, release=release)
+        g = IpcAllGather([4, 8], torch.float32, torch.device("cpu"), nbuf=2, release=release, protocol=protocol)
+        barriers = [0]
+        real_barrier = dist.barrier
+
+        def counting_barrier(*a, **k):
+            barriers[0] += 1
+            return real_barrier(*a, **k)
+
+        dist.barrier = counting_barrier  # host handshakes issued by the gathers below
         seen = []
         slow = rank == world - 1
 
@@ -131,48 +139,57 @@ def _slow_consumer_worker(rank, world, port, q, release):
                 g.enqueue(lambda t=prev: consume(t))
             prev = full
         g.enqueue(lambda t=prev: consume(t))
+        n_barriers = barriers[0]
+        dist.barrier = real_barrier
         g.synchronize()
         bad = [k for k, t in enumerate(seen)
                if not torch.equal(t.view(world, 4, 8)[:, 0, 0], torch.arange(world, dtype=torch.float32) + 100 * k)]
         g.close()
-        q.put((rank, bad))
+        q.put((rank, (bad, n_barriers)))
         dist.destroy_process_group()
     except BaseException as e:
         q.put((rank, repr(e)))
         raise
 
 
-def _run_slow_consumer(world, release):
+def _run_slow_consumer(world, release, protocol="flags"):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_slow_consumer_worker, args=(r, world, port, q, release)) for r in range(world)]
+    procs = [ctx.Process(target=_slow_consumer_worker, args=(r, world, port, q, release, protocol))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
     for r, v in res.items():
-        assert isinstance(v, list), f"rank {r} failed: {v}"
+        assert isinstance(v, tuple), f"rank {r} failed: {v}"
     return res
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_ipc_gather_slow_consumer_slot_reuse(world):
+@pytest.mark.parametrize("world,protocol", [(2, "flags"), (3, "flags"), (8, "flags"), (2, "events"), (3, "events")])
+def test_ipc_gather_slow_consumer_slot_reuse(world, protocol):
     """Write-after-read across processes: every rank reads step k's gathered slot after it has
     enqueued step k + 1 (the overlap the double buffer is for); the last rank's stream lags (each
-    read sleeps) while the others race ahead and reuse the slot at step k + 2.  The release events
-    (protocol steps 1-3, parallel/ipc_gather.py) make every push wait until the slow rank has
-    read the slot's previous contents: every rank sees every step intact."""
-    res = _run_slow_consumer(world, release=True)
-    assert all(v == [] for v in res.values()), res
+    read sleeps) while the others race ahead and reuse the slot at step k + 2.  The release step
+    (parallel/ipc_gather.py: counted flags, or events + host barriers) makes every push wait until
+    the slow rank has read the slot's previous contents: every rank sees every step intact.  The
+    flags protocol does it without a single host barrier on the gather path."""
+    res = _run_slow_consumer(world, release=True, protocol=protocol)
+    assert all(v[0] == [] for v in res.values()), res
+    if protocol == "flags":
+        assert all(v[1] == 0 for v in res.values()), res
+    else:
+        assert all(v[1] == 2 * 6 for v in res.values()), res
 
 
-def test_ipc_gather_slow_consumer_detects_race_without_release():
+@pytest.mark.parametrize("protocol", ["flags", "events"])
+def test_ipc_gather_slow_consumer_detects_race_without_release(protocol):
     """The same run with the release wait disabled corrupts the slow rank's reads: the test above
     can see the race it guards against."""
-    res = _run_slow_consumer(2, release=False)
-    assert res[1], "expected the lagging rank to read overwritten slots"
+    res = _run_slow_consumer(2, release=False, protocol=protocol)
+    assert res[1][0], "expected the lagging rank to read overwritten slots"
 
 
 @pytest.mark.gpu
