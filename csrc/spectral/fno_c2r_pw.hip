@@ -26,10 +26,12 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
 
+#include "../ops/tuning.h"
 #include "dft_gemm.h"
 
 #ifndef FNO_EPI_SWAP
@@ -567,8 +569,18 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
   const int nch = (p.W + CH - 1) / CH;
   const int64_t units = static_cast<int64_t>(p.B) * p.H * nch;
   // Persistent grid: at most as many workgroups as are resident at once (a second partial round
-  // of workgroups would double the kernel time), and >= 4 chunks per wave.
-  const int64_t nwg = std::max<int64_t>(std::min<int64_t>((units + 15) / 16, resident_wgs<BF, KS, CO>()), 1);
+  // of workgroups would double the kernel time), and >= 4 chunks per wave (tuning builds:
+  // MI_DFT_FNO_UPW = minimum chunks per wave, MI_DFT_FNO_WGS = workgroup cap)
+  static const int upw = [] {
+    const char* e = tuning_env("MI_DFT_FNO_UPW");
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  static const int64_t wgs_cap = [] {
+    const char* e = tuning_env("MI_DFT_FNO_WGS");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1) << 40;
+  }();
+  const int64_t nwg = std::max<int64_t>(
+      std::min<int64_t>(std::min<int64_t>((units + 4 * upw - 1) / (4 * upw), resident_wgs<BF, KS, CO>()), wgs_cap), 1);
   const dim3 grid(static_cast<uint32_t>(nwg));
   const float2* yw = static_cast<const float2*>(p.yw);
   const bf16x8* g0 = static_cast<const bf16x8*>(p.g0);
