@@ -44,6 +44,8 @@ def main(argv=None):
     rb = torch.randn(M, C, device=dev).to(torch.bfloat16)
     v = {
         "fc1_gelu amd": lambda: ops.linear(x, w1, b1, 1, None),
+        # hipBLASLt's GELU epilogue is the tanh form: the like-for-like hand kernel is act 2
+        "fc1_gelu_tanh amd": lambda: ops.linear(x, w1, b1, 2, None),
         "fc1_gelu hipblaslt": lambda: torch._addmm_activation(b1h, x, w1.t(), use_gelu=True),
         "fc1 amd": lambda: ops.linear(x, w1, b1, 0, None),
         "fc1 hipblaslt": lambda: F.linear(x, w1, b1h),
@@ -51,6 +53,7 @@ def main(argv=None):
         "fc2 hipblaslt": lambda: F.linear(h, w2, b2h),
         # the bf16 block's forms (persistent variants under MI_DFT_GEMM_PERSIST=1)
         "fc1_gelu amd LN": lambda: ops.linear_ln(x, w1, c1_b, b1, st_b, 1),
+        "fc1_gelu_tanh amd LN": lambda: ops.linear_ln(x, w1, c1_b, b1, st_b, 2),
         "fc2 amd (+res)": lambda: ops.linear(h, w2, b2, 0, rb),
         # the model's fc2: bias pending into the next block, + the next LN's partial statistics
         "fc2 amd (+res, no bias)": lambda: ops.linear(h, w2, None, 0, rb),
@@ -91,6 +94,10 @@ def main(argv=None):
     y = ops.linear(x[:4096], w1, b1, 1, None).float()
     ref = F.gelu(F.linear(x[:4096].float(), w1.float(), b1))
     print("rel err", ((y - ref).norm() / ref.norm()).item())
+    yt = ops.linear(x[:4096], w1, b1, 2, None).float()
+    print("rel err tanh form vs erf reference", ((yt - ref).norm() / ref.norm()).item(),
+          "vs tanh reference", ((yt - F.gelu(F.linear(x[:4096].float(), w1.float(), b1), approximate="tanh")).norm()
+                                / ref.norm()).item())
     return out
 
 

@@ -942,7 +942,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::T
               "amd_dft.c2r_ln_add_split: X must be [..., km, C, 2] with the leading dims and C of x and km <= n/2+1");
   at::Tensor X = X_.contiguous(), x = x_.contiguous();
   const int64_t km = X.size(axis), C = x.size(-1);
-  if (X.numel() > 0 && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
+  if (X.numel() > 0 && afno_w_enabled() && afno_w_supported(static_cast<int>(n), static_cast<int>(C), static_cast<int>(km)) &&
       x.numel() / (n * C) < (int64_t(1) << 31)) {
     at::Tensor stats = stats_.to(at::kFloat).contiguous(), g = g_.to(at::kFloat).contiguous(),
                b = b_.to(at::kFloat).contiguous();

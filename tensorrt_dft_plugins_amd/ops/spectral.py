@@ -254,7 +254,8 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
                                                  writes LN2's per-64-channel partials of the stored
                                                  x1 (c2r_ln_add_part)
       h     = GELU(fc1(LN2(x1)))                 ln_stats_merge + hand MFMA GEMM with LN2 folded in
-                                                 (linear_ln) and the erf GELU in the epilogue
+                                                 (linear_ln) and the GELU in the epilogue -- in the
+                                                 tanh form unless cfg.bf16_gelu == "erf" (see AFNOConfig)
       x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue, which also
                                                  emits the next LN1's partials of x1 + b2
                                                  (linear_stats)
@@ -292,7 +293,7 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
             x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
             st2 = ops.ln_stats(x1, None, blk.norm2.eps)
         w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
-        hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 1)
+        hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 2 if getattr(c, "bf16_gelu", "tanh") == "tanh" else 1)
         if C > 64 * 64:
             x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
             return x1, m.fc2.bias

@@ -107,3 +107,37 @@ def test_linear_ln_gpu(device, M, act):
     if act:
         ref = F.gelu(ref)
     assert rel_l2(y.float().cpu(), ref) < 8e-3
+
+
+def test_linear_gelu_tanh_cpu_semantics():
+    """act = 2: GELU in the tanh form (torch's approximate="tanh"), the bf16 path's option."""
+    torch.manual_seed(2)
+    x, w, b = torch.randn(5, 64), torch.randn(256, 64) / 8, torch.randn(256)
+    y = torch.ops.amd_dft.linear(x, w, b, 2, None)
+    assert rel_l2(y, F.gelu(F.linear(x, w, b), approximate="tanh")) < 1e-6
+    with pytest.raises(RuntimeError):
+        torch.ops.amd_dft.linear(x, w, b, 3, None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ln", [False, True])
+def test_linear_gelu_tanh_gpu(device, ln):
+    """act = 2 on the hand GEMM (FourCastNet fc1 shape, plain and LN-folded) vs torch's tanh GELU in
+    fp32, and its distance from the erf form stays below bf16 resolution."""
+    torch.manual_seed(11)
+    M, K, N = 1000, 768, 3072
+    x = (torch.randn(M, K) * 1.5 + (3.0 if ln else 0.0)).to(torch.bfloat16)
+    w, b = torch.randn(N, K) / K ** 0.5, torch.randn(N) * 0.1
+    if ln:
+        g, be = torch.randn(K) * 0.2 + 1, torch.randn(K) * 0.1
+        wg, c1, c2 = _ln_fold_operands(w, b, g, be)
+        st = torch.ops.amd_dft.ln_stats(x.to(device), None, 1e-6)
+        y = torch.ops.amd_dft.linear_ln(x.to(device), wg.to(device), c1.to(device), c2.to(device), st, 2)
+        pre = F.linear(F.layer_norm(x.float(), (K,), g, be, 1e-6), w, b)
+    else:
+        wb = w.to(torch.bfloat16)
+        y = torch.ops.amd_dft.linear(x.to(device), wb.to(device), b.to(device), 2, None)
+        pre = F.linear(x.float(), wb.float(), b)
+    yf = y.float().cpu()
+    assert rel_l2(yf, F.gelu(pre, approximate="tanh")) < 8e-3
+    assert (F.gelu(pre, approximate="tanh") - F.gelu(pre)).abs().max() < 5e-4  # the form's own distance
