@@ -37,6 +37,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kNKS = kDftGemmKB / 32;  // 32-deep MFMA k-steps per block
 
+#ifndef DFTW_B0_LDS
+#define DFTW_B0_LDS 1  // twiddle block staged once per workgroup in LDS (0: every wave loads it from L2)
+#endif
+
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -63,7 +67,17 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
   const int rowA = min(row0 + (lane & 15), R - 1);
   const int kq = 8 * (lane >> 4);
   // twiddle block, fragment order [kk][g][re/im][hi/lo][lane]
+  constexpr int NB0 = kNKS * G * 4 * 64;
   bf16x8 bfr[kNKS][G][2][2];
+#if DFTW_B0_LDS
+  // copied once per workgroup through LDS: read by every wave straight from global, the same 16 KB
+  // (G = 2) was fetched ~2700 times at kernel start (44 MB of L2 reads next to the 41.5 MB input)
+  __shared__ bf16x8 b0s[NB0];
+  constexpr int NBT = (NB0 + 64 * NW - 1) / (64 * NW);
+  bf16x8 b0v[NBT];
+#pragma unroll
+  for (int q = 0; q < NBT; ++q) b0v[q] = b0[min(static_cast<int>(threadIdx.x) + 64 * NW * q, NB0 - 1)];
+#else
 #pragma unroll
   for (int kk = 0; kk < kNKS; ++kk)
 #pragma unroll
@@ -72,6 +86,7 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int h = 0; h < 2; ++h) bfr[kk][g][c][h] = b0[(((kk * G + g) * 2 + c) * 2 + h) * 64 + lane];
+#endif
   f32x4 are[G], aim[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) are[g] = aim[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -119,7 +134,24 @@ dftw_r2c_kernel(const void* __restrict__ x, float2* __restrict__ out,
     const int t = static_cast<int>(threadIdx.x) + 64 * NW * q;
     if (t < nph) phs[t] = phv[q];
   }
+#if DFTW_B0_LDS
+#pragma unroll
+  for (int q = 0; q < NBT; ++q) {
+    const int t = static_cast<int>(threadIdx.x) + 64 * NW * q;
+    if (t < NB0) b0s[t] = b0v[q];
+  }
+#endif
   __syncthreads();
+#if DFTW_B0_LDS
+#pragma unroll
+  for (int kk = 0; kk < kNKS; ++kk)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) bfr[kk][g][c][h] = b0s[(((kk * G + g) * 2 + c) * 2 + h) * 64 + lane];
+#endif
   for (int s0 = wv; s0 < nblk; s0 += NW * PF) {
     if (s0 != wv) {
 #pragma unroll
