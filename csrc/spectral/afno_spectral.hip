@@ -210,9 +210,38 @@ struct AfnoArgs {
 template <class S, bool PERM>
 __device__ __forceinline__ int brow(int n) { return PERM ? (n & 1) * S::BS + (n >> 1) : n; }
 
-template <class S, bool TR = false, bool PERM = false>
+// B (weight) fragments of a GEMM's first D k-steps.  The weights do not depend on the tile, so
+// (AFNO_BEARLY16 / AFNO_BEARLY3) GEMM 1's are requested right after the tile's input loads and GEMM 2's right after
+// GEMM 1: their L2 round trips overlap the FFT passes / epilogue 1 instead of opening each GEMM
+// (the barriers between are LDS-only for loads: __syncthreads waits on no outstanding global load).
+// bit 0: GEMM 1's fragments early, bit 1: GEMM 2's; per kernel (bf16 / bf16x3).  Measured
+// (profiles/afno_bearly_r5.txt): bf16x3 both -1.3 %, bf16 GEMM 2 early +3 % (168 VGPRs at 3 workgroups
+// per CU), so the bf16 kernel keeps the in-GEMM prefetch
+#ifndef AFNO_BEARLY16
+#define AFNO_BEARLY16 0
+#endif
+#ifndef AFNO_BEARLY3
+#define AFNO_BEARLY3 3
+#endif
+template <class S>
+struct BFrags {
+  static constexpr int D = AFNO_BPF < S::KS ? AFNO_BPF : S::KS - 1, NQ = D + 1;
+  bf16x8 q[NQ][S::NTW];
+};
+template <class S, bool PERM>
+__device__ __forceinline__ void b_prefetch(BFrags<S>& f, const uint16_t* __restrict__ Bt) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int s2 = 0; s2 < BFrags<S>::D; ++s2)
+#pragma unroll
+    for (int nj = 0; nj < S::NTW; ++nj)
+      f.q[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
+}
+
+template <class S, bool EARLY, bool TR = false, bool PERM = false>
 __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                                          f32x4 (&acc)[S::MT][S::NTW]) {
+                                          f32x4 (&acc)[S::MT][S::NTW], BFrags<S>& f) {
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
@@ -220,14 +249,11 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
   for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 24 KS VGPRs)
-  constexpr int D = AFNO_BPF < S::KS ? AFNO_BPF : S::KS - 1, NQ = D + 1;
-  bf16x8 bq[NQ][S::NTW];
-#pragma unroll
-  for (int s2 = 0; s2 < D; ++s2)
-#pragma unroll
-    for (int nj = 0; nj < S::NTW; ++nj)
-      bq[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
+  // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 24 KS VGPRs); the
+  // first D are in f (b_prefetch)
+  constexpr int D = BFrags<S>::D, NQ = BFrags<S>::NQ;
+  auto& bq = f.q;
+  if constexpr (!EARLY) b_prefetch<S, PERM>(f, Bt);
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
     if (ks + D < S::KS) {
@@ -271,6 +297,9 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   using P0 = HPass<R0, L, NP>;
   using P1 = HPass<R1, L, NP>;
 
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * K;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * K;
+  BFrags<S> pre1, pre2;  // the GEMMs' first k-steps of weight fragments
   // ---------------- forward FFT_H: pass 0 straight from global
   {
     cpair v[P0::Q][R0];
@@ -287,6 +316,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         v[q][r] = make_cpair(c0, c1);
       }
     }
+    if constexpr ((AFNO_BEARLY16 & 1) != 0) b_prefetch<S, false>(pre1, w1t);  // behind the tile loads: pass 0 waits for those only
     h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
@@ -332,12 +362,11 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   __syncthreads();
   // ---------------- GEMM1 + bias + ReLU -> H1 (bf16, in place of A)
   const int lane = tid & 63, w = tid >> 6;
-  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * K;
-  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * K;
   const float* b1 = a.b1 + blk * K;
   const float* b2 = a.b2 + blk * K;
   f32x4 acc[S::MT][S::NTW];
-  gemm_tile<S, AFNO_X3_T>(A, w1t, acc);
+  gemm_tile<S, (AFNO_BEARLY16 & 1) != 0, AFNO_X3_T>(A, w1t, acc, pre1);
+  if constexpr ((AFNO_BEARLY16 & 2) != 0) b_prefetch<S, true>(pre2, w2t);  // overlaps epilogue 1
   __syncthreads();
 #pragma unroll
   for (int nj = 0; nj < S::NTW; ++nj) {
@@ -370,7 +399,7 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
   // ---------------- GEMM2 + bias + softshrink -> X (fp16 complex, conjugated for the inverse):
   // transposed tile with (re, im)-interleaved columns, so a lane holds channels c0, c0 + 1 of one
   // row and writes them as one 8-byte piece (row pitch XP)
-  gemm_tile<S, true, true>(A, w2t, acc);
+  gemm_tile<S, (AFNO_BEARLY16 & 2) != 0, true, true>(A, w2t, acc, pre2);
   __syncthreads();
   const float lam = a.lambda;
 #pragma unroll
@@ -498,9 +527,34 @@ __device__ __forceinline__ void put_split4(uint16_t* Ahi, uint16_t* Alo, int idx
 // TR: the same products with the MFMA operands swapped, so the accumulator tile is the transpose:
 // a lane holds 4 CONSECUTIVE output columns n of one row m (instead of 4 rows of one column) --
 // the epilogue then writes 8-byte bf16x4 pieces instead of single bf16 values.
-template <class S, bool TR = false, bool PERM = false>
+// B (weight) fragments stream from L2 AFNO_BPF3 k-steps ahead: with one k-step of lookahead the L2
+// latency is exposed every k-step (a timing-only build that reused the first k-step's fragments ran
+// 164 us faster, round 2).  The first D k-steps are requested early (b_prefetch_x3, AFNO_BEARLY3).
+template <class S>
+struct BFragsX3 {
+  static constexpr int D0 = S::NTW >= 4 ? 1 : AFNO_BPF3;  // 4 column tiles per wave: no registers for 2
+  static constexpr int D = D0 < S::KS ? D0 : S::KS - 1, NQ = D + 1;
+  bf16x8 h[NQ][S::NTW], l[NQ][S::NTW];
+};
+template <class S, bool PERM>
+__device__ __forceinline__ void b_prefetch_x3(BFragsX3<S>& f, const uint16_t* __restrict__ Bt) {
+  constexpr int K2 = 2 * S::K;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int s2 = 0; s2 < BFragsX3<S>::D; ++s2)
+#pragma unroll
+    for (int nj = 0; nj < S::NTW; ++nj) {
+      const uint16_t* row = Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
+      f.h[s2][nj] = *reinterpret_cast<const bf16x8*>(row);
+      f.l[s2][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
+    }
+}
+
+template <class S, bool EARLY, bool TR = false, bool PERM = false>
 __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, const uint16_t* __restrict__ Al,
-                                             const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW]) {
+                                             const uint16_t* __restrict__ Bt, f32x4 (&acc)[S::MT][S::NTW],
+                                             BFragsX3<S>& f) {
   constexpr int K2 = 2 * S::K;  // split weight row: k32-interleaved [hi(32) | lo(32)] chunks
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -509,20 +563,10 @@ __device__ __forceinline__ void gemm_tile_x3(const uint16_t* __restrict__ Ah, co
   for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B (weight) fragments stream from L2 AFNO_BPF3 k-steps ahead: with one k-step of lookahead
-  // the L2 latency is exposed every k-step (a timing-only build that reused the first k-step's
-  // fragments ran 164 us faster, round 2)
-  constexpr int D0 = S::NTW >= 4 ? 1 : AFNO_BPF3;  // 4 column tiles per wave: no registers for 2
-  constexpr int D = D0 < S::KS ? D0 : S::KS - 1, NQ = D + 1;
-  bf16x8 bh[NQ][S::NTW], bl[NQ][S::NTW];
-#pragma unroll
-  for (int s2 = 0; s2 < D; ++s2)
-#pragma unroll
-    for (int nj = 0; nj < S::NTW; ++nj) {
-      const uint16_t* row = Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * K2 + s2 * 64 + kq * 8;
-      bh[s2][nj] = *reinterpret_cast<const bf16x8*>(row);
-      bl[s2][nj] = *reinterpret_cast<const bf16x8*>(row + 32);
-    }
+  constexpr int D = BFragsX3<S>::D, NQ = BFragsX3<S>::NQ;
+  auto& bh = f.h;
+  auto& bl = f.l;
+  if constexpr (!EARLY) b_prefetch_x3<S, PERM>(f, Bt);
 #pragma unroll
   for (int ks = 0; ks < S::KS; ++ks) {
     if (ks + D < S::KS) {
@@ -588,6 +632,9 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   float* yout = static_cast<float*>(a.y) + base;
   using P0 = HPass<R0, L, NP>;
   using P1 = HPass<R1, L, NP>;
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * 2 * K;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * 2 * K;
+  BFragsX3<S> pre1, pre2;  // the GEMMs' first k-steps of weight fragments
   // ---------------- forward FFT_H: pass 0 straight from global
   {
     cpair v[P0::Q][R0];
@@ -604,6 +651,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
         v[q][r] = make_cpair(c0, c1);
       }
     }
+    if constexpr ((AFNO_BEARLY3 & 1) != 0) b_prefetch_x3<S, false>(pre1, w1t);  // behind the tile loads: pass 0 waits for those only
     h_twiddle_dft<R0, L, NP, 1, P0::Q>(v, nullptr);  // first pass: no twiddles
 #pragma unroll
     for (int q = 0; q < P0::Q; ++q) {
@@ -650,12 +698,11 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   __syncthreads();
   AFNO_STAMP(4, __builtin_amdgcn_s_memtime());
   const int lane = tid & 63, w = tid >> 6;
-  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * 2 * K;
-  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * 2 * K;
   const float* b1 = a.b1 + blk * K;
   const float* b2 = a.b2 + blk * K;
   f32x4 acc[S::MT][S::NTW];
-  gemm_tile_x3<S, AFNO_X3_T>(Ah, Al, w1t, acc);
+  gemm_tile_x3<S, (AFNO_BEARLY3 & 1) != 0, AFNO_X3_T>(Ah, Al, w1t, acc, pre1);
+  if constexpr ((AFNO_BEARLY3 & 2) != 0) b_prefetch_x3<S, true>(pre2, w2t);  // overlaps epilogue 1
   __syncthreads();
   AFNO_STAMP(5, __builtin_amdgcn_s_memtime());
 #pragma unroll
@@ -685,7 +732,7 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
   __syncthreads();
   AFNO_STAMP(6, __builtin_amdgcn_s_memtime());
   // transposed tile, (re, im)-interleaved columns: one 16-byte write of two channels per lane and row
-  gemm_tile_x3<S, true, true>(Ah, Al, w2t, acc);
+  gemm_tile_x3<S, (AFNO_BEARLY3 & 2) != 0, true, true>(Ah, Al, w2t, acc, pre2);
   __syncthreads();
   AFNO_STAMP(7, __builtin_amdgcn_s_memtime());
   const float lam = a.lambda;
