@@ -111,6 +111,11 @@ struct AfnoShape {
   static constexpr int64_t MAIN16 = cmax(cmax(L * BS * 4, L * XP * 4), 32 * MT * APitch);
   static constexpr int64_t MAIN32 = cmax(cmax(2 * L * BS * 4, 2 * L * XP * 4), 64 * MT * APitch);
   static constexpr int64_t LDS16 = MAIN16 + TWN * 8, LDS32 = MAIN32 + TWN * 8;
+  static constexpr int64_t LDS16X2 = 2 * MAIN16 + TWN * 8;  // two-tile bf16 kernel: one region per tile
+  // the two-tile kernel where two of its workgroups share a CU and its 2 MT x NTW accumulators fit
+  // beside the FFT registers without spilling (BS <= 96)
+  static constexpr bool TPW2 = BS <= 96 && 2 * LDS16X2 <= 160 * 1024;
+  static_assert(MAIN16 % 16 == 0, "tile regions 16-byte aligned");
   static_assert(R0 * R1 == L && BS % 16 == 0 && L <= 128, "AFNO instance geometry");
 };
 
@@ -239,14 +244,17 @@ __device__ __forceinline__ void b_prefetch(BFrags<S>& f, const uint16_t* __restr
       f.q[s2][nj] = *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + s2 * 32 + kq * 8);
 }
 
-template <class S, bool EARLY, bool TR = false, bool PERM = false>
+// TPW > 1 (two-tile kernel): row tiles mi of TPW (b, kw) tiles, tile mi / MT's A in its own LDS region
+// (RSE bf16 elements apart); every weight fragment then feeds TPW x MT row tiles
+template <class S, bool EARLY, bool TR = false, bool PERM = false, int TPW = 1>
 __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
-                                          f32x4 (&acc)[S::MT][S::NTW], BFrags<S>& f) {
+                                          f32x4 (&acc)[TPW * S::MT][S::NTW], BFrags<S>& f) {
+  constexpr int RSE = static_cast<int>(S::MAIN16 / 2);
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
 #pragma unroll
-  for (int mi = 0; mi < S::MT; ++mi)
+  for (int mi = 0; mi < TPW * S::MT; ++mi)
 #pragma unroll
     for (int nj = 0; nj < S::NTW; ++nj) acc[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
   // B fragments stream from L2 AFNO_BPF k-steps ahead (a full preload would need 24 KS VGPRs); the
@@ -263,12 +271,12 @@ __device__ __forceinline__ void gemm_tile(const uint16_t* __restrict__ A, const 
             *reinterpret_cast<const bf16x8*>(Bt + brow<S, PERM>(S::ct(w, nj) * 16 + r16) * S::K + (ks + D) * 32 + kq * 8);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of its use (see gemm_tile_x3)
-    bf16x8 afr[S::MT];
+    bf16x8 afr[TPW * S::MT];
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
-      afr[mi] = *reinterpret_cast<const bf16x8*>(A + (mi * 16 + r16) * S::APitch + ks * 32 + kq * 8);
+    for (int mi = 0; mi < TPW * S::MT; ++mi)
+      afr[mi] = *reinterpret_cast<const bf16x8*>(A + (mi / S::MT) * RSE + ((mi % S::MT) * 16 + r16) * S::APitch + ks * 32 + kq * 8);
 #pragma unroll
-    for (int mi = 0; mi < S::MT; ++mi)
+    for (int mi = 0; mi < TPW * S::MT; ++mi)
 #pragma unroll
       for (int nj = 0; nj < S::NTW; ++nj) {
         if constexpr (TR) acc[mi][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks % NQ][nj], afr[mi], acc[mi][nj], 0, 0, 0);
@@ -470,6 +478,219 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
         for (int r = 0; r < R1; ++r) {
           const int n = j + r * R0;
           stc2<BFO>(yout, n * row_stride + 4 * tp, make_float2(v[q][r].re[0], -v[q][r].im[0]),
+                    make_float2(v[q][r].re[1], -v[q][r].im[1]));
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ two tiles per workgroup (bf16)
+// The same stages for two (b, kw) tiles of one channel block: each tile has its own LDS region
+// (staging / A / X, MAIN16 bytes), the FFT passes run both tiles between the same barriers, and the two
+// GEMMs see 2 MT row tiles -- every weight fragment loaded from L2 feeds twice the MFMAs, which is what
+// binds the GEMM phases (profiles/afno_nt512_r5.txt: doubling the fragment loads per MFMA cost +48 %).
+// LDS 2 x 38.4 KB at H = 90, BS = 96: 2 workgroups (4 tiles) per CU instead of 3 single-tile ones.
+#ifndef AFNO_TPW16
+#define AFNO_TPW16 2  // (b, kw) tiles per workgroup of the bf16 kernel: 1 or 2
+#endif
+template <class S, bool BFI, bool BFO>
+__global__ void __launch_bounds__(kNT, 2) afno_spectral2_kernel(const AfnoArgs a) {
+  static_assert(AFNO_X3_T, "the two-tile kernel has only the transposed GEMM-1 epilogue");
+  constexpr int L = S::L, R0 = S::R0, R1 = S::R1, BS = S::BS, NP = S::NP, K = S::K, AP = S::APitch;
+  constexpr int64_t RB = S::MAIN16;  // bytes per tile region
+  extern __shared__ __attribute__((aligned(16))) h2_t lds[];
+  auto reg = [&](int t) { return reinterpret_cast<h2_t*>(reinterpret_cast<char*>(lds) + t * RB); };
+  auto areg = [&](int t) { return reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(lds) + t * RB); };
+  float2* twl = reinterpret_cast<float2*>(reinterpret_cast<char*>(lds) + 2 * RB);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < S::TWN; i += kNT) twl[i] = a.tw[i];  // visible after the pass-0 barrier
+  const int blk = blockIdx.x % a.NB;
+  const int pair = blockIdx.x / a.NB;  // tiles bk = 2 pair, 2 pair + 1 (host: B KM even)
+  const int row_stride = a.KM * a.C * 2;
+  const void* xin[2];
+  void* yout[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int bk = 2 * pair + t, kw = bk % a.KM, b = bk / a.KM;
+    AMD_DFT_DEV_CHECK((blk + 1) * BS <= a.C && kw < a.KM && L == a.H, "afno_spectral2_kernel");
+    const int64_t base = ((static_cast<int64_t>(b) * L * a.KM + kw) * a.C + blk * BS) * 2;
+    xin[t] = static_cast<const char*>(a.x) + base * (BFI ? 2 : 4);
+    yout[t] = static_cast<char*>(a.y) + base * (BFO ? 2 : 4);
+  }
+  using P0 = HPass<R0, L, NP>;
+  using P1 = HPass<R1, L, NP>;
+  const uint16_t* w1t = a.w1t + static_cast<int64_t>(blk) * K * K;
+  const uint16_t* w2t = a.w2t + static_cast<int64_t>(blk) * K * K;
+  BFrags<S> pre1, pre2;
+  // ---------------- forward FFT_H: pass 0 straight from global, both tiles' loads first
+  {
+    cpair v[2][P0::Q][R0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < P0::Q; ++q) {
+        const int bb = tid + q * kNT;
+        const bool ok = P0::NB % kNT == 0 || bb < P0::NB;
+        const int bc = ok ? bb : 0;
+        const int tp = bc % NP, j = bc / NP;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+          float2 c0, c1;
+          ldc2<BFI>(xin[t], (j + r * P0::LR) * row_stride + 4 * tp, c0, c1);
+          v[t][q][r] = make_cpair(c0, c1);
+        }
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      h_twiddle_dft<R0, L, NP, 1, P0::Q>(v[t], nullptr);
+#pragma unroll
+      for (int q = 0; q < P0::Q; ++q) {
+        const int bb = tid + q * kNT;
+        if (P0::NB % kNT == 0 || bb < P0::NB) {
+          const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+          for (int r = 0; r < R0; ++r) st_hp(reg(t), (j * R0 + r) * BS + 2 * tp, v[t][q][r]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> A_t (bf16, [h][re | im])
+  {
+    cpair v[2][P1::Q][R1];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < P1::Q; ++q) {
+        const int bb = tid + q * kNT;
+        if (P1::NB % kNT == 0 || bb < P1::NB) {
+          const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+          for (int r = 0; r < R1; ++r) v[t][q][r] = ld_hp(reg(t), (j + r * P1::LR) * BS + 2 * tp);
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      h_twiddle_dft<R1, L, NP, R0, P1::Q>(v[t], twl);
+#pragma unroll
+      for (int q = 0; q < P1::Q; ++q) {
+        const int bb = tid + q * kNT;
+        if (P1::NB % kNT == 0 || bb < P1::NB) {
+          const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+          for (int r = 0; r < R1; ++r) {
+            const int n = j + r * R0;
+            uint32_t* row = reinterpret_cast<uint32_t*>(areg(t) + n * AP);
+            row[tp] = static_cast<uint32_t>(f2bf16(v[t][q][r].re[0])) | (static_cast<uint32_t>(f2bf16(v[t][q][r].re[1])) << 16);
+            row[NP + tp] = static_cast<uint32_t>(f2bf16(v[t][q][r].im[0])) | (static_cast<uint32_t>(f2bf16(v[t][q][r].im[1])) << 16);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- GEMM1 + bias + ReLU -> H1 (in place of A_t)
+  const int lane = tid & 63, w = tid >> 6;
+  const float* b1 = a.b1 + blk * K;
+  const float* b2 = a.b2 + blk * K;
+  f32x4 acc[2 * S::MT][S::NTW];
+  gemm_tile<S, false, AFNO_X3_T, false, 2>(areg(0), w1t, acc, pre1);
+  __syncthreads();
+#pragma unroll
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;
+    const int n0 = (S::NTW * w + nj) * 16 + 4 * (lane >> 4);
+    const float4 bias = *reinterpret_cast<const float4*>(b1 + n0);
+#pragma unroll
+    for (int mi = 0; mi < 2 * S::MT; ++mi) {
+      const int m = (mi % S::MT) * 16 + (lane & 15);
+      *reinterpret_cast<uint2*>(areg(mi / S::MT) + m * AP + n0) =
+          make_uint2(static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][0] + bias.x, 0.f))) |
+                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][1] + bias.y, 0.f))) << 16),
+                     static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][2] + bias.z, 0.f))) |
+                         (static_cast<uint32_t>(f2bf16(fmaxf(acc[mi][nj][3] + bias.w, 0.f))) << 16));
+    }
+  }
+  __syncthreads();
+  // ---------------- GEMM2 + bias + softshrink -> X_t (fp16, pitch XP, conjugated)
+  gemm_tile<S, false, true, true, 2>(areg(0), w2t, acc, pre2);
+  __syncthreads();
+  const float lam = a.lambda;
+#pragma unroll
+  for (int nj = 0; nj < S::NTW; ++nj) {
+    if (!S::ct_live(w, nj)) continue;
+    const int c0 = ((S::NTW * w + nj) * 16 + 4 * (lane >> 4)) >> 1;
+    const float2 bre = *reinterpret_cast<const float2*>(b2 + c0), bim = *reinterpret_cast<const float2*>(b2 + BS + c0);
+#pragma unroll
+    for (int mi = 0; mi < 2 * S::MT; ++mi) {
+      const int m = (mi % S::MT) * 16 + (lane & 15);
+      if (m < L) {
+        const float v0 = acc[mi][nj][0] + bre.x, v1 = acc[mi][nj][1] + bim.x;
+        const float v2 = acc[mi][nj][2] + bre.y, v3 = acc[mi][nj][3] + bim.y;
+        *reinterpret_cast<h4_t*>(reg(mi / S::MT) + m * S::XP + c0) =
+            h4_t{static_cast<_Float16>(v0 - __builtin_amdgcn_fmed3f(v0, -lam, lam)),
+                 static_cast<_Float16>(__builtin_amdgcn_fmed3f(v1, -lam, lam) - v1),
+                 static_cast<_Float16>(v2 - __builtin_amdgcn_fmed3f(v2, -lam, lam)),
+                 static_cast<_Float16>(__builtin_amdgcn_fmed3f(v3, -lam, lam) - v3)};
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- inverse FFT_H: pass 0 LDS (pitch XP) -> LDS (pitch BS), both tiles
+  {
+    cpair v[2][P0::Q][R0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < P0::Q; ++q) {
+        const int bb = tid + q * kNT;
+        if (P0::NB % kNT == 0 || bb < P0::NB) {
+          const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+          for (int r = 0; r < R0; ++r) v[t][q][r] = ld_hp(reg(t), (j + r * P0::LR) * S::XP + 2 * tp);
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      h_twiddle_dft<R0, L, NP, 1, P0::Q>(v[t], nullptr);
+#pragma unroll
+      for (int q = 0; q < P0::Q; ++q) {
+        const int bb = tid + q * kNT;
+        if (P0::NB % kNT == 0 || bb < P0::NB) {
+          const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+          for (int r = 0; r < R0; ++r) st_hp(reg(t), (j * R0 + r) * BS + 2 * tp, v[t][q][r]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------- pass 1: LDS -> registers -> global (conj back), one tile at a time
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    cpair v[P1::Q][R1];
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[q][r] = ld_hp(reg(t), (j + r * P1::LR) * BS + 2 * tp);
+      }
+    }
+    h_twiddle_dft<R1, L, NP, R0, P1::Q>(v, twl);
+#pragma unroll
+    for (int q = 0; q < P1::Q; ++q) {
+      const int bb = tid + q * kNT;
+      if (P1::NB % kNT == 0 || bb < P1::NB) {
+        const int tp = bb % NP, j = bb / NP;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          const int n = j + r * R0;
+          stc2<BFO>(yout[t], n * row_stride + 4 * tp, make_float2(v[q][r].re[0], -v[q][r].im[0]),
                     make_float2(v[q][r].re[1], -v[q][r].im[1]));
         }
       }
@@ -835,17 +1056,25 @@ __global__ void __launch_bounds__(kNT, 2) afno_spectral_x3_kernel(const AfnoArgs
 using KernFn = void (*)(AfnoArgs);
 struct AfnoInstance {
   int H, R0, R1, BS;
-  int64_t lds_bf16, lds_x3;  // dynamic LDS bytes of the bf16 and bf16x3 kernels
-  KernFn bf16[2][2];         // [bf16_in][bf16_out]
+  int64_t lds_bf16, lds_x3, lds_bf16x2;  // dynamic LDS bytes of the bf16, bf16x3 and two-tile bf16 kernels
+  KernFn bf16[2][2];                     // [bf16_in][bf16_out]
   KernFn x3;
+  KernFn bf16x2[2][2];                   // two (b, kw) tiles per workgroup
 };
 
 template <class S>
 AfnoInstance make_instance() {
-  AfnoInstance r{S::L, S::R0, S::R1, S::BS, S::LDS16, S::LDS32,
+  AfnoInstance r{S::L, S::R0, S::R1, S::BS, S::LDS16, S::LDS32, S::LDS16X2,
                  {{afno_spectral_kernel<S, false, false>, afno_spectral_kernel<S, false, true>},
                   {afno_spectral_kernel<S, true, false>, afno_spectral_kernel<S, true, true>}},
-                 afno_spectral_x3_kernel<S>};
+                 afno_spectral_x3_kernel<S>,
+                 {{nullptr, nullptr}, {nullptr, nullptr}}};
+  if constexpr (S::TPW2) {
+    r.bf16x2[0][0] = afno_spectral2_kernel<S, false, false>;
+    r.bf16x2[0][1] = afno_spectral2_kernel<S, false, true>;
+    r.bf16x2[1][0] = afno_spectral2_kernel<S, true, false>;
+    r.bf16x2[1][1] = afno_spectral2_kernel<S, true, true>;
+  }
   return r;
 }
 
@@ -912,6 +1141,10 @@ void launch_afno_spectral(const AfnoLaunch& p, void* stream) {
   if (p.x3) {
     if (p.bf16_in || p.bf16_out) throw std::runtime_error("amd_dft: afno_spectral: the bf16x3 variant is fp32 in/out");
     launch_kernel(in->x3, in->lds_x3, nblocks, a, stream);
+    return;
+  }
+  if (AFNO_TPW16 == 2 && in->bf16x2[0][0] != nullptr && (static_cast<int64_t>(p.B) * p.KM) % 2 == 0) {
+    launch_kernel(in->bf16x2[p.bf16_in ? 1 : 0][p.bf16_out ? 1 : 0], in->lds_bf16x2, nblocks / 2, a, stream);
     return;
   }
   launch_kernel(in->bf16[p.bf16_in ? 1 : 0][p.bf16_out ? 1 : 0], in->lds_bf16, nblocks, a, stream);

@@ -97,6 +97,25 @@ def test_afno_spectral_shapes_bf16(device, H, bs):
     assert rel_l2(outb.float(), ref) < 1.2e-2
 
 
+@pytest.mark.parametrize("H,bs", sorted(S.AFNO_FUSED_SHAPES))
+@pytest.mark.parametrize("KM", [3, 4])
+def test_afno_spectral_tile_pairs_bf16(device, H, bs, KM):
+    """bf16 kernel with B * KM even (two (b, kw) tiles per workgroup where the instance has the two-tile
+    kernel) and odd (one tile per workgroup), bf16 and fp32 spectra, against the CPU op."""
+    torch.manual_seed(H * 31 + bs + KM)
+    B, nb = 2, 2
+    C = nb * bs
+    xw = torch.randn(B, H, KM, C, 2)
+    w1, b1, w2, b2 = _afno_params(nb, bs, scale=0.05, seed=bs + 1)
+    w1t, w2t, b1p, b2p = S.pack_afno_weights(w1, b1, w2, b2)
+    ref = torch.ops.amd_dft.afno_spectral(xw, w1t, w2t, b1p, b2p, 0.01)
+    args = [t.to(device) for t in (w1t, w2t, b1p, b2p)]
+    out = torch.ops.amd_dft.afno_spectral(xw.to(device), *args, 0.01)
+    assert rel_l2(out, ref) < 6e-3
+    outb = torch.ops.amd_dft.afno_spectral(xw.to(device, torch.bfloat16), *args, 0.01)
+    assert rel_l2(outb.float(), ref) < 1.2e-2
+
+
 @pytest.mark.parametrize("H,bs", _NEW_SHAPES)
 def test_afno_spectral_shapes_x3(device, H, bs):
     torch.manual_seed(H * 7 + bs)
