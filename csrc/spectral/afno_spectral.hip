@@ -488,9 +488,9 @@ __global__ void __launch_bounds__(kNT, S::OCC) afno_spectral_kernel(const AfnoAr
 // ------------------------------------------------------------------ two tiles per workgroup (bf16)
 // The same stages for two (b, kw) tiles of one channel block: each tile has its own LDS region
 // (staging / A / X, MAIN16 bytes), the FFT passes run both tiles between the same barriers, and the two
-// GEMMs see 2 MT row tiles -- every weight fragment loaded from L2 feeds twice the MFMAs, which is what
-// binds the GEMM phases (profiles/afno_nt512_r5.txt: doubling the fragment loads per MFMA cost +48 %).
-// LDS 2 x 38.4 KB at H = 90, BS = 96: 2 workgroups (4 tiles) per CU instead of 3 single-tile ones.
+// GEMMs see 2 MT row tiles -- every weight fragment loaded from L2 feeds twice the MFMAs.  LDS 2 x 38.4 KB
+// at H = 90, BS = 96: 2 workgroups (4 tiles) per CU instead of 3 single-tile ones; -2 % at [32, 90, 46, 768]
+// (profiles/afno_two_tile_r5.txt).
 #ifndef AFNO_TPW16
 #define AFNO_TPW16 2  // (b, kw) tiles per workgroup of the bf16 kernel: 1 or 2
 #endif
