@@ -29,6 +29,10 @@ struct GemmLaunch {
   int direct_epi = 0;        // gemm.hip MODE 0: 1 = store straight from the MFMA layout (A/B only)
   float* stats_part = nullptr;       // + residual output (fp32 split mode or bf16): [M, N/64, 2] (mean, M2) per 64-feature chunk
   const float* stats_pre = nullptr;  // [N] added to the output before the statistics (required with stats_part)
+  // split-pair residual (fp32 fc2 with statistics only): residual = [M, 2N] bf16x3 pairs of x - m (k32-interleaved)
+  // and res_mean = [M, 2] whose .x is the per-token shift m
+  const float* res_mean = nullptr;
+  const uint16_t* res_lo2 = nullptr;  // optional with res_mean: [M, N] bf16 third split term of x - m
   int ntiles = 0;            // set by launch_gemm: > 0 = persistent grid (gemm.hip PERSIST), tiles in turn
 #ifdef AMD_DFT_GEMM_STAMPS
   long long* stamps = nullptr;  // diagnostic build only (bench/gemm_stamps.hip): per-block phase clocks

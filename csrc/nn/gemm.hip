@@ -306,7 +306,7 @@ __device__ __forceinline__ float row_sum16(float x) {
 // (MI_DFT_GEMM_PERSIST=1, bit-exact: tests/test_gemm_variants.py).
 // NT: N % 256 != 0 -- the last feature panel is ragged (N % 64 == 0): its W rows past N are clamped in
 // the DMA, its bias / c1 loads clamped, and the epilogue halves past N store nothing (wave-uniform).
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false,
+template <int ACT, bool BIAS, int RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool PERSIST = false,
           bool NT = false>
 __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   static_assert(!PERSIST || MODE == 0, "persistent tiles: token-major operands and outputs only");
@@ -618,7 +618,15 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         const int c = lane % LPR, rsub = lane / LPR;
         // residual per lane and pass: OUT 1 4 fp32, OUT 0 8 bf16, OUT 2 8 fp32
         struct F8 { float4 a, b; };
-        typedef typename std::conditional<OUT == 1, float4, typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
+        // RES 2 (OUT 1): the residual as bf16x3 split pairs of x - m (k32-interleaved rows, c2r_ln_add_split's
+        // pairs) plus the per-token shift m = p.res_mean[2 t]: x = m + (hi + lo), 2^-18 of |x - m| off
+        // RES 3: plus the third split term p.res_lo2 [M, N] bf16 (x to ~2^-27 of |x - m|, below fp32 rounding)
+        struct P4 { uint2 h, l; float m; };
+        struct P6 { uint2 h, l, t; float m; };
+        typedef typename std::conditional<
+            OUT == 1, typename std::conditional<RES == 3, P6, typename std::conditional<RES == 2, P4, float4>::type>::type,
+            typename std::conditional<OUT == 2, F8, uint4>::type>::type RT;
+        static_assert(RES < 2 || (OUT == 1 && SPLIT), "split-pair residual: fp32 output of the bf16x3 GEMM");
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int fh = f0 + wr * 128 + h * 64;  // first feature of this half
@@ -630,13 +638,24 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
           // for OUT 2 (8 fp32 per pass: the whole half would hold 128 VGPRs beside the accumulators)
           // -- each of those spilled when the whole half was prefetched
-          constexpr int PD = (OUT == 2 || PERSIST) ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
+          constexpr int PD = RES == 3 ? 2 : (OUT == 2 || PERSIST) ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
           auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
             int rt = min(tbase + it * RPI + rsub, M - 1);
             if constexpr (MODE == 1) {
               if (p.res_rows > 0) rt %= p.res_rows;  // position embedding broadcast over the batch
             }
-            if constexpr (OUT == 2) {
+            if constexpr (RES >= 2) {
+              const int f = fh + 4 * c;  // 4 features in one 32-chunk: hi at (f / 32) 64 + f % 32, lo 32 after
+              const uint16_t* rp = static_cast<const uint16_t*>(p.residual) + static_cast<int64_t>(rt) * (2 * N) +
+                                   (f >> 5) * 64 + (f & 31);
+              if constexpr (RES == 3)
+                rr[it] = P6{*reinterpret_cast<const uint2*>(rp), *reinterpret_cast<const uint2*>(rp + 32),
+                            *reinterpret_cast<const uint2*>(p.res_lo2 + static_cast<int64_t>(rt) * N + f),
+                            p.res_mean[static_cast<int64_t>(rt) * 2]};
+              else
+                rr[it] = P4{*reinterpret_cast<const uint2*>(rp), *reinterpret_cast<const uint2*>(rp + 32),
+                            p.res_mean[static_cast<int64_t>(rt) * 2]};
+            } else if constexpr (OUT == 2) {
               const int64_t o = static_cast<int64_t>(rt) * N + fh + 8 * c;
               const float* rp = static_cast<const float*>(p.residual) + o;
               rr[it] = F8{*reinterpret_cast<const float4*>(rp), *reinterpret_cast<const float4*>(rp + 4)};
@@ -699,7 +718,22 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
               const char* rp = reg + (row - sh * (64 / SUB)) * 256;  // same row & 15 (64 / SUB is a multiple of 16)
               if constexpr (OUT == 1) {
                 float4 v = *reinterpret_cast<const float4*>(rp + ((c ^ (row & 15)) << 4));
-                if constexpr (RES) {
+                if constexpr (RES >= 2) {
+                  const auto& q = rr[it];
+                  const auto bf = [](uint32_t w, bool hi) { return __uint_as_float(hi ? (w & 0xffff0000u) : (w << 16)); };
+                  float r4[4] = {bf(q.h.x, false) + bf(q.l.x, false), bf(q.h.x, true) + bf(q.l.x, true),
+                                 bf(q.h.y, false) + bf(q.l.y, false), bf(q.h.y, true) + bf(q.l.y, true)};
+                  if constexpr (RES == 3) {
+                    r4[0] += bf(q.t.x, false);
+                    r4[1] += bf(q.t.x, true);
+                    r4[2] += bf(q.t.y, false);
+                    r4[3] += bf(q.t.y, true);
+                  }
+                  v.x += r4[0] + q.m;
+                  v.y += r4[1] + q.m;
+                  v.z += r4[2] + q.m;
+                  v.w += r4[3] + q.m;
+                } else if constexpr (RES) {
                   v.x += rr[it].x;
                   v.y += rr[it].y;
                   v.z += rr[it].z;
@@ -884,7 +918,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         return;
       }
     }
-    constexpr bool ERES = RES;
+    constexpr bool ERES = RES == 1;  // RES 2 (split-pair residual) only with the staged statistics epilogue (host-checked)
     ResT rq[ERES ? 2 : 1][2][4];  // [buffer][i of the pair][j]
     if constexpr (ERES) {
 #pragma unroll
@@ -949,7 +983,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   }  // tile loop
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST, bool NT>
+template <int ACT, bool BIAS, int RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST, bool NT>
 void launch_kernel_nt(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   auto kern = gemm_bf16_kernel<ACT, BIAS, RES, LN, MODE, SPLIT, OUT, STATS, PERSIST, NT>;
   // the dynamic-LDS limit is a per-device function attribute: set it once per (instance, device)
@@ -964,7 +998,7 @@ void launch_kernel_nt(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), kLds, st, p);
 }
 
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST>
+template <int ACT, bool BIAS, int RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS, bool PERSIST>
 void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   if constexpr (!PERSIST && MODE != 2) {
     if (p.N % kBF != 0) {  // ragged last feature panel (launch_gemm: staged epilogue, one tile per workgroup)
@@ -978,7 +1012,7 @@ void launch_kernel(const GemmLaunch& p, hipStream_t st, dim3 grid) {
 
 // CAN_PERSIST: the instance has a persistent variant (the fp32 block's GEMMs); p.ntiles > 0 (set by
 // launch_gemm, MI_DFT_GEMM_PERSIST=1) selects it with grid = workgroups, else one tile per workgroup
-template <int ACT, bool BIAS, bool RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool CAN_PERSIST = false>
+template <int ACT, bool BIAS, int RES, bool LN, int MODE, bool SPLIT, int OUT, bool STATS = false, bool CAN_PERSIST = false>
 void launch_one(const GemmLaunch& p, hipStream_t st, dim3 grid) {
   if constexpr (CAN_PERSIST) {
     if (p.ntiles > 0) {
@@ -1040,7 +1074,9 @@ void launch_split(const GemmLaunch& p, hipStream_t st, dim3 grid) {
     if (!p.stats_pre) throw std::runtime_error("amd_dft: gemm: statistics need stats_pre (zeros when there is none)");
     if constexpr (ACT == 0 && !BIAS) {
       if (p.direct_epi) throw std::runtime_error("amd_dft: gemm: statistics need the LDS-staged epilogue");
-      launch_one<ACT, BIAS, true, false, 0, true, 1, true, true>(p, st, grid);
+      if (p.res_mean && p.res_lo2) launch_one<ACT, BIAS, 3, false, 0, true, 1, true, true>(p, st, grid);
+      else if (p.res_mean) launch_one<ACT, BIAS, 2, false, 0, true, 1, true, true>(p, st, grid);
+      else launch_one<ACT, BIAS, true, false, 0, true, 1, true, true>(p, st, grid);
     } else {
       throw std::runtime_error("amd_dft: gemm: output statistics only without activation and bias");
     }

@@ -928,10 +928,28 @@ void check_split_out(const at::Tensor& X, const at::Tensor& x, const char* op) {
   TORCH_CHECK(x.size(-1) % 64 == 0, "amd_dft.", op, ": C must be a multiple of 64");
 }
 
+// (out, pairs, part) of the ATen paths -> out_mode's first result: out (1), its lo2 term
+// bf16(out - m - (hi + lo)) (2, m = stats[:, 0], the pairs' centring) or nothing (0)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> out_mode_result(std::tuple<at::Tensor, at::Tensor, at::Tensor> r,
+                                                                const at::Tensor& stats, int64_t out_mode) {
+  TORCH_CHECK(out_mode >= 0 && out_mode <= 2, "amd_dft.c2r_ln_add_split: out_mode must be 0, 1 or 2");
+  if (out_mode == 1) return r;
+  at::Tensor& out = std::get<0>(r);
+  if (out_mode == 0) {
+    out = at::empty({0}, out.options());
+    return r;
+  }
+  const int64_t C = out.size(-1);
+  at::Tensor z = out.reshape({-1, C}).to(at::kFloat) - stats.to(at::kFloat).reshape({-1, 2}).select(1, 0).unsqueeze(1);
+  at::Tensor pr = std::get<1>(r).to(at::kFloat).reshape({-1, C / 32, 2, 32});
+  out = (z - (pr.select(2, 0) + pr.select(2, 1)).reshape({-1, C})).to(at::kBFloat16);
+  return r;
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::Tensor& X_, int64_t dim, int64_t n, double scale,
                                                                      const at::Tensor& x_, const at::Tensor& stats_,
                                                                      const at::Tensor& g_, const at::Tensor& b_,
-                                                                     const std::optional<at::Tensor>& pre_) {
+                                                                     const std::optional<at::Tensor>& pre_, int64_t out_mode) {
   const c10::DeviceGuard guard(X_.device());
   check_ln_args(x_, dim, stats_, g_, b_, pre_, "c2r_ln_add_split");
   check_split_out(X_, x_, "c2r_ln_add_split");
@@ -949,7 +967,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::T
     at::Tensor pre;
     if (pre_.has_value()) pre = pre_->to(at::kFloat).contiguous();
     const int64_t M = x.numel() / C;
-    at::Tensor out = at::empty_like(x);
+    // out_mode 1: the fp32 output; 2: instead its bf16 third split term (lo2, [M, C]); 0: neither
+    TORCH_CHECK(out_mode >= 0 && out_mode <= 2, "amd_dft.c2r_ln_add_split: out_mode must be 0, 1 or 2");
+    at::Tensor out = out_mode == 1 ? at::empty_like(x)
+                                   : out_mode == 2 ? at::empty({M, C}, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options());
     at::Tensor pairs = at::empty({M, 2 * C}, x.options().dtype(at::kBFloat16));
     at::Tensor part = at::empty({M, C / 64, 2}, x.options());
     AfnoWLaunch p;  // fp32 two-pass kernel with the split / statistics epilogue (afno_wfft.hip)
@@ -959,7 +980,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::T
     p.beta = b.data_ptr<float>();
     p.pre = pre_.has_value() ? pre.data_ptr<float>() : nullptr;
     p.spec = X.data_ptr();
-    p.out = out.data_ptr();
+    p.out = out_mode == 1 ? out.data_ptr() : nullptr;
+    p.lo2 = out_mode == 2 ? reinterpret_cast<uint16_t*>(out.data_ptr()) : nullptr;
     p.pairs = reinterpret_cast<uint16_t*>(pairs.data_ptr());
     p.part = part.data_ptr<float>();
     p.O = static_cast<int>(M / n);
@@ -972,15 +994,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cuda(const at::T
     return {checked(out, "c2r_ln_add_split"), pairs, part};
   }
   fallback_note("c2r_ln_add_split", "no fused W-transform for this shape: c2r_ln_add + ATen split / statistics");
-  return split_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_), stats_);
+  auto r = split_and_partials(c2r_ln_add_cuda(X, dim, n, scale, x, stats_, g_, b_, pre_), stats_);
+  return out_mode_result(r, stats_, out_mode);
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_cpu(const at::Tensor& X, int64_t dim, int64_t n, double scale,
                                                                     const at::Tensor& x, const at::Tensor& stats,
                                                                     const at::Tensor& g, const at::Tensor& b,
-                                                                    const std::optional<at::Tensor>& pre) {
+                                                                    const std::optional<at::Tensor>& pre, int64_t out_mode) {
   check_split_out(X, x, "c2r_ln_add_split");
-  return split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre), stats);
+  auto r = split_and_partials(c2r_ln_add_cpu(X, dim, n, scale, x, stats, g, b, pre), stats);
+  return out_mode_result(r, stats, out_mode);
 }
 
 // bf16 block: c2r_ln_add + the next LayerNorm's per-64-channel partials (mean, M2) of the STORED
@@ -1060,9 +1084,12 @@ std::tuple<at::Tensor, at::Tensor> c2r_ln_add_part_meta(const at::Tensor&, int64
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> c2r_ln_add_split_meta(const at::Tensor&, int64_t, int64_t, double,
                                                                      const at::Tensor& x, const at::Tensor&, const at::Tensor&,
-                                                                     const at::Tensor&, const std::optional<at::Tensor>&) {
+                                                                     const at::Tensor&, const std::optional<at::Tensor>&,
+                                                                     int64_t out_mode) {
   const int64_t C = x.size(-1), M = x.numel() / std::max<int64_t>(C, 1);
-  return {at::empty_like(x), at::empty({M, 2 * C}, x.options().dtype(at::kBFloat16)), at::empty({M, C / 64, 2}, x.options())};
+  return {out_mode == 1 ? at::empty_like(x)
+                        : out_mode == 2 ? at::empty({M, C}, x.options().dtype(at::kBFloat16)) : at::empty({0}, x.options()),
+          at::empty({M, 2 * C}, x.options().dtype(at::kBFloat16)), at::empty({M, C / 64, 2}, x.options())};
 }
 
 // ------------------------------------------------------------------ CPU impls (torch.fft)
@@ -1243,7 +1270,7 @@ TORCH_LIBRARY(amd_dft, m) {
   m.def("c2r_ln_add(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
         "Tensor? pre=None) -> Tensor");
   m.def("c2r_ln_add_split(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
-        "Tensor? pre=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor? pre=None, int out_mode=1) -> (Tensor, Tensor, Tensor)");
   m.def("c2r_ln_add_part(Tensor X, int dim, int n, float scale, Tensor x, Tensor stats, Tensor gamma, Tensor beta, "
         "Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("Rfft(Tensor x, int normalized=0, int onesided=1, int signal_ndim=1) -> Tensor");

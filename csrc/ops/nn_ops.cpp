@@ -501,6 +501,88 @@ std::tuple<at::Tensor, at::Tensor> linear3_stats_cuda(const at::Tensor& xs_, con
   return {y, part};
 }
 
+// fc2 of the fp32 block with the residual stream carried as c2r_ln_add_split's split pairs (no fp32 copy of it):
+// residual = m + (hi + lo), rpairs [M, 2N] bf16 k32-interleaved pairs of x - m, rstats [M, 2] with m = rstats[:, 0]
+// (the block's LN1 statistics, which centred those pairs).  2^-18 of |x - m| off the fp32 residual.
+// rlo2 (optional): the split's third term bf16(x - m - (hi + lo)) [M, N] (c2r_ln_add_split out_mode 2): the
+// residual then matches the fp32 stream to ~2^-27 of |x - m| (fp32 rounding: 2^-24 of |x|)
+at::Tensor pairs_residual_cpu(const at::Tensor& rpairs, const at::Tensor& rstats, int64_t N,
+                              const c10::optional<at::Tensor>& rlo2) {
+  at::Tensor pr = rpairs.to(at::kFloat).reshape({-1, N / 32, 2, 32});
+  at::Tensor z = (pr.select(2, 0) + pr.select(2, 1)).reshape({-1, N});
+  if (rlo2.has_value() && rlo2->defined()) z = z + rlo2->to(at::kFloat).reshape({-1, N});
+  return z + rstats.to(at::kFloat).reshape({-1, 2}).select(1, 0).unsqueeze(1);
+}
+
+void check_pairs_residual(const at::Tensor& rpairs, const at::Tensor& rstats, int64_t M, int64_t N) {
+  TORCH_CHECK(rpairs.scalar_type() == at::kBFloat16 && rpairs.numel() == M * 2 * N,
+              "amd_dft.linear3_stats_pr: rpairs must be [M, 2N] bf16 split pairs");
+  TORCH_CHECK(rstats.numel() == M * 2, "amd_dft.linear3_stats_pr: rstats must be [M, 2] (shift, rstd)");
+  TORCH_CHECK(N % 32 == 0, "amd_dft.linear3_stats_pr: N must be a multiple of 32");
+}
+
+std::tuple<at::Tensor, at::Tensor> linear3_stats_pr_cpu(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor& rpairs,
+                                                        const at::Tensor& rstats, const c10::optional<at::Tensor>& pre,
+                                                        const c10::optional<at::Tensor>& rlo2) {
+  const int64_t N = ws.size(0), M = xs.numel() / std::max<int64_t>(xs.size(-1), 1);
+  check_pairs_residual(rpairs, rstats, M, N);
+  return linear3_stats_cpu(xs, ws, pairs_residual_cpu(rpairs, rstats, N, rlo2), pre);
+}
+
+std::tuple<at::Tensor, at::Tensor> linear3_stats_pr_cuda(const at::Tensor& xs_, const at::Tensor& ws_, const at::Tensor& rpairs_,
+                                                         const at::Tensor& rstats_, const c10::optional<at::Tensor>& pre_,
+                                                         const c10::optional<at::Tensor>& rlo2_) {
+  const c10::DeviceGuard guard(xs_.device());
+  check_split_linear(xs_, ws_, c10::nullopt, "linear3_stats_pr");
+  TORCH_CHECK(xs_.size(-1) == ws_.size(1), "amd_dft.linear3_stats_pr: xs [..., 2K], ws [N, 2K]");
+  const int64_t K = ws_.size(1) / 2, N = ws_.size(0), M = xs_.numel() / std::max<int64_t>(2 * K, 1);
+  TORCH_CHECK(gemm_supported(M, N, K), "amd_dft.linear3_stats_pr: the bf16x3 GEMM needs N % 64 == 0 and K % 64 == 0");
+  check_pairs_residual(rpairs_, rstats_, M, N);
+  at::Tensor xs = xs_.contiguous(), ws = ws_.contiguous(), rp = rpairs_.contiguous(), rs = rstats_.to(at::kFloat).contiguous();
+  at::Tensor pre;
+  if (pre_.has_value() && pre_->defined()) {
+    pre = pre_->to(at::kFloat).contiguous();
+    TORCH_CHECK(pre.numel() == N, "amd_dft.linear3_stats_pr: pre must have N entries");
+  } else {
+    pre = at::zeros({N}, xs.options().dtype(at::kFloat));
+  }
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = N;
+  at::Tensor y = at::empty(os, xs.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({M, N / 64, 2}, xs.options().dtype(at::kFloat));
+  GemmLaunch p;
+  p.x = reinterpret_cast<const uint16_t*>(xs.data_ptr());
+  p.w = reinterpret_cast<const uint16_t*>(ws.data_ptr());
+  at::Tensor rl;
+  if (rlo2_.has_value() && rlo2_->defined()) {
+    TORCH_CHECK(rlo2_->scalar_type() == at::kBFloat16 && rlo2_->numel() == M * N,
+                "amd_dft.linear3_stats_pr: rlo2 must be [M, N] bf16");
+    rl = rlo2_->contiguous();
+  }
+  p.residual = rp.data_ptr();
+  p.res_mean = rs.data_ptr<float>();
+  p.res_lo2 = rl.defined() ? reinterpret_cast<const uint16_t*>(rl.data_ptr()) : nullptr;
+  p.y = y.data_ptr();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.split = 1;
+  p.out = 1;
+  p.stats_part = part.data_ptr<float>();
+  p.stats_pre = pre.data_ptr<float>();
+  if (M > 0) launch_gemm(p, c10::hip::getCurrentHIPStream(xs.device().index()).stream());
+  return {y, part};
+}
+
+std::tuple<at::Tensor, at::Tensor> linear3_stats_pr_meta(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor&,
+                                                         const at::Tensor&, const c10::optional<at::Tensor>&,
+                                                         const c10::optional<at::Tensor>&) {
+  std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
+  os.back() = ws.size(0);
+  const int64_t M = xs.numel() / std::max<int64_t>(xs.size(-1), 1);
+  return {at::empty(os, xs.options().dtype(at::kFloat)), at::empty({M, ws.size(0) / 64, 2}, xs.options().dtype(at::kFloat))};
+}
+
 std::tuple<at::Tensor, at::Tensor> linear3_stats_meta(const at::Tensor& xs, const at::Tensor& ws, const at::Tensor&,
                                                       const c10::optional<at::Tensor>&) {
   std::vector<int64_t> os(xs.sizes().begin(), xs.sizes().end());
@@ -777,6 +859,8 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("split_bf16(Tensor x, bool rows=True) -> Tensor");
   m.def("linear3(Tensor xs, Tensor ws, Tensor? bias=None, int act=0, Tensor? residual=None, bool split_out=False) -> Tensor");
   m.def("linear3_stats(Tensor xs, Tensor ws, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
+  m.def("linear3_stats_pr(Tensor xs, Tensor ws, Tensor rpairs, Tensor rstats, Tensor? pre=None, Tensor? rlo2=None) -> "
+        "(Tensor, Tensor)");
   m.def("linear_stats(Tensor x, Tensor w, Tensor residual, Tensor? pre=None) -> (Tensor, Tensor)");
   m.def("linear3_ln(Tensor xs, Tensor ws, Tensor c1, Tensor? bias, Tensor stats, int act=0) -> Tensor");
   m.def("patch_linear3(Tensor xs, Tensor ws, Tensor? bias=None, Tensor? pos=None, int p=8) -> Tensor");
@@ -792,6 +876,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cuda));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cuda));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cuda));
+  m.impl("linear3_stats_pr", AMD_DFT_TRACED("amd_dft::linear3_stats_pr", amd_dft::linear3_stats_pr_cuda));
   m.impl("linear_stats", AMD_DFT_TRACED("amd_dft::linear_stats", amd_dft::linear_stats_cuda));
   m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cuda));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cuda));
@@ -807,6 +892,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("split_bf16", AMD_DFT_TRACED("amd_dft::split_bf16", amd_dft::split_bf16_cpu));
   m.impl("linear3", AMD_DFT_TRACED("amd_dft::linear3", amd_dft::linear3_cpu));
   m.impl("linear3_stats", AMD_DFT_TRACED("amd_dft::linear3_stats", amd_dft::linear3_stats_cpu));
+  m.impl("linear3_stats_pr", AMD_DFT_TRACED("amd_dft::linear3_stats_pr", amd_dft::linear3_stats_pr_cpu));
   m.impl("linear_stats", AMD_DFT_TRACED("amd_dft::linear_stats", amd_dft::linear_stats_cpu));
   m.impl("linear3_ln", AMD_DFT_TRACED("amd_dft::linear3_ln", amd_dft::linear3_ln_cpu));
   m.impl("patch_linear3", AMD_DFT_TRACED("amd_dft::patch_linear3", amd_dft::patch_linear3_cpu));
@@ -822,6 +908,7 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("split_bf16", &amd_dft::split_bf16_meta);
   m.impl("linear3", &amd_dft::linear3_meta);
   m.impl("linear3_stats", &amd_dft::linear3_stats_meta);
+  m.impl("linear3_stats_pr", &amd_dft::linear3_stats_pr_meta);
   m.impl("linear_stats", &amd_dft::linear_stats_meta);
   m.impl("linear3_ln", &amd_dft::linear3_ln_meta);
   m.impl("patch_linear3", &amd_dft::patch_linear3_meta);

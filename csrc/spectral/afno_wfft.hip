@@ -84,6 +84,7 @@ struct WArgs {
   void* out;             // R2C: [O, KM, C, 2]; C2R: [O, 180, C]
   uint16_t* pairs;       // C2R, SPLIT: [O * 180, 2C] bf16 split pairs of out - mean(x) (stats .x)
   float* part;           // C2R, SPLIT / PART: [O * 180, C / 64, 2] (mean, M2) of out per 64-channel slab
+  uint16_t* lo2;         // C2R, SPLIT, optional: [O * 180, C] bf16(out - mean(x) - (hi + lo))
   int C, nslab;
   float scale;
 };
@@ -459,7 +460,9 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
       y[2 * p] = u[k2].re[p] * sc + xp[2 * p] + h[2 * p];
       y[2 * p + 1] = -u[k2].im[p] * sc + xp[2 * p + 1] + h[2 * p + 1];
     }
-    stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
+    // SPLIT with out == nullptr: only the split pairs (the residual then travels as them, see
+    // linear3_stats_pr) -- the fp32 store is the largest of this kernel's three output streams
+    if (!SPLIT || a.out != nullptr) stx4<F32>(ob, lo + kA * k2 * C, y[0], y[1], y[2], y[3]);
     if constexpr (PART) {
       // the stored bf16 values (8 B) over this lane's own residual slot of the LDS image, which no other
       // thread reads: no barrier between the FFT and the epilogue (one before the sweep below)
@@ -481,6 +484,13 @@ __global__ void __launch_bounds__(kThreads, SPLIT ? AFNO_C2R_SPLIT_OCC : 3) afno
       uint16_t* pr = pbase + (n * (2 * C) + (c0 >> 5) * 64 + (c0 & 31));  // k32-interleaved [hi(32) | lo(32)]
       *reinterpret_cast<uint2*>(pr) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(pr + 32) = make_uint2(l01, l23);
+      if (a.lo2 != nullptr) {  // wave-uniform: the split's third term, 16 lanes x 8 B = a 128-byte row piece
+        const auto up = [](uint32_t w, bool hi) { return __uint_as_float(hi ? (w & 0xffff0000u) : (w << 16)); };
+        const float r0 = z0 - (up(h01, false) + up(l01, false)), r1 = z1 - (up(h01, true) + up(l01, true));
+        const float r2 = z2 - (up(h23, false) + up(l23, false)), r3 = z3 - (up(h23, true) + up(l23, true));
+        *reinterpret_cast<uint2*>(a.lo2 + static_cast<int64_t>(o) * kL * C + n * C + c0) =
+            make_uint2(bfpack(r0, r1), bfpack(r2, r3));
+      }
       *reinterpret_cast<float4*>(lds + n * kPitch + kPPL * g) = make_float4(y[0], y[1], y[2], y[3]);
     }
     // one output position at a time: interleaving the positions' epilogues (the scheduler's
@@ -555,6 +565,7 @@ WArgs make_args(const AfnoWLaunch& p) {
   a.out = p.out;
   a.pairs = p.pairs;
   a.part = p.part;
+  a.lo2 = p.lo2;
   a.C = p.C;
   a.nslab = p.C / kSlab;
   a.scale = p.scale;

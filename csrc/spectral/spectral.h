@@ -83,6 +83,9 @@ struct AfnoWLaunch {
   // next GEMM's operand) and its per-64-channel LayerNorm partials [O*L, C/64] (mean, M2)
   uint16_t* pairs = nullptr;
   float* part = nullptr;
+  // C2R SPLIT, optional: [O*L, C] bf16 third term of the split, bf16(out - m - (hi + lo)): with the pairs it
+  // carries out to ~2^-27 of |out - m| (below fp32 rounding), so the fp32 copy (out) can be skipped
+  uint16_t* lo2 = nullptr;
 };
 bool afno_w_supported(int L, int C, int KM);
 void launch_afno_w_r2c_ln(const AfnoWLaunch& p, void* stream);

@@ -342,6 +342,15 @@ def _ln_folded_fc3(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
                          build)
 
 
+# How the fp32 FourCastNet block hands the post-filter residual stream x1 to fc2 (profiles/f32_pair_residual_r5.txt):
+#   "fp32"  (default) the C2R epilogue's fp32 copy of x1;
+#   "pairs" the split pairs fc1 already reads + the per-token LN1 mean (the C2R skips its fp32 write; x1 to
+#           2^-18 of |x1 - mean|: full-depth rel-L2 1.0e-5 instead of 6.4e-6), +0.3..0.8 % samples/s;
+#   "lo2"   the pairs + a bf16 third term (x1 to ~2^-27 of |x1 - mean|, below fp32 rounding): precision kept,
+#           but fc2's wider residual epilogue costs more than the C2R saves (-0.7..-1.2 %).
+F32_RESIDUAL = "fp32"
+
+
 def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None,
                          split_out: bool = False):
     """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
@@ -378,7 +387,13 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     stats = ops.ln_stats_merge(part, n1.eps) if part is not None else ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    x1, x1s, part2 = ops.c2r_ln_add_split(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+    # F32_RESIDUAL: fc2 takes the residual as x1's split pairs (+ the per-token shift, + the third term), so the
+    # C2R epilogue skips x1's fp32 copy -- the largest of its output streams
+    mode = F32_RESIDUAL if (not split_out and C <= 64 * 64) else "fp32"
+    if mode not in ("fp32", "pairs", "lo2"):
+        raise ValueError(f"F32_RESIDUAL must be 'fp32', 'pairs' or 'lo2', got {mode!r}")
+    x1, x1s, part2 = ops.c2r_ln_add_split(yw, 2, W, scale, xs, stats, g1, be1, pre32,
+                                          {"fp32": 1, "pairs": 0, "lo2": 2}[mode])
     # x1s holds x1 - mean(x) per token (centred split): st2's mean is shifted to match.
     # ln_stats_merge takes <= 64 chunks of 64 channels
     if C <= 64 * 64:
@@ -395,7 +410,10 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
         x1 = ops.linear3(hid, w2s, None, 0, x1.reshape(-1, C), False).reshape(B, H, W, C)
         return x1, m.fc2.bias
     b2 = _f32(m, "fc2_b", m.fc2.bias)
-    x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
+    if mode != "fp32":
+        x1n, part_next = ops.linear3_stats_pr(hid, w2s, x1s, stats.reshape(-1, 2), b2, x1 if mode == "lo2" else None)
+    else:
+        x1n, part_next = ops.linear3_stats(hid, w2s, x1.reshape(-1, C), b2)
     return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
 
 

@@ -86,6 +86,58 @@ def test_linear3_stats_cpu_semantics():
     assert yo.shape == (5, 768) and po.shape == (5, 12, 2)
 
 
+def _pairs_and_shift(r, seed=0):
+    """A residual as the fp32 block's C2R epilogue hands it to fc2: split pairs of r - m plus the shift m."""
+    g = torch.Generator().manual_seed(seed)
+    m = torch.randn(r.shape[0], generator=g) * 2
+    st = torch.stack([m, torch.rand(r.shape[0], generator=g) + 0.5], 1)
+    return ops.split_bf16(r - m[:, None], True), st
+
+
+def test_linear3_stats_pr_cpu_semantics():
+    """fc2 with the residual given as split pairs of r - m plus the per-token shift m: the same as
+    linear3_stats with the residual m + unsplit(pairs) (2^-18 of |r - m| from r itself)."""
+    torch.manual_seed(4)
+    x, w, r, pre = torch.randn(37, 128), torch.randn(256, 128) * 0.1, torch.randn(37, 256) + 3, torch.randn(256)
+    rp, st = _pairs_and_shift(r)
+    xs, ws = ops.split_bf16(x, True), ops.split_bf16(w, True)
+    y, part = ops.linear3_stats_pr(xs, ws, rp, st, pre)
+    y0, part0 = ops.linear3_stats(xs, ws, unsplit_bf16(rp) + st[:, :1], pre)
+    assert torch.equal(y, y0) and torch.equal(part, part0)
+    assert rel_l2(y, F.linear(x, w) + r) < 3e-5
+    yo, po = ops.linear3_stats_pr(torch.empty(5, 6144, device="meta", dtype=torch.bfloat16),
+                                  torch.empty(768, 6144, device="meta", dtype=torch.bfloat16),
+                                  torch.empty(5, 1536, device="meta", dtype=torch.bfloat16), torch.empty(5, 2, device="meta"))
+    assert yo.shape == (5, 768) and po.shape == (5, 12, 2)
+    # + the third split term: the residual to ~2^-27 of |r - m|
+    lo2 = ((r - st[:, :1]) - unsplit_bf16(rp)).bfloat16()
+    y3, _ = ops.linear3_stats_pr(xs, ws, rp, st, pre, lo2)
+    y4, _ = ops.linear3_stats(xs, ws, r, pre)
+    assert rel_l2(y3, y4) < 1e-7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(777, 768, 3072), (300, 256, 64)])
+def test_linear3_stats_pr_gpu(device, M, N, K):
+    """The bf16x3 fc2 GEMM reading its residual as split pairs + shift (RES 2 epilogue) against the same
+    GEMM with that residual materialised in fp32; the partials against an fp64 reference."""
+    torch.manual_seed(M + K)
+    x, w, r = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(M, N) * 3 + 1
+    pre = torch.randn(N) * 0.5
+    rp, st = _pairs_and_shift(r, M)
+    xs, ws = ops.split_bf16(x.to(device), True), ops.split_bf16(w.to(device), True)
+    y, part = ops.linear3_stats_pr(xs, ws, rp.to(device), st.to(device), pre.to(device))
+    y0, _ = ops.linear3_stats(xs, ws, (unsplit_bf16(rp) + st[:, :1]).to(device), pre.to(device))
+    assert rel_l2(y.cpu(), y0.cpu()) < 1e-7
+    lo2 = ((r - st[:, :1]) - unsplit_bf16(rp)).bfloat16()
+    y3, part3 = ops.linear3_stats_pr(xs, ws, rp.to(device), st.to(device), pre.to(device), lo2.to(device))
+    y4, _ = ops.linear3_stats(xs, ws, r.to(device), pre.to(device))
+    assert rel_l2(y3.cpu(), y4.cpu()) < 1e-7
+    assert rel_l2(y.cpu(), F.linear(x, w) + r) < 2e-5
+    ref = _ln_stats_ref(y.cpu(), pre)
+    assert torch.allclose(ops.ln_stats_merge(part, 1e-6).cpu(), ref, rtol=2e-5, atol=2e-6)
+
+
 def _ln_fold_operands(w, b, g, be):
     """(split(W * gamma), c1 from the split pairs, c2 = W beta + b): what _ln_folded_fc3 builds."""
     ws = ops.split_bf16((w.double() * g.double()[None, :]).float(), True)
@@ -278,6 +330,17 @@ def test_c2r_ln_add_split_gpu(device, with_pre):
     sref[:, 0] -= st[:, 0]
     sts = ops.ln_stats_merge(part, 1e-6, d(st)).cpu()
     assert torch.allclose(sts, sref, rtol=2e-5, atol=2e-6), (sts - sref).abs().max()
+    # out_mode 0 / 2 (the residual travels as the pairs [+ the third split term]): no fp32 output, the same
+    # pairs and partials; pairs + lo2 + mean give the fp32 output back to ~2^-27 of |y - mean|
+    for mode in (0, 2):
+        y2, pairs2, part2 = ops.c2r_ln_add_split(d(X), 2, W, 1.0 / math.sqrt(H * W), d(x), d(st), d(g), d(be), d(pre), mode)
+        assert torch.equal(pairs2, pairs) and torch.equal(part2, part)
+        if mode == 0:
+            assert y2.numel() == 0
+        else:
+            z = (y.reshape(-1, C) - d(st)[:, :1]).cpu()
+            back = (unsplit_bf16(pairs.cpu()) + y2.cpu().float())
+            assert (back - z).abs().max() <= 2 ** -26 * z.abs().max(), (back - z).abs().max()
 
 
 @pytest.mark.gpu
@@ -462,7 +525,8 @@ def test_fp32_block_gate_checks_real_mlp_width():
     assert not S._mlp_gemm_ok(Mlp(256, 600), split=False)
 
 
-def test_fused_fp32_block_composition_and_export_cpu(monkeypatch):
+@pytest.mark.parametrize("residual", ["fp32", "pairs", "lo2"])
+def test_fused_fp32_block_composition_and_export_cpu(monkeypatch, residual):
     """The fp32 fused block (c2r_ln_add_split -> ln_stats_merge -> linear3_ln -> linear3_stats) forced onto
     the CPU op implementations: equals the torch model, and exports / re-imports through ONNX (the
     three-output c2r_ln_add_split node included) -- the engine bench.py times is built this way on the GPU."""
@@ -485,12 +549,16 @@ def test_fused_fp32_block_composition_and_export_cpu(monkeypatch):
 
     monkeypatch.setattr(S, "afno_block_fused_f32", spy)
     monkeypatch.setattr(S, "_ln_fused_ok", lambda blk, t: t.dtype == torch.float32)
+    monkeypatch.setattr(S, "F32_RESIDUAL", residual)
     with torch.no_grad():
         out = m.set_backend("amd")(x)
     assert len(calls) == cfg.depth
     assert rel_l2(out, ref) < 1e-5
     data = ex.export(m, x)
     ops_in_graph = {n.op_type for n in P.load_model(data).graph.node if n.domain == "com.amd.dft"}
-    assert {"c2r_ln_add_split", "linear3_ln", "ln_stats_merge", "linear3_stats"} <= ops_in_graph
+    # "pairs" / "lo2": blocks before the last carry the residual into fc2 as c2r_ln_add_split's pairs
+    # (linear3_stats_pr); "fp32": as the C2R epilogue's fp32 copy (linear3_stats)
+    fc2 = "linear3_stats" if residual == "fp32" else "linear3_stats_pr"
+    assert {"c2r_ln_add_split", "linear3_ln", "ln_stats_merge", fc2} <= ops_in_graph
     (y,) = OnnxGraph(data, device="cpu").run(x)
     assert rel_l2(y, ref) < 1e-5
