@@ -638,7 +638,11 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
           // staged (OUT 0 / 1: 4 VGPRs per pass), half of them with bias / LN vectors live, 4 ahead
           // for OUT 2 (8 fp32 per pass: the whole half would hold 128 VGPRs beside the accumulators)
           // -- each of those spilled when the whole half was prefetched
-          constexpr int PD = RES == 3 ? 2 : (OUT == 2 || PERSIST) ? 4 : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
+          // RES 2 / 3 (5 / 7 VGPRs per pass): 4 / 2 passes ahead in the persistent form, 8 / 2 otherwise (deeper spilled)
+          constexpr int PD = RES == 3 ? 2
+                             : (OUT == 2 || PERSIST) ? 4
+                             : RES == 2 ? NIT / 2
+                                        : (BIAS || LN ? NIT / 2 : NIT);  // bias / c1 vectors hold 64 more VGPRs
           auto load_rr = [&](int it) {  // OUT 1: 4 fp32 features per lane; OUT 0: 8 bf16; OUT 2: 8 fp32
             int rt = min(tbase + it * RPI + rsub, M - 1);
             if constexpr (MODE == 1) {

@@ -345,9 +345,9 @@ def _ln_folded_fc3(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
 # How the fp32 FourCastNet block hands the post-filter residual stream x1 to fc2 (profiles/f32_pair_residual_r5.txt):
 #   "fp32"  (default) the C2R epilogue's fp32 copy of x1;
 #   "pairs" the split pairs fc1 already reads + the per-token LN1 mean (the C2R skips its fp32 write; x1 to
-#           2^-18 of |x1 - mean|: full-depth rel-L2 1.0e-5 instead of 6.4e-6), +0.3..0.8 % samples/s;
+#           2^-18 of |x1 - mean|: full-depth rel-L2 1.0e-5 instead of 6.4e-6), +0.5..1.0 % samples/s;
 #   "lo2"   the pairs + a bf16 third term (x1 to ~2^-27 of |x1 - mean|, below fp32 rounding): precision kept,
-#           but fc2's wider residual epilogue costs more than the C2R saves (-0.7..-1.2 %).
+#           but fc2's wider residual epilogue costs more than the C2R saves (-0.3..-0.9 %).
 F32_RESIDUAL = "fp32"
 
 
