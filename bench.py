@@ -7,6 +7,14 @@ Metric/config from BASELINE.json: "rfft2 720x1440 us + FourCastNet-FNO samples/s
 MI355X"; FourCastNet AFNO (720x1440, patch 8, embed 768, depth 12, 8 AFNO blocks), batch 32
 per GPU (weak scaling), synthetic inputs, random-init weights.
 
+Headline engine = the reference's workflow (/root/reference/README.md:57-75,
+/root/reference/tests/test_dft.py:73-115): the FourCastNet model written with the ONNX-contrib
+``OnnxRfft2`` / ``OnnxIrfft2`` Functions and stock ops, exported to ONNX (com.microsoft Rfft / Irfft
++ Einsum / LayerNorm / MatMul ...), built into an engine whose build-time graph optimizer maps the
+stock patterns onto the hand kernels (every rewrite verified on the device), serialized,
+deserialized, and replayed as one hipGraph per step.  The library-native export (com.amd.dft
+nodes) is timed as the extra key ``native_export_samples_per_s``.
+
 Headline precision = fp32, the reference's only precision (its plugins accept kFLOAT only,
 /root/reference/src/dft_plugins/dft_plugins.cpp:101-102): fp32 activations / residual stream /
 spectra / FFTs; GEMMs as 3-product bf16 splits with fp32 accumulation (bf16x3: ~5e-6 relative
@@ -212,13 +220,25 @@ class _EngineFn:
         return self.eng.graph.run(x)[0]
 
 
-def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None):
-    """Model -> (default) ONNX export with its com.amd.dft nodes -> serialized engine bytes ->
+def check_optimizer_report(opt: dict, depth: int) -> None:
+    """The contrib engine must have every FourCastNet block on the fused kernels: one ``afno_block``
+    rewrite per block and no rejected rewrite (a rejection keeps stock nodes = a slower engine that
+    would still run)."""
+    ap = opt.get("applied", {})
+    if ap.get("afno_block") != depth or opt.get("rejected"):
+        raise SystemExit(f"contrib engine not fully optimized: applied {ap}, rejected {opt.get('rejected')}")
+
+
+def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None, export="contrib"):
+    """Model -> ONNX export -> engine build (graph optimizer) -> serialized engine bytes ->
     deserialized engine -> hipGraph-captured DP runner: the timed step is the engine a user
     would load with ``dftexec --loadEngine`` (reference: export -> build -> serialize ->
-    deserialize -> execute_v2, /root/reference/tests/test_dft.py:89-115)."""
+    deserialize -> execute_v2, /root/reference/tests/test_dft.py:89-115).
+    ``export="contrib"``: the reference's way of writing the model (ONNX-contrib Rfft/Irfft + stock
+    ops); ``"amd"``: the library-native export (com.amd.dft nodes)."""
     torch.manual_seed(seed)  # the same weights on every rank (data parallel = one model)
-    model = AFNONet(cfg, backend="amd").to(dev).to(dtype).eval()
+    backend = export if dev.type == "cuda" else "amd"  # CPU (harness tests): the model itself
+    model = AFNONet(cfg, backend=backend).to(dev).to(dtype).eval()
     torch.manual_seed(seed + 1 + input_seed)  # each rank's own batch
     x = torch.randn(B, cfg.in_chans, *cfg.img_size, device=dev).to(dtype)
     info = {"engine": False}
@@ -227,11 +247,23 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None):
         from tensorrt_dft_plugins_amd.engine import Engine
 
         t0 = time.perf_counter()
-        blob = Engine.build(model, (x,), device=dev, use_graph=False).serialize()
+        built = Engine.build(model, (x,), device=dev, use_graph=False)
+        opt = built.header.extra.get("optimizer", {})
+        if export == "contrib":
+            log(f"{dtype}: contrib graph optimizer: {opt.get('nodes_before')} -> {opt.get('nodes_after')} nodes, "
+                f"rewrites {opt.get('applied')}, rejected {opt.get('rejected')} ({opt.get('seconds')} s)")
+            check_optimizer_report(opt, cfg.depth)
+        blob = built.serialize()
+        del built, model
+        torch.cuda.empty_cache()
         eng = Engine.deserialize(blob, device=dev, use_graph=False)
         fn = _EngineFn(eng)
-        info = {"engine": True, "engine_bytes": len(blob), "engine_build_load_s": round(time.perf_counter() - t0, 1)}
-        log(f"{dtype}: engine exported, serialized ({len(blob) / 1e6:.0f} MB) and deserialized in "
+        info = {"engine": True, "engine_bytes": len(blob), "engine_build_load_s": round(time.perf_counter() - t0, 1),
+                "export": export}
+        if export == "contrib":
+            info["optimizer"] = {"nodes_before": opt.get("nodes_before"), "nodes_after": opt.get("nodes_after"),
+                                 "applied": opt.get("applied"), "rejected": len(opt.get("rejected") or [])}
+        log(f"{dtype}: {export} engine exported, serialized ({len(blob) / 1e6:.0f} MB) and deserialized in "
             f"{info['engine_build_load_s']}s")
     t0 = time.perf_counter()
     runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph,
@@ -251,11 +283,17 @@ def multi_gpu_diagnostics(runner, steps: int, world: int, dev, cuda: bool) -> di
     if ranks != world:
         raise SystemExit(f"collective spans {ranks} ranks, WORLD_SIZE is {world}")
     busy = runner.comm_busy_ms()
+    # the last timed step's gathered buffer against every rank's local output (exact checksums)
+    ver = runner.verify_gather()
+    if ver["gather_verified"] is False:
+        raise SystemExit(f"gathered output does not match the ranks' local outputs: {ver}")
     g_only = runner.gather_only_ms(5)
     vals = torch.tensor([busy / steps if busy is not None else -1.0, g_only if g_only is not None else -1.0],
                         dtype=torch.float64, device=dev if cuda else "cpu")
     dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-    out = {"collective_ranks": ranks}
+    out = {"collective_ranks": ranks, "gather_verified": ver["gather_verified"]}
+    if runner.gather_fallback:
+        out["gather_fallback"] = runner.gather_fallback
     if vals[0] >= 0:
         out["comm_busy_ms_per_step"] = round(float(vals[0]), 3)
     if vals[1] >= 0:
@@ -312,6 +350,10 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-engine", dest="engine", action="store_false",
                     help="capture the nn.Module directly instead of the serialized engine")
+    ap.add_argument("--export", choices=["contrib", "amd"], default="contrib",
+                    help="headline engine: the stock ONNX-contrib export (reference workflow) or the native one")
+    ap.add_argument("--native-steps", type=int, default=10,
+                    help="timed steps of the native-export fp32 engine extra (0: skip)")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--gather", choices=["rccl", "ipc"], default=os.environ.get("MI_DFT_GATHER", "rccl"),
                     help="output all-gather: RCCL ring collective or direct IPC pushes over xGMI")
@@ -331,8 +373,6 @@ def main(argv=None) -> int:
         torch.cuda.set_device(dev)
     lib_note = _ensure_library(rank, world, cuda)
     tdp.load_plugins()
-    gemm_table = None  # (hipBLASLt solution tables were a round-1 comparator, removed round 5)
-    from tensorrt_dft_plugins_amd.ops.spectral import mlp_on_hand_gemm
 
     if a.tiny:
         cfg = AFNOConfig(img_size=(48, 96), in_chans=4, out_chans=4, embed_dim=64, depth=2, num_blocks=4)
@@ -353,10 +393,12 @@ def main(argv=None) -> int:
         extra.update(time_fno_block_us())
         log(f"single-op probes: {extra}")
 
-    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234, rank, gather_dtype=gdt)
-    log(f"world={world} batch/GPU={B} dtype={head_dt}")
+    head_export = a.export if head_dt == torch.float32 else "amd"  # the contrib model is the reference's fp32
+    eng_info, runner = build_runner(cfg, head_dt, B, dev, a, 1234, rank, gather_dtype=gdt, export=head_export)
+    log(f"world={world} batch/GPU={B} dtype={head_dt} engine={eng_info.get('export', 'module')}")
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
+    gather_backend_used = runner.gather_backend
     comm_diag = multi_gpu_diagnostics(runner, a.steps, world, dev, cuda) if world > 1 else {}
     runner.close()
     del runner
@@ -366,13 +408,25 @@ def main(argv=None) -> int:
     samples_per_s = world * B / (elapsed / a.steps)
     tflops = samples_per_s * flops_per_sample(cfg) / 1e12
 
+    if cuda and a.native_steps > 0 and not a.tiny and head_export == "contrib" and a.engine:
+        # the same fp32 model through the library-native export (com.amd.dft nodes)
+        _, r2 = build_runner(cfg, head_dt, B, dev, a, 1234, rank, gather_dtype=gdt, export="amd")
+        e2 = run_steps(r2, a.native_steps, 2, world, dev, cuda)
+        extra["native_export_samples_per_s"] = round(world * B / (e2 / a.native_steps), 3)
+        extra["native_export_ms_per_step"] = round(e2 * 1000.0 / a.native_steps, 3)
+        r2.close()
+        del r2
+        torch.cuda.empty_cache()
     if cuda and a.extra_steps > 0 and not a.tiny:
         other = "bf16" if a.dtype == "fp32" else "fp32"
-        # same weight / input seeds as the headline: only the precision differs
-        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 1234, rank)
+        # same weight / input seeds as the headline: only the precision differs (native export:
+        # the contrib model is written the reference's fp32 way)
+        _, r2 = build_runner(cfg, DTYPES[other], B, dev, a, 1234, rank, export="amd" if other == "bf16" else a.export)
         e2 = run_steps(r2, a.extra_steps, 2, world, dev, cuda)
         extra[f"{other}_samples_per_s"] = round(world * B / (e2 / a.extra_steps), 3)
         extra[f"{other}_ms_per_step"] = round(e2 * 1000.0 / a.extra_steps, 3)
+        if other == "bf16":
+            extra["bf16_gelu"] = cfg.bf16_gelu
         r2.close()
         del r2
 
@@ -406,15 +460,19 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{world}",
                 "per_gpu_batch": B,
                 "hipgraph": not a.no_graph and cuda,
-                "runtime": "serialized engine (ONNX com.amd.dft nodes, save/load, hipGraph replay)"
+                "runtime": ("serialized engine (stock ONNX-contrib export: com.microsoft Rfft/Irfft + standard ops; "
+                            "build-time graph optimizer onto the hand kernels; save/load; hipGraph replay)"
+                            if eng_info.get("export") == "contrib" else
+                            "serialized engine (ONNX com.amd.dft nodes, save/load, hipGraph replay)")
                 if eng_info.get("engine") else "captured nn.Module",
                 "engine_bytes": eng_info.get("engine_bytes"),
+                **({"optimizer": eng_info["optimizer"]} if "optimizer" in eng_info else {}),
                 "output_allgather": gathered,
-                "gather_backend": (a.gather if a.gather == "ipc" else ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()))
+                "gather_backend": (gather_backend_used if gather_backend_used == "ipc" else
+                                   ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()))
                 if world > 1 and gathered else None,
-                "gemm": "hipblaslt" if gemm_table or (cuda and not mlp_on_hand_gemm()) else "hand-mfma",
+                "gemm": "hand-mfma",
                 "gemm_precision": "bf16x3 split, fp32 accumulate" if head_dt == torch.float32 else "bf16, fp32 accumulate",
-                "gemm_table": gemm_table,
                 "gather_dtype": ("bf16" if gdt is not None else ("bf16" if head_dt == torch.bfloat16 else "fp32"))
                 if world > 1 and gathered else None,
                 "comm_env": dict({k: os.environ[k] for k in COMM_ENV if k in os.environ},

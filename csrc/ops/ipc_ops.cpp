@@ -10,6 +10,7 @@
 //   _ipc_event_*    inter-process events (hipEventInterprocess): record on the producer's
 //                   stream, hipStreamWaitEvent on the consumer's
 //   _ipc_write_value / _ipc_wait_value   stream-ordered flag words (hipStreamWrite/WaitValue32)
+//   _ipc_can_access_peer                 hipDeviceCanAccessPeer (checked for every rank pair first)
 //   _ipc_push       one kernel copying a source to N destination pointers concurrently on
 //                   the current stream (peer stores over xGMI, one link per destination)
 // Names start with '_' so they are never exported into ONNX graphs (raw device pointers).
@@ -110,6 +111,15 @@ void ipc_stream_wait(int64_t ev, int64_t device) {
 
 void ipc_event_destroy(int64_t ev) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)); }
 
+// Whether `device` can map and store into `peer`'s memory (the direct mesh's precondition: every
+// push is a peer store over the xGMI link between the two GPUs).
+bool ipc_can_access_peer(int64_t device, int64_t peer) {
+  if (device == peer) return true;
+  int ok = 0;
+  hip_ok(hipDeviceCanAccessPeer(&ok, static_cast<int>(device), static_cast<int>(peer)), "_ipc_can_access_peer");
+  return ok != 0;
+}
+
 // Stream-ordered 32-bit flag write / wait (the counted gather protocol: no host handshake).  The
 // write runs on the command processor after everything enqueued before it on the current stream;
 // the wait blocks the stream (not the host, not a CU) until *ptr >= value.  ptr: a hipMalloc'd
@@ -167,6 +177,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("_ipc_event_record(int ev, int device) -> ()", &amd_dft::ipc_event_record);
   m.def("_ipc_stream_wait(int ev, int device) -> ()", &amd_dft::ipc_stream_wait);
   m.def("_ipc_event_destroy(int ev) -> ()", &amd_dft::ipc_event_destroy);
+  m.def("_ipc_can_access_peer(int device, int peer) -> bool", &amd_dft::ipc_can_access_peer);
   m.def("_ipc_write_value(int ptr, int value, int device) -> ()", &amd_dft::ipc_write_value);
   m.def("_ipc_wait_value(int ptr, int value, int device) -> ()", &amd_dft::ipc_wait_value);
   m.def("_ipc_push(Tensor src, int[] dst_ptrs, int offset) -> ()", &amd_dft::ipc_push);

@@ -4,6 +4,13 @@
 // hipMemcpyAsync per peer on one stream serialises them).  16-byte vector loads and stores,
 // 4 per thread in flight; the source is read once per destination (L2/MALL-resident after the
 // first pass).
+//
+// Visibility: the peer stores go over the fabric into another GPU's memory, and the consumer
+// learns of them from a stream packet (flag write / interprocess event) that the command processor
+// runs after this kernel.  Each workgroup therefore ends with a SYSTEM-scope release once all of
+// its waves' stores have completed: every storing wave waits for its stores (vmcnt(0)), the
+// workgroup synchronises, and one lane issues the release fence, which writes back anything the
+// local L2 still holds for the peer lines before the kernel can be seen as complete.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -23,17 +30,26 @@ __global__ void __launch_bounds__(kThreads) ipc_push_kernel(const uint4* __restr
   uint4* dst = reinterpret_cast<uint4*>(d.ptr[blockIdx.y]) + off16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads * kUnroll;
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kThreads * kUnroll + threadIdx.x; base < n16; base += stride) {
-    uint4 v[kUnroll];
+    if (base + static_cast<int64_t>(kUnroll - 1) * kThreads < n16) {
+      // whole batch in range: kUnroll independent loads in flight, then the stores (no per-element
+      // guard -- with one the compiler parks the array in LDS and waits for every load in turn)
+      uint4 v[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int64_t i = base + static_cast<int64_t>(u) * kThreads;
-      if (i < n16) v[u] = src[i];
-    }
+      for (int u = 0; u < kUnroll; ++u) v[u] = src[base + static_cast<int64_t>(u) * kThreads];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int64_t i = base + static_cast<int64_t>(u) * kThreads;
-      if (i < n16) dst[i] = v[u];
+      for (int u = 0; u < kUnroll; ++u) dst[base + static_cast<int64_t>(u) * kThreads] = v[u];
+    } else {
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t i = base + static_cast<int64_t>(u) * kThreads;
+        if (i < n16) dst[i] = src[i];
+      }
     }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: peers and host
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 

@@ -47,11 +47,11 @@ class AFNOConfig:
     num_blocks: int = 8
     sparsity_threshold: float = 0.01
     hard_thresholding_fraction: float = 1.0
-    # GELU of the bf16 block's fc1 epilogue on the hand GEMM: "tanh" (torch's approximate="tanh":
-    # |difference| < 5e-4 absolute, below half a bf16 ulp for |y| >= 0.25; measured on the fc1 shape:
-    # rel-L2 vs the exact fp32 reference 1.676e-3 against 1.665e-3 for the erf form, at 7-9 % less
-    # fc1 time -- profiles/gelu_tanh_bf16_r5.txt) or "erf".  fp32 models always use the erf form.
-    bf16_gelu: str = "tanh"
+    # GELU of the bf16 block's fc1 epilogue on the hand GEMM: "erf" (default: FourCastNet's nn.GELU)
+    # or "tanh" (torch's approximate="tanh", an explicit opt-in: |difference| < 5e-4 absolute, rel-L2
+    # vs the exact fp32 reference 1.676e-3 against 1.665e-3 for erf on the fc1 shape, at 7-9 % less
+    # fc1 time -- profiles/gelu_tanh_bf16_r5.txt).  fp32 models always use the erf form.
+    bf16_gelu: str = "erf"
 
     @property
     def h(self) -> int:

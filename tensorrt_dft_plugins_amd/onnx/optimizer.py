@@ -83,6 +83,13 @@ class OptimizeReport:
         return sum(1 for a in self.applied if a["pattern"] == kind)
 
 
+def _why(e: BaseException) -> str:
+    """Rejection reason: a RewriteRejected's message, else the unexpected error's type and text
+    (a shape the matcher did not foresee, a missing constant, a kernel's TORCH_CHECK inside the
+    verification): the rewrite is dropped and the original nodes stay, the build continues."""
+    return str(e) if isinstance(e, RewriteRejected) else f"{type(e).__name__}: {e}"
+
+
 class RewriteRejected(Exception):
     pass
 
@@ -569,8 +576,8 @@ def rewrite_layernorm(ctx: Ctx) -> None:
             err = _verify(ctx, old, [n], [x], [out], [y], _precision_tol(dt))
             ctx.replace(old, [n], {out: y})
             ctx.report.applied.append({"pattern": "layer_norm", "at": sq.name, "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "layer_norm", "at": sq.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "layer_norm", "at": sq.name, "why": _why(e)})
 
 
 def _gemm_ok(N: int, K: int, split: bool) -> bool:
@@ -646,8 +653,8 @@ def rewrite_linear(ctx: Ctx) -> None:
             ctx.replace(old, new, {out: y})
             ctx.report.applied.append({"pattern": "linear" + ("_gelu" if act else "") + ("_residual" if residual else ""),
                                        "at": mm.name, "rel_l2": err, "precision": "bf16x3" if split else "bf16"})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "linear", "at": mm.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "linear", "at": mm.name, "why": _why(e)})
 
 
 def fuse_split_chains(ctx: Ctx) -> None:
@@ -708,8 +715,8 @@ def rewrite_pointwise_conv(ctx: Ctx) -> None:
             ctx.replace(old, [n], {out: y})
             ctx.report.applied.append({"pattern": "pointwise_conv" + ("_gelu" if gelu else ""), "at": cv.name,
                                        "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "pointwise_conv", "at": cv.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "pointwise_conv", "at": cv.name, "why": _why(e)})
 
 
 def rewrite_patch_embed(ctx: Ctx) -> None:
@@ -727,10 +734,16 @@ def rewrite_patch_embed(ctx: Ctx) -> None:
             continue
         x = cv.inputs[0]
         try:
+            if cv.attrs.get("group", 1) != 1 or any(d != 1 for d in cv.attrs.get("dilations", [1, 1])):
+                raise RewriteRejected("patch embedding needs group == 1 and unit dilations")
             dt = g.dtype(x)
             if dt not in (torch.float32, torch.bfloat16) or p != 8:
                 raise RewriteRejected("patch embedding needs p == 8 and fp32/bf16")
+            if g.shape(x) is None or len(g.shape(x)) != 4:
+                raise RewriteRejected("patch embedding input shape unknown / not 4-D")
             B, Cin, Hh, Ww = g.shape(x)
+            if W.shape[1] != Cin:
+                raise RewriteRejected("patch embedding weight does not span every input channel")
             N = W.shape[0]
             h, w = Hh // p, Ww // p
             if N % 64:
@@ -768,8 +781,8 @@ def rewrite_patch_embed(ctx: Ctx) -> None:
             err = _verify(ctx, old, new, [x], [out], [y2], _precision_tol(dt))
             ctx.replace(old, new, {out: y2})
             ctx.report.applied.append({"pattern": "patch_embed", "at": cv.name, "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "patch_embed", "at": cv.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "patch_embed", "at": cv.name, "why": _why(e)})
 
 
 def rewrite_unpatch_head(ctx: Ctx) -> None:
@@ -819,8 +832,8 @@ def rewrite_unpatch_head(ctx: Ctx) -> None:
             err = _verify(ctx, old, new, [t], [out], [y], _precision_tol(dt))
             ctx.replace(old, new, {out: y})
             ctx.report.applied.append({"pattern": "unpatch_head", "at": mm.name, "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "unpatch_head", "at": mm.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "unpatch_head", "at": mm.name, "why": _why(e)})
 
 
 # ----------------------------------------------------------------------------------------- spectral regions
@@ -1075,8 +1088,8 @@ def rewrite_afno(ctx: Ctx) -> None:
             ctx.replace(old, new, {out: o})
             ctx.report.applied.append({"pattern": "afno_filter", "at": rf.name, "rel_l2": err, "modes": [r1 - r0, km],
                                        "lambda": lam, "skips": int(add1 is not None) + int(add2 is not None)})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "afno_filter", "at": rf.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "afno_filter", "at": rf.name, "why": _why(e)})
 
 
 def _afno_mlp_ref(X: torch.Tensor, w: List[torch.Tensor], b: List[torch.Tensor], lam: float, nb: int, bs: int):
@@ -1195,8 +1208,8 @@ def rewrite_fno(ctx: Ctx) -> None:
             ctx.replace(old, new, {out: o})
             ctx.report.applied.append({"pattern": "fno_spectral" + ("_pointwise" if conv is not None else "")
                                        + ("_gelu" if gelu else ""), "at": rf.name, "rel_l2": err, "modes": [m1, m2]})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "fno_spectral", "at": rf.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "fno_spectral", "at": rf.name, "why": _why(e)})
 
 
 # ----------------------------------------------------------------------------------------- whole blocks
@@ -1311,8 +1324,8 @@ def fuse_afno_blocks(ctx: Ctx) -> None:
             err = _verify(ctx, old, new, [x], [fc2.outputs[0]], [y], 2e-4, scales=(1.0, 4.0))
             ctx.replace(old, new, {fc2.outputs[0]: y})
             ctx.report.applied.append({"pattern": "afno_block", "at": c2r.name, "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "afno_block", "at": c2r.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "afno_block", "at": c2r.name, "why": _why(e)})
     _chain_afno_blocks(ctx)
 
 
@@ -1373,8 +1386,8 @@ def _chain_afno_blocks(ctx: Ctx) -> None:
                 err = _verify(ctx, old, new, [hid, res], [head.outputs[0]], [hy], 2e-4)
                 ctx.replace(old, new, {head.outputs[0]: hy})
                 ctx.report.applied.append({"pattern": "afno_block_head", "at": fc2.name, "rel_l2": err})
-        except RewriteRejected as e:
-            ctx.report.rejected.append({"pattern": "afno_block_chain", "at": fc2.name, "why": str(e)})
+        except Exception as e:  # noqa: BLE001 -- any failure keeps the original nodes
+            ctx.report.rejected.append({"pattern": "afno_block_chain", "at": fc2.name, "why": _why(e)})
 
 
 # ----------------------------------------------------------------------------------------- driver

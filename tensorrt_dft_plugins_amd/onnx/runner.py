@@ -13,6 +13,7 @@ hipGraph by :mod:`tensorrt_dft_plugins_amd.engine`.
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -74,26 +75,33 @@ def _ints(x) -> List[int]:
     return [int(v) for v in x]
 
 
-_DEV_CONSTS: Dict[tuple, torch.Tensor] = {}
+_DEV_CONSTS: Dict[tuple, torch.Tensor] = {}   # small host values, by value (bounded by the graphs' constants)
+_DEV_LARGE: Dict[tuple, tuple] = {}            # large host tensors, by object identity, dropped with them
 
 
 def _to_dev(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     """Host value -> device.  0-dim host tensors stay on the host (PyTorch treats them as
-    scalars, no copy); small host tensors are memoised by value so the copy happens during
-    warm-up and never inside hipGraph capture."""
-    if t.dim() == 0:
+    scalars, no copy); host tensors are memoised so the copy happens during warm-up and never
+    inside hipGraph capture: small ones by value; a large one (e.g. folded ScatterND indices,
+    held in its graph's constants) by identity, and its device copy is released when the host
+    tensor is -- i.e. with the graph that owns it (a process-global memo of large
+    constants grew without bound over repeated engine builds)."""
+    if t.dim() == 0 or t.device == torch.device(device):
         return t
     if t.numel() <= 4096:
         key = (str(device), t.dtype, tuple(t.shape), tuple(t.reshape(-1).tolist()))
-    else:  # a large host constant (e.g. ScatterND indices): memoised by storage; it lives in the graph
-        key = (str(device), t.dtype, tuple(t.shape), t.data_ptr(), t._version)
-    v = _DEV_CONSTS.get(key)
-    if v is None:
-        # the entry keeps the host tensor alive too, so a storage-keyed entry can never be
-        # matched by another tensor reusing a freed address
-        v = (t.to(device), t)
-        _DEV_CONSTS[key] = v
-    return v[0]
+        v = _DEV_CONSTS.get(key)
+        if v is None:
+            v = _DEV_CONSTS[key] = t.to(device)
+        return v
+    key = (str(device), id(t), t._version)
+    hit = _DEV_LARGE.get(key)
+    if hit is not None and hit[0]() is t:
+        return hit[1]
+    d = t.to(device)
+    _DEV_LARGE[key] = (weakref.ref(t), d)
+    weakref.finalize(t, _DEV_LARGE.pop, key, None)
+    return d
 
 
 def _align(a, b):
@@ -358,10 +366,11 @@ def _slice(attrs, x, starts=None, ends=None, axes=None, steps=None):
     for s, e, a, st in zip(starts, ends, axes, steps):
         n = x.shape[a]
         if st < 0:
-            # ONNX: start clamped to [0, n-1], end to [-1, n-1], walking down (e.g. torch's F.pad
-            # export reverses its pads list this way)
+            # ONNX: negative start / end get n added, then start is clamped to [0, n-1] and end to
+            # [-1, n-1], walking down (end -1 after the addition = past index 0; e.g. torch's F.pad
+            # export reverses its pads list with a very negative end this way)
             s = max(0, min(n - 1, s + n if s < 0 else s))
-            e = max(-1, min(n - 1, e + n if e < -1 else e)) if e >= -n else -1
+            e = max(-1, min(n - 1, e + n if e < 0 else e))
             rev.append((a % x.dim(), list(range(s, e, st))))
             continue
         s = max(0, min(n, s + n if s < 0 else s))

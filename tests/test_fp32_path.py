@@ -545,11 +545,10 @@ def test_fused_fp32_block_composition_and_export_cpu(monkeypatch, residual):
 
     def spy(*a, **k):
         calls.append(1)
-        return orig(*a, **k)
+        return orig(*a, residual_mode=residual, **k)
 
     monkeypatch.setattr(S, "afno_block_fused_f32", spy)
     monkeypatch.setattr(S, "_ln_fused_ok", lambda blk, t: t.dtype == torch.float32)
-    monkeypatch.setattr(S, "F32_RESIDUAL", residual)
     with torch.no_grad():
         out = m.set_backend("amd")(x)
     assert len(calls) == cfg.depth

@@ -230,3 +230,32 @@ def test_constant_subgraphs_folded_at_load():
     assert all(op not in ("Tanh", "Transpose", "Mul") for *_, op in g.nodes)
     (y,) = g.run(x)
     assert torch.allclose(y, ref, atol=1e-6)
+
+
+def test_slice_negative_step_end_minus_one():
+    """ONNX Slice with a negative step: end = -1 means index n - 1 after the n is added,
+    so starts=[-1], ends=[-1], steps=[-1] is empty; a very negative end walks down past index 0."""
+    from tensorrt_dft_plugins_amd.onnx.runner import _slice
+
+    x = torch.arange(6.0)
+    t = lambda v: torch.tensor(v, dtype=torch.int64)  # noqa: E731
+    assert _slice({}, x, t([-1]), t([-1]), t([0]), t([-1])).numel() == 0
+    assert _slice({}, x, t([-1]), t([-(2 ** 63) + 1]), t([0]), t([-1])).tolist() == [5, 4, 3, 2, 1, 0]
+    assert _slice({}, x, t([4]), t([1]), t([0]), t([-2])).tolist() == [4, 2]
+    assert _slice({}, x, t([-2]), t([-5]), t([0]), t([-1])).tolist() == [4, 3, 2]
+
+
+def test_large_host_constant_device_copy_released_with_it():
+    """The device copy of a large host constant lives exactly as long as the host tensor (its
+    graph's constant), not for the process."""
+    import gc
+
+    from tensorrt_dft_plugins_amd.onnx import runner as R
+
+    t = torch.arange(10000)
+    d = R._to_dev(t, torch.device("meta"))  # any other device: a distinct copy object
+    assert d is not t and R._to_dev(t, torch.device("meta")) is d  # memoised while alive
+    n = len(R._DEV_LARGE)
+    del t, d
+    gc.collect()
+    assert len(R._DEV_LARGE) == n - 1

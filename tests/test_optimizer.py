@@ -221,3 +221,58 @@ def test_dftexec_builds_and_loads_contrib_fno(tmp_path):
                        capture_output=True, text=True, env=env, cwd=ROOT, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.load(open(times))["iterations"] == 3
+
+
+def test_optimizer_grouped_patch_conv_keeps_stock_nodes():
+    """A grouped k = stride = 8 convolution is not the patch embedding: the rewrite is rejected with
+    a reason and the build keeps the stock Conv, whose result is unchanged."""
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.pe = nn.Conv2d(4, 64, kernel_size=8, stride=8, groups=2)
+
+        def forward(self, x):
+            return self.pe(x).flatten(2).transpose(1, 2)
+
+    torch.manual_seed(6)
+    m = M().eval()
+    x = torch.randn(1, 4, 16, 32)
+    od, rep = optimize(ex.export(m, x), [list(x.shape)], [x.dtype], device="cpu")
+    assert not any(a["pattern"] == "patch_embed" for a in rep.applied)
+    assert any(r["pattern"] == "patch_embed" and "group" in r["why"] for r in rep.rejected), rep.rejected
+    with torch.no_grad():
+        want = m(x)
+    (y,) = OnnxGraph(od, device="cpu").run(x)
+    assert _rel(y, want) < 1e-6
+
+
+def test_optimizer_unexpected_error_rejects_instead_of_failing(monkeypatch):
+    """Any exception inside a rewrite (not only RewriteRejected) drops that rewrite with its reason
+    and the build goes on with the original nodes (a TypeError / KeyError / TORCH_CHECK
+    used to abort the whole engine build)."""
+    from tensorrt_dft_plugins_amd.onnx import optimizer as O
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = nn.Linear(128, 256)
+
+        def forward(self, x):
+            return torch.nn.functional.gelu(self.fc(x))
+
+    torch.manual_seed(7)
+    m = M().eval()
+    x = torch.randn(4, 128)
+
+    def boom(*a, **k):
+        raise KeyError("simulated missing constant")
+
+    monkeypatch.setattr(O, "_verify", boom)
+    od, rep = optimize(ex.export(m, x), [list(x.shape)], [x.dtype], device="cpu")
+    assert not rep.applied
+    assert any("KeyError" in r["why"] for r in rep.rejected), rep.rejected
+    with torch.no_grad():
+        want = m(x)
+    (y,) = OnnxGraph(od, device="cpu").run(x)
+    assert _rel(y, want) < 1e-6
