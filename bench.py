@@ -220,13 +220,20 @@ class _EngineFn:
         return self.eng.graph.run(x)[0]
 
 
-def check_optimizer_report(opt: dict, depth: int) -> None:
+def check_optimizer_report(opt: dict, depth: int, dev) -> None:
     """The contrib engine must have every FourCastNet block on the fused kernels: one ``afno_block``
     rewrite per block and no rejected rewrite (a rejection keeps stock nodes = a slower engine that
-    would still run)."""
+    would still run).  Collective on multi-rank runs: if any rank's build falls short, every rank
+    exits (no rank left waiting in a collective for one that stopped)."""
     ap = opt.get("applied", {})
-    if ap.get("afno_block") != depth or opt.get("rejected"):
-        raise SystemExit(f"contrib engine not fully optimized: applied {ap}, rejected {opt.get('rejected')}")
+    bad = ap.get("afno_block") != depth or bool(opt.get("rejected"))
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([1.0 if bad else 0.0], device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        bad = bool(t.item() > 0)
+    if bad:
+        raise SystemExit(f"contrib engine not fully optimized on at least one rank: applied {ap}, "
+                         f"rejected {opt.get('rejected')}")
 
 
 def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None, export="contrib"):
@@ -252,7 +259,7 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None, e
         if export == "contrib":
             log(f"{dtype}: contrib graph optimizer: {opt.get('nodes_before')} -> {opt.get('nodes_after')} nodes, "
                 f"rewrites {opt.get('applied')}, rejected {opt.get('rejected')} ({opt.get('seconds')} s)")
-            check_optimizer_report(opt, cfg.depth)
+            check_optimizer_report(opt, cfg.depth, dev)
         blob = built.serialize()
         del built, model
         torch.cuda.empty_cache()

@@ -196,10 +196,27 @@ __device__ __forceinline__ float2 ln_pair(const Ctx& x, int n, float2 v, float2&
   return make_float2((xp.x - s.x) * s.y * x.g.x + x.be.x, (xp.y - s.x) * s.y * x.g.y + x.be.y);
 }
 
+// Column layouts of the 720-point transforms at T = 4 (rfft2 / irfft2 columns, the FNO H transforms):
+// position n of slot t at n*T + t + COL_PW * (n / 8) -- two pad slots per 8 positions instead of one
+// per position.  A bank simulation of the (8, 9, 10) Stockham pattern (pass-0 writes at stride 8
+// positions, passes 1-2 reads of consecutive positions, ds_read/write_b64) gives 1.95 cycles per wave
+// instruction against 3.16 for the T + 1 stride (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS was
+// 3.72 on this kernel).  Every access of both radix orders configured for 720 ((8, 9, 10), (24, 30))
+// stays affine in the unrolled radix index (n / 8 splits into a per-thread part and a constant), so
+// the compiler still folds the offsets into ds_read / ds_write immediates.
+#ifndef AMD_DFT_COL_PW8
+#define AMD_DFT_COL_PW8 1  // 0: the T + 1 stride for these columns too (A/B build)
+#endif
+template <bool COLS, int T, int L>
+constexpr __host__ __device__ int col_pw() {
+  return (AMD_DFT_COL_PW8 && COLS && L == 720 && T == 4) ? 2 : 0;
+}
+
 template <bool COLS, int T, int L>
 __device__ __forceinline__ int lidx(const Ctx& x, int n) {
   constexpr int LP = lds_padl<COLS, L>(L) + 1;
-  if constexpr (COLS && T >= 4) return n * (T + 1) + x.t;  // one pad slot per position: linear in n
+  if constexpr (col_pw<COLS, T, L>() > 0) return n * T + x.t + col_pw<COLS, T, L>() * (n >> 3);
+  else if constexpr (COLS && T >= 4) return n * (T + 1) + x.t;  // one pad slot per position: linear in n
   else if constexpr (COLS) return lds_pad(n * T + x.t);
   else return x.t * LP + lds_padl<COLS, L>(n);
 }
@@ -582,7 +599,8 @@ __device__ __forceinline__ void fixed_tile(const FixedArgs& a, int32_t bid, int 
 // LDS image of one tile (float2 entries) for T signal slots
 template <bool COLS, int T, int L>
 constexpr int tile_lds(int slots = T) {
-  return COLS ? (T >= 4 ? L * (T + 1) + 2 : lds_pad(L * T) + 2) : slots * (lds_padl<COLS, L>(L) + 1);
+  return col_pw<COLS, T, L>() > 0 ? L * T + col_pw<COLS, T, L>() * (L / 8 + 1) + 2
+         : COLS ? (T >= 4 ? L * (T + 1) + 2 : lds_pad(L * T) + 2) : slots * (lds_padl<COLS, L>(L) + 1);
 }
 
 template <Kind K, bool COLS, int TP, int T, class F, bool BFI, bool BFO, bool PR, int NADD, bool PV>

@@ -65,3 +65,34 @@ __device__ __forceinline__ gelu_f2 gelu_tanh2(gelu_f2 x) {
 }
 
 }  // namespace amd_dft
+
+namespace amd_dft {
+
+// erf-GELU for bf16 outputs: x Phi(x) ~= x sigmoid(x q(x^2)), q a quadratic in x^2 (x^2 clamped at 64,
+// where Phi is 1 to fp32 precision) fitted minimax on [-10, 10]:
+//   |error vs the exact erf form| <= 2.6e-5 absolute (fp32 evaluation; the tanh form: 4.7e-4),
+// i.e. 1/40 of half a bf16 ulp at |y| = 0.25 -- FourCastNet's nn.GELU at the resolution of a bf16
+// output, for one packed FMA and two min more than the tanh form (the A&S erf: 11 packed + 4 + the
+// same transcendentals).  Used where the bf16 models' GELU is configured as "erf".
+//   x sigmoid(x q) = x / (1 + 2^(x k(x^2))),  k = -q log2(e)
+constexpr float kGeluFitK0 = -2.3011176586151123f;
+constexpr float kGeluFitK1 = -0.10677912831306458f;
+constexpr float kGeluFitK2 = 0.0010148165747523308f;
+
+__device__ __forceinline__ float gelu_erf_fit(float x) {
+  const float x2 = fminf(x * x, 64.f);
+  const float z = x * fmaf(x2, fmaf(x2, kGeluFitK2, kGeluFitK1), kGeluFitK0);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
+}
+
+__device__ __forceinline__ gelu_f2 gelu_erf_fit2(gelu_f2 x) {
+  const gelu_f2 xx = x * x;
+  const gelu_f2 x2 = {fminf(xx.x, 64.f), fminf(xx.y, 64.f)};
+  const gelu_f2 q = __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, gelu_f2(kGeluFitK2), gelu_f2(kGeluFitK1)),
+                                              gelu_f2(kGeluFitK0));
+  const gelu_f2 z = x * q;
+  const gelu_f2 d = gelu_f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + gelu_f2(1.f);
+  return x * gelu_f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
+}  // namespace amd_dft

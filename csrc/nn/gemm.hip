@@ -265,6 +265,9 @@ __device__ __forceinline__ void epi_act(const f32x4& a4, const float4& bias, con
   } else if constexpr (ACT == 2) {
     v[0] = gelu_tanh2(v[0]);
     v[1] = gelu_tanh2(v[1]);
+  } else if constexpr (ACT == 3) {
+    v[0] = gelu_erf_fit2(v[0]);
+    v[1] = gelu_erf_fit2(v[1]);
   }
 }
 
@@ -1195,7 +1198,8 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
     return;
   }
   if (p.split) {
-    if (p.act == 2) throw std::runtime_error("amd_dft: gemm: the tanh GELU form is a bf16-path option (split GEMMs: act 1)");
+    if (p.act == 2 || p.act == 3)
+      throw std::runtime_error("amd_dft: gemm: the tanh / fitted GELU forms are bf16-path options (split GEMMs: act 1)");
     if (p.act == 1) {
       if (bias) launch_split<1, true>(p, st, grid);
       else launch_split<1, false>(p, st, grid);
@@ -1209,6 +1213,9 @@ void launch_gemm(const GemmLaunch& p_, void* stream) {
   } else if (p.act == 2) {  // tanh-form GELU (the bf16 path's option, see gelu.h)
     if (bias) launch_res<2, true>(p, st, grid);
     else launch_res<2, false>(p, st, grid);
+  } else if (p.act == 3) {  // erf GELU at bf16-output resolution (gelu.h: gelu_erf_fit)
+    if (bias) launch_res<3, true>(p, st, grid);
+    else launch_res<3, false>(p, st, grid);
   } else {
     if (bias) launch_res<0, true>(p, st, grid);
     else launch_res<0, false>(p, st, grid);

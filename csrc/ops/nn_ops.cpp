@@ -79,20 +79,33 @@ at::Tensor unpatchify_meta(const at::Tensor& t, int64_t C, int64_t h, int64_t w,
 // act: 0 none, 1 GELU (erf).  CUDA: the hand-written MFMA GEMM (csrc/nn/gemm.hip) when
 // N % 64 == 0 and K % 64 == 0 (a ragged last 256-feature panel is masked in the kernel), otherwise
 // hipBLASLt through at::linear (counted: fallback_counts / MI_DFT_STRICT).
+// act 3: the bf16 paths' erf GELU, x sigmoid(x q(x^2)) (csrc/nn/gelu.h: gelu_erf_fit), same constants
+at::Tensor gelu_erf_fit_ref(const at::Tensor& y) {
+  const at::Tensor x2 = at::clamp_max(y * y, 64.0);
+  const at::Tensor z = y * (x2 * (x2 * 0.0010148165747523308 + -0.10677912831306458) + -2.3011176586151123);
+  return y / (at::exp2(z) + 1.0);
+}
+
+at::Tensor apply_act_ref(const at::Tensor& y, int64_t act) {
+  if (act == 1) return at::gelu(y);
+  if (act == 2) return at::gelu(y, "tanh");
+  if (act == 3) return gelu_erf_fit_ref(y);
+  return y;
+}
+
 at::Tensor linear_ref(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
                       const c10::optional<at::Tensor>& residual) {
   at::Tensor y = at::linear(x.to(at::kFloat), w.to(at::kFloat),
                             bias.has_value() && bias->defined() ? c10::optional<at::Tensor>(bias->to(at::kFloat))
                                                                 : c10::nullopt);
-  if (act == 1) y = at::gelu(y);
-  if (act == 2) y = at::gelu(y, "tanh");
+  y = apply_act_ref(y, act);
   if (residual.has_value() && residual->defined()) y = y + residual->to(at::kFloat);
   return y.to(x.scalar_type());
 }
 
 at::Tensor linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act,
                       const c10::optional<at::Tensor>& residual) {
-  TORCH_CHECK(act >= 0 && act <= 2, "amd_dft.linear: act must be 0 (none), 1 (gelu) or 2 (gelu, tanh form)");
+  TORCH_CHECK(act >= 0 && act <= 3, "amd_dft.linear: act must be 0 (none), 1 (gelu), 2 (gelu, tanh form) or 3 (gelu, bf16 erf fit)");
   TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == w.size(0), "amd_dft.linear: bias must have N entries");
   return linear_ref(x, w, bias, act, residual);
 }
@@ -100,7 +113,7 @@ at::Tensor linear_cpu(const at::Tensor& x, const at::Tensor& w, const c10::optio
 at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& bias,
                        int64_t act, const c10::optional<at::Tensor>& residual) {
   const c10::DeviceGuard guard(x_.device());
-  TORCH_CHECK(act >= 0 && act <= 2, "amd_dft.linear: act must be 0 (none), 1 (gelu) or 2 (gelu, tanh form)");
+  TORCH_CHECK(act >= 0 && act <= 3, "amd_dft.linear: act must be 0 (none), 1 (gelu), 2 (gelu, tanh form) or 3 (gelu, bf16 erf fit)");
   TORCH_CHECK(w_.dim() == 2 && x_.size(-1) == w_.size(1), "amd_dft.linear: x [..., K], w [N, K]");
   const int64_t K = w_.size(1), N = w_.size(0), M = x_.numel() / std::max<int64_t>(K, 1);
   TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "amd_dft.linear: bias must have N entries");
@@ -141,7 +154,7 @@ at::Tensor linear_cuda(const at::Tensor& x_, const at::Tensor& w_, const c10::op
 // (x - mean) w exactly, with no cancellation beyond fp32 accumulation.
 void check_linear_ln(const at::Tensor& x, const at::Tensor& w, const at::Tensor& c1, const c10::optional<at::Tensor>& bias,
                      const at::Tensor& stats, int64_t act) {
-  TORCH_CHECK(act >= 0 && act <= 2, "amd_dft.linear_ln: act must be 0 (none), 1 (gelu) or 2 (gelu, tanh form)");
+  TORCH_CHECK(act >= 0 && act <= 3, "amd_dft.linear_ln: act must be 0 (none), 1 (gelu), 2 (gelu, tanh form) or 3 (gelu, bf16 erf fit)");
   TORCH_CHECK(w.dim() == 2 && x.size(-1) == w.size(1), "amd_dft.linear_ln: x [..., K], w [N, K]");
   const int64_t K = w.size(1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
   TORCH_CHECK(c1.numel() == N, "amd_dft.linear_ln: c1 must have N entries");
@@ -157,8 +170,7 @@ at::Tensor linear_ln_ref(const at::Tensor& x, const at::Tensor& w, const at::Ten
   at::Tensor t = at::matmul(xf, w.to(at::kFloat).t());
   at::Tensor y = st.select(1, 1).unsqueeze(1) * (t - st.select(1, 0).unsqueeze(1) * c1.to(at::kFloat).reshape({1, -1}));
   if (bias.has_value() && bias->defined()) y = y + bias->to(at::kFloat).reshape({1, -1});
-  if (act == 1) y = at::gelu(y);
-  if (act == 2) y = at::gelu(y, "tanh");
+  y = apply_act_ref(y, act);
   std::vector<int64_t> os(x.sizes().begin(), x.sizes().end());
   os.back() = w.size(0);
   return y.reshape(os).to(x.scalar_type());

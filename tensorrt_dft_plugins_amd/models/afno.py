@@ -47,10 +47,12 @@ class AFNOConfig:
     num_blocks: int = 8
     sparsity_threshold: float = 0.01
     hard_thresholding_fraction: float = 1.0
-    # GELU of the bf16 block's fc1 epilogue on the hand GEMM: "erf" (default: FourCastNet's nn.GELU)
-    # or "tanh" (torch's approximate="tanh", an explicit opt-in: |difference| < 5e-4 absolute, rel-L2
-    # vs the exact fp32 reference 1.676e-3 against 1.665e-3 for erf on the fc1 shape, at 7-9 % less
-    # fc1 time -- profiles/gelu_tanh_bf16_r5.txt).  fp32 models always use the erf form.
+    # GELU of the bf16 block's fc1 epilogue on the hand GEMM (ops.spectral._BF16_GELU_ACT):
+    #   "erf" (default) FourCastNet's nn.GELU, evaluated as x sigmoid(x q(x^2)) to 2.6e-5 absolute of
+    #         the exact form -- below bf16 output resolution, at about the tanh form's cost;
+    #   "erf_exact" the A&S erf form of the fp32 path; "tanh" torch's approximate="tanh" (|difference|
+    #         <= 4.7e-4, an explicit opt-in; profiles/gelu_tanh_bf16_r5.txt).
+    # fp32 models always use the exact erf form.
     bf16_gelu: str = "erf"
 
     @property

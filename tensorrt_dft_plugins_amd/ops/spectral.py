@@ -233,6 +233,14 @@ def _mlp_gemm_ok(m, split: bool) -> bool:
             and k_ok(f2.in_features))
 
 
+# AFNOConfig.bf16_gelu -> the hand GEMM's epilogue activation for bf16 outputs (csrc/nn/gelu.h):
+#   "erf"       the erf GELU as x sigmoid(x q(x^2)), |error| <= 2.6e-5 absolute against the exact form
+#               (1/40 of half a bf16 ulp at |y| = 0.25) -- FourCastNet's nn.GELU at bf16 resolution
+#   "erf_exact" the A&S 7.1.26 erf form the fp32 path uses (|error| <= 1.5e-7)
+#   "tanh"      torch's approximate="tanh" (|difference| <= 4.7e-4: an explicit opt-in)
+_BF16_GELU_ACT = {"erf": 3, "erf_exact": 1, "tanh": 2}
+
+
 def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, part: Optional[torch.Tensor] = None):
     """FourCastNet block (bf16) with LN1 fused into the AFNO W-transforms and fc2 accumulated
     in place.
@@ -248,8 +256,9 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
                                                  writes LN2's per-64-channel partials of the stored
                                                  x1 (c2r_ln_add_part)
       h     = GELU(fc1(LN2(x1)))                 ln_stats_merge + hand MFMA GEMM with LN2 folded in
-                                                 (linear_ln) and the GELU in the epilogue -- the
-                                                 exact erf form unless cfg.bf16_gelu == "tanh" (see AFNOConfig)
+                                                 (linear_ln) and the GELU in the epilogue -- FourCastNet's
+                                                 erf form at bf16-output resolution unless cfg.bf16_gelu says
+                                                 otherwise (see AFNOConfig and _BF16_GELU_ACT)
       x1   += h @ W2^T                           hand MFMA GEMM, residual in the epilogue, which also
                                                  emits the next LN1's partials of x1 + b2
                                                  (linear_stats)
@@ -285,7 +294,7 @@ def afno_block_fused(blk, xs: torch.Tensor, pre: Optional[torch.Tensor] = None, 
         x1 = ops.c2r_ln_add(yw, 2, W, scale, xs, stats, g1, be1, pre32)
         st2 = ops.ln_stats(x1, None, blk.norm2.eps)
     w1g, c1, c2 = _ln_folded_fc(m.fc1, blk.norm2)
-    hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, 2 if getattr(c, "bf16_gelu", "erf") == "tanh" else 1)
+    hid = ops.linear_ln(x1.reshape(-1, C), w1g, c1, c2, st2, _BF16_GELU_ACT[getattr(c, "bf16_gelu", "erf")])
     if C > 64 * 64:
         x1 = ops.linear(hid, m.fc2.weight, None, 0, x1.reshape(-1, C)).reshape(B, H, W, C)
         return x1, m.fc2.bias

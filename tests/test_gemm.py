@@ -116,7 +116,7 @@ def test_linear_gelu_tanh_cpu_semantics():
     y = torch.ops.amd_dft.linear(x, w, b, 2, None)
     assert rel_l2(y, F.gelu(F.linear(x, w, b), approximate="tanh")) < 1e-6
     with pytest.raises(RuntimeError):
-        torch.ops.amd_dft.linear(x, w, b, 3, None)
+        torch.ops.amd_dft.linear(x, w, b, 4, None)
 
 
 @pytest.mark.gpu
@@ -141,3 +141,32 @@ def test_linear_gelu_tanh_gpu(device, ln):
     yf = y.float().cpu()
     assert rel_l2(yf, F.gelu(pre, approximate="tanh")) < 8e-3
     assert (F.gelu(pre, approximate="tanh") - F.gelu(pre)).abs().max() < 5e-4  # the form's own distance
+
+
+def test_linear_gelu_erf_fit_cpu_semantics():
+    """act = 3: the bf16 paths' erf GELU (x sigmoid(x q(x^2)), csrc/nn/gelu.h) is within 2.6e-5 absolute of
+    the exact erf GELU over the whole line, 18x closer than the tanh form."""
+    x = torch.linspace(-30, 30, 600001, dtype=torch.float64).float().reshape(-1, 1)
+    w = torch.ones(64, 1)  # y[:, n] = x
+    y = torch.ops.amd_dft.linear(x, w, None, 3)[:, 0].double()
+    exact = torch.nn.functional.gelu(x[:, 0].double())
+    assert (y - exact).abs().max() < 3e-5
+    tanh = torch.nn.functional.gelu(x[:, 0].double(), approximate="tanh")
+    assert (tanh - exact).abs().max() > 4e-4  # the form it replaces as the bf16 default
+
+
+@pytest.mark.gpu
+def test_linear_gelu_erf_fit_gpu(device):
+    """act = 3 on the hand GEMM (FourCastNet fc1 shape, bf16) against the exact erf GELU of the same
+    pre-activation: the epilogue's form is below bf16 resolution."""
+    torch.manual_seed(3)
+    M, K, N = 4096, 768, 3072
+    x = torch.randn(M, K, device=device).to(torch.bfloat16)
+    w = (0.03 * torch.randn(N, K, device=device)).to(torch.bfloat16)
+    b = 0.1 * torch.randn(N, device=device)
+    y = torch.ops.amd_dft.linear(x, w, b, 3).float()
+    pre = torch.nn.functional.linear(x.float(), w.float(), b)
+    ref = torch.nn.functional.gelu(pre)
+    assert rel_l2(y, ref) < 4e-3  # bf16 output rounding
+    yt = torch.ops.amd_dft.linear(x, w, b, 2).float()
+    assert rel_l2(y, ref) <= rel_l2(yt, ref)
