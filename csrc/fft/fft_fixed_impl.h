@@ -196,16 +196,15 @@ __device__ __forceinline__ float2 ln_pair(const Ctx& x, int n, float2 v, float2&
   return make_float2((xp.x - s.x) * s.y * x.g.x + x.be.x, (xp.y - s.x) * s.y * x.g.y + x.be.y);
 }
 
-// Column layouts of the 720-point transforms at T = 4 (rfft2 / irfft2 columns, the FNO H transforms):
-// position n of slot t at n*T + t + COL_PW * (n / 8) -- two pad slots per 8 positions instead of one
-// per position.  A bank simulation of the (8, 9, 10) Stockham pattern (pass-0 writes at stride 8
-// positions, passes 1-2 reads of consecutive positions, ds_read/write_b64) gives 1.95 cycles per wave
-// instruction against 3.16 for the T + 1 stride (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS was
-// 3.72 on this kernel).  Every access of both radix orders configured for 720 ((8, 9, 10), (24, 30))
-// stays affine in the unrolled radix index (n / 8 splits into a per-thread part and a constant), so
-// the compiler still folds the offsets into ds_read / ds_write immediates.
+// Column layouts of the 720-point transforms at T = 4 (rfft2 / irfft2 columns, the FNO H transforms),
+// A/B build -DAMD_DFT_COL_PW8=1: position n of slot t at n*T + t + COL_PW * (n / 8) -- two pad slots per
+// 8 positions instead of one per position.  Bank-conflict cycles per LDS instruction 3.72 -> 1.08
+// (VERDICT r5 #6), but the extra index arithmetic is not folded into ds_read / ds_write immediates:
+// +29 % VALU and +18 % LDS instructions per wave, rfft2 / irfft2 +0.5 us and the FNO block +1.3 us
+// (profiles/fft_lds_pad_r6.txt; the conflicts it removes were ~90 cycles of a ~10k-cycle wave).  The
+// shipped default keeps the T + 1 stride.
 #ifndef AMD_DFT_COL_PW8
-#define AMD_DFT_COL_PW8 1  // 0: the T + 1 stride for these columns too (A/B build)
+#define AMD_DFT_COL_PW8 0  // 1: the two-pads-per-8 column layout (A/B build, measured slower)
 #endif
 template <bool COLS, int T, int L>
 constexpr __host__ __device__ int col_pw() {
