@@ -161,6 +161,15 @@ int main() {
   g1.act = 1;
   g1.stamps = stamps;
   run("fc1 bf16 + GELU", g1, stamps);
+  GemmLaunch g1f = g1;  // the bf16 model's fc1: LayerNorm folded, fitted erf GELU (act 3)
+  g1f.act = 3;
+  g1f.ln_stats = lnst;
+  g1f.ln_c1 = c1;
+  run("fc1 bf16 + LN fold + GELU (erf fit)", g1f, stamps);
+  GemmLaunch g1p = g1;  // plain: no bias, no activation (the hipBLASLt comparison shape)
+  g1p.act = 0;
+  g1p.bias = nullptr;
+  run("fc1 bf16 plain", g1p, stamps);
   GemmLaunch g2;
   g2.x = h;
   g2.w = w2;

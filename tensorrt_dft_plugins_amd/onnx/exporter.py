@@ -289,7 +289,9 @@ def export(model: torch.nn.Module, args: Any, f: Optional[str | io.BytesIO] = No
             model, args, buf, dynamo=False, operator_export_type=torch.onnx.OperatorExportTypes.ONNX,
             opset_version=opset_version, verbose=verbose, input_names=input_names, output_names=output_names,
             dynamic_axes=dynamic_axes, do_constant_folding=do_constant_folding,
-            custom_opsets={CONTRIB_DOMAIN: 1, AMD_DOMAIN: 1},
+            # no declared custom opsets: the exporter imports exactly the domains the graph uses
+            # (com.microsoft and / or com.amd.dft, version 1) -- declaring both warned about the unused one
+            custom_opsets={},
         )
     data = buf.getvalue()
     if isinstance(f, str):
