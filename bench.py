@@ -111,6 +111,24 @@ def _rccl_log_read(d: str | None) -> dict:
     return rccl_choices(text)
 
 
+def init_single_rank_group() -> None:
+    """A process group of one rank (``--force-gather``): RCCL (backend "nccl") on a GPU, Gloo on the
+    CPU, rendezvous on 127.0.0.1 and a free port."""
+    import socket
+    from datetime import timedelta
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    if torch.cuda.is_available():
+        dev = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                timeout=timedelta(seconds=300), device_id=dev)
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                timeout=timedelta(seconds=300))
+
+
 def log(msg: str) -> None:
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -193,7 +211,7 @@ def run_steps(runner, steps: int, warmup: int, world: int, dev, cuda: bool) -> f
     sync()
     barrier()
     sync()
-    if world > 1 and hasattr(runner, "time_comm"):
+    if getattr(runner, "gather", False) and hasattr(runner, "time_comm"):
         runner.time_comm(True)  # event pair around each timed gather (comm-stream busy time)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -274,7 +292,8 @@ def build_runner(cfg, dtype, B, dev, a, seed, input_seed=0, gather_dtype=None, e
             f"{info['engine_build_load_s']}s")
     t0 = time.perf_counter()
     runner = DataParallelInference(fn, x, gather=not a.no_gather, use_graph=not a.no_graph,
-                                   gather_backend=a.gather, gather_dtype=gather_dtype)
+                                   gather_backend=a.gather, gather_dtype=gather_dtype,
+                                   force_gather=getattr(a, "force_gather", False))
     log(f"{dtype}: captured forward (graph={runner.cap.use_graph}) in {time.perf_counter() - t0:.1f}s")
     return info, runner
 
@@ -364,6 +383,9 @@ def main(argv=None) -> int:
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--gather", choices=["rccl", "ipc"], default=os.environ.get("MI_DFT_GATHER", "rccl"),
                     help="output all-gather: RCCL ring collective or direct IPC pushes over xGMI")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="single process: create a one-rank process group (RCCL on a GPU) and run the output "
+                         "all-gather + its verification in every timed step (the multi-GPU comm path on one GPU)")
     ap.add_argument("--no-fft", action="store_true", help="skip the rfft2 720x1440 / FNO block probes")
     ap.add_argument("--tiny", action="store_true", help="tiny model/grid (harness smoke test, CPU ok)")
     ap.add_argument("--json-out", default=None)
@@ -371,6 +393,8 @@ def main(argv=None) -> int:
 
     rccl_dir = _rccl_log_setup(int(os.environ.get("WORLD_SIZE", "1")))
     rank, world, local = init_distributed()
+    if a.force_gather and world == 1 and not dist.is_initialized():
+        init_single_rank_group()
     if world != a.gpus and world > 1:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     cuda = torch.cuda.is_available()
@@ -406,7 +430,7 @@ def main(argv=None) -> int:
     elapsed = run_steps(runner, a.steps, a.warmup, world, dev, cuda)
     gathered = runner.gather
     gather_backend_used = runner.gather_backend
-    comm_diag = multi_gpu_diagnostics(runner, a.steps, world, dev, cuda) if world > 1 else {}
+    comm_diag = multi_gpu_diagnostics(runner, a.steps, world, dev, cuda) if gathered else {}
     runner.close()
     del runner
     if cuda:
@@ -477,11 +501,11 @@ def main(argv=None) -> int:
                 "output_allgather": gathered,
                 "gather_backend": (gather_backend_used if gather_backend_used == "ipc" else
                                    ("rccl" if dist.get_backend() == "nccl" else dist.get_backend()))
-                if world > 1 and gathered else None,
+                if gathered else None,
                 "gemm": "hand-mfma",
                 "gemm_precision": "bf16x3 split, fp32 accumulate" if head_dt == torch.float32 else "bf16, fp32 accumulate",
                 "gather_dtype": ("bf16" if gdt is not None else ("bf16" if head_dt == torch.bfloat16 else "fp32"))
-                if world > 1 and gathered else None,
+                if gathered else None,
                 "comm_env": dict({k: os.environ[k] for k in COMM_ENV if k in os.environ},
                                  **({"rccl": rccl} if rccl else {})),
             },
@@ -496,7 +520,7 @@ def main(argv=None) -> int:
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -87,6 +87,21 @@ def shard_checksum(t: torch.Tensor, chunk: int = 1 << 24) -> torch.Tensor:
     return torch.stack([s0, s1]).cpu()
 
 
+_HOST_GROUP = {}
+
+
+def _host_group():
+    """A Gloo group over the default group's ranks for host-side exchanges (created once per default
+    process group: ``new_group`` is collective, so every rank reaches this in the same order)."""
+    if dist.get_backend() == "gloo":
+        return None
+    key = id(dist.group.WORLD)
+    if key not in _HOST_GROUP:
+        _HOST_GROUP.clear()
+        _HOST_GROUP[key] = dist.new_group(backend="gloo")
+    return _HOST_GROUP[key]
+
+
 def ipc_peer_access_problem(device: torch.device) -> Optional[str]:
     """Why the direct IPC mesh cannot span the ranks (None if it can): every rank's device index is
     all-gathered and each rank checks ``hipDeviceCanAccessPeer`` to every peer's device; one
@@ -96,8 +111,9 @@ def ipc_peer_access_problem(device: torch.device) -> Optional[str]:
     rank, world = world_info()
     dev = device.index if device.index is not None else torch.cuda.current_device()
     devs: List[Optional[int]] = [None] * world
+    grp = None
     if world > 1:
-        grp = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else None
+        grp = _host_group()
         dist.all_gather_object(devs, dev, group=grp)
     else:
         devs = [dev]

@@ -382,3 +382,17 @@ def test_rccl_world1_capture_and_gather_gpu():
                        text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "rccl capture probe ok" in r.stdout
+
+
+def test_bench_force_gather_single_process_cpu():
+    """``bench.py --force-gather`` at world 1: a one-rank process group (Gloo here, RCCL on a GPU) and the
+    output all-gather + its exact-checksum verification in every timed step."""
+    import json
+
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--tiny", "--force-gather", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["config"]["output_allgather"] is True
+    assert d["multi_gpu"]["collective_ranks"] == 1 and d["multi_gpu"]["gather_verified"] is True
