@@ -193,6 +193,11 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 #ifndef GEMM_HALF
 #define GEMM_HALF 3
 #endif
+// GEMM_HALF_BAL: the two-phase schedule's B-region DMA spread over wave group 1's two read sections
+// (see half_batch in gemm_bf16_kernel); 0 (default) = all of it in the read-B section (the round-4 form)
+#ifndef GEMM_HALF_BAL
+#define GEMM_HALF_BAL 0  // 1: measured slower (profiles/gemm_dma_balance_r6.txt)
+#endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
                                               Mid&& mid) {
@@ -377,24 +382,31 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   // HALF: two-phase K-tile schedule (see the main loop); wave group as a scalar for its branches
   constexpr bool HALF = ((GEMM_HALF >> (SPLIT ? 1 : 0)) & 1) && !PERSIST && MODE != 1;
   const int wrs = __builtin_amdgcn_readfirstlane(wr);
-  // HALF batch(kt): R0 (each group its own feature rows) + R1 / R2 (all token rows, wave group 1 only)
-  auto half_batch = [&](int kt, char* st) {
+  // HALF batch(kt): R0 (each group its own feature rows) + R1 / R2 (all token rows, wave group 1 only).
+  // BAL (GEMM_HALF_BAL): wave group 1 issues R2(kt) one section later, in its read-A section of K-tile
+  // kt - 1 (ahead of that section's R3), instead of in the read-B section with R0 / R1: its sections
+  // then carry 6 + 6 DMA pieces instead of 2 + 10, and no read section's DMA issue outlasts the partner
+  // wave's MFMA cluster.  R2(kt)'s old contents (K-tile kt - 2) were last read in read-A(kt - 2) by both
+  // groups; it lands before the read-B wait of K-tile kt - 1 (issued ahead of R3(kt), so that wait keeps
+  // counting R3's two pieces as the only younger ones).
+  constexpr bool BAL = HALF && GEMM_HALF_BAL;
+  auto half_batch = [&](int kt, char* st, bool with_r2) {
     if constexpr (HALF) {
       stage_region<0, MODE, SPLIT>(W, X, K, f0, t0, M, kt, st, wave, lane0, p, gb);
       if (wrs == 1) {
         stage_region<1, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, kt, st, wave - 4, lane0, p, gb);
-        stage_region<2, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, kt, st, wave - 4, lane0, p, gb);
+        if (with_r2) stage_region<2, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, kt, st, wave - 4, lane0, p, gb);
       }
     }
   };
   bf16x8 a0[8], a1[8], b0[4], b1[4];
   if constexpr (HALF) {
-    // ---- prologue: batch(0), R3(0), batch(1)
-    half_batch(0, smem);
+    // ---- prologue: batch(0), R3(0), batch(1) (BAL: batch(1) without R2(1), which read-A(0) issues)
+    half_batch(0, smem, true);
     stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, 0, smem, wave, lane0, p, gb);
     if (KT > 1) {
-      half_batch(1, smem + kStage);
-      if (wrs == 1) wait_vm<12>();  // batch(0) landed; younger: R3(0) (2) + batch(1) (10 / 2)
+      half_batch(1, smem + kStage, !BAL);
+      if (wrs == 1) wait_vm<BAL ? 8 : 12>();  // batch(0) landed; younger: R3(0) (2) + batch(1) (6 / 10 / 2)
       else wait_vm<4>();
     } else {
       wait_vm<2>();
@@ -481,8 +493,10 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
         // ---- read A(t)
         if (n1) {
-          if (wrs == 1) wait_vm<10>();  // R3(t) landed; younger: batch(t+1)
+          if (wrs == 1) wait_vm<BAL ? 6 : 10>();  // R3(t) landed; younger: batch(t+1) (BAL: without R2(t+1))
           else wait_vm<2>();
+          if (BAL && wrs == 1)  // R2(t+1) ahead of R3(t+1) (see half_batch)
+            stage_region<2, MODE, SPLIT, false, false, 4>(W, X, K, f0, t0, M, t + 1, nxt, wave - 4, lane, p, gb);
           stage_region<3, MODE, SPLIT>(W, X, K, f0, t0, M, t + 1, nxt, wave, lane, p, gb);
         } else {
           wait_vm<0>();
@@ -497,7 +511,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
         barrier();
         // ---- read B(t)
         if (n1) wait_vm<2>();  // batch(t+1) landed; younger: R3(t+1)
-        if (n2) half_batch(t + 2, cur);
+        if (n2) half_batch(t + 2, cur, !BAL);
         read_a<3>(a0, cur, wr, r16, kq);
         barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
