@@ -96,3 +96,46 @@ def test_contrib_fno_engine_full_size(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Throughput" in r.stdout
     print(r.stdout.strip().splitlines()[-1])
+
+
+def test_contrib_fourcastnet_engine_headline_config():
+    """The headline configuration through the reference's workflow: FourCastNet at depth 12,
+    batch 32, 720x1440, written with the ONNX-contrib Rfft/Irfft + stock ops, exported, optimized (every block on the
+    fused kernels, nothing rejected), serialized, deserialized and replayed -- against the torch fp32 model."""
+    torch.manual_seed(2)
+    cfg = AFNOConfig(depth=12)
+    m = AFNONet(cfg, backend="contrib").cuda().eval()
+    x = torch.randn(32, cfg.in_chans, *cfg.img_size, device="cuda")
+    eng = Engine.build(m, (x,))
+    opt = eng.header.extra["optimizer"]
+    assert opt["applied"].get("afno_block") == 12 and not opt["rejected"], opt
+    eng2 = Engine.deserialize(eng.serialize())
+    del eng
+    torch.cuda.empty_cache()
+    (y,) = eng2.infer(x)
+    del eng2
+    torch.cuda.empty_cache()
+    ref = AFNONet(cfg, backend="torch").cuda().eval()
+    ref.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        want = ref(x)
+    err = _rel(y, want)
+    print(f"contrib FourCastNet engine (depth 12, batch 32, 720x1440) rel-L2 vs torch fp32: {err:.3e}")
+    assert err < 5e-5
+
+
+def test_contrib_and_native_engines_agree():
+    """The contrib-export engine (bench.py's headline) and the native-export engine run the same kernels: equal
+    outputs to the last few bits at depth 2, batch 2, 720x1440 (profiles/engine_diff_r6.txt: same sequence at depth 12)."""
+    torch.manual_seed(3)
+    cfg = AFNOConfig(depth=2)
+    x = torch.randn(2, cfg.in_chans, *cfg.img_size, device="cuda")
+    outs, ops = {}, {}
+    for backend in ("contrib", "amd"):
+        torch.manual_seed(4)
+        m = AFNONet(cfg, backend=backend).cuda().eval()
+        eng = Engine.build(m, (x,))
+        outs[backend] = eng.infer(x)[0]
+        ops[backend] = [n[4] for n in eng.graph.nodes if n[4] != "Reshape"]
+    assert ops["contrib"] == ops["amd"], ops
+    assert _rel(outs["contrib"], outs["amd"]) < 1e-6
