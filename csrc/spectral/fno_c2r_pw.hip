@@ -134,6 +134,27 @@ __device__ __forceinline__ float act(float v) {
   return v;
 }
 
+#ifndef FNO_BF_ACT
+#define FNO_BF_ACT 3  // bf16 output's GELU: 3 the fitted erf form (default), 2 the tanh form (A/B build: its cost)
+#endif
+#ifndef FNO_ACT_PACKED
+#define FNO_ACT_PACKED 1  // epilogue GELU on value pairs with packed f32 VALU (csrc/nn/gelu.h); 0: per value
+#endif
+// the activation of two values: packed f32 FMAs / MULs issue once for both (the transcendentals stay per
+// value); the fp32 form is gelu.h's A&S arrangement (same 1.5e-7 bound as gelu_erf above)
+template <int ACT>
+__device__ __forceinline__ float2 act2(float a, float b) {
+  if constexpr (FNO_ACT_PACKED && ACT != 0) {
+    gelu_f2 r;
+    if constexpr (ACT == 1) r = gelu_erf2(gelu_f2{a, b});
+    else if constexpr (ACT == 2) r = gelu_tanh2(gelu_f2{a, b});
+    else r = gelu_erf_fit2(gelu_f2{a, b});
+    return make_float2(r.x, r.y);
+  } else {
+    return make_float2(act<ACT>(a), act<ACT>(b));
+  }
+}
+
 // row_ror:n inside 16-lane rows: lane i receives lane (i - n) mod 16 of its row
 template <int N>
 __device__ __forceinline__ float row_ror(float v) {
@@ -455,7 +476,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
               const int p4 = hp * TPS + pp;
               float v[4];
 #pragma unroll
-              for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
+              for (int i = 0; i < 4; i += 2) {
+                const float2 r = act2<ACT>(acc[p4][ot][i], acc[p4][ot][i + 1]);
+                v[i] = r.x;
+                v[i + 1] = r.y;
+              }
               if (ch < Cout) store4<BF>(es + ch * EP + (16 * pp + 4 * lq) * ES, v);
             }
           }
@@ -489,8 +514,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           uint32_t d[4][2];
 #pragma unroll
           for (int p4 = 0; p4 < 4; ++p4) {
-            d[p4][0] = pk_bf16(act<ACT>(acc[p4][ot][0]), act<ACT>(acc[p4][ot][1]));
-            d[p4][1] = pk_bf16(act<ACT>(acc[p4][ot][2]), act<ACT>(acc[p4][ot][3]));
+            const float2 r0 = act2<ACT>(acc[p4][ot][0], acc[p4][ot][1]), r1 = act2<ACT>(acc[p4][ot][2], acc[p4][ot][3]);
+            d[p4][0] = pk_bf16(r0.x, r0.y);
+            d[p4][1] = pk_bf16(r1.x, r1.y);
           }
 #pragma unroll
           for (int pp = 0; pp < 2; ++pp)
@@ -517,7 +543,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           for (int p4 = 0; p4 < 4; ++p4) {
             float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = act<ACT>(acc[p4][ot][i]);
+            for (int i = 0; i < 4; i += 2) {
+              const float2 r = act2<ACT>(acc[p4][ot][i], acc[p4][ot][i + 1]);
+              v[i] = r.x;
+              v[i + 1] = r.y;
+            }
             if (o < Cout && pxg + 16 * p4 < W) store4<BF>(yb + yrow[ot] + (w0 + 64 * pg + 16 * p4) * ES, v);
           }
         }
@@ -530,7 +560,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         for (int i = 0; i < 4; ++i) {
           const float a0 = acc[0][CO - 1][i], a1 = row_ror<4>(acc[1][CO - 1][i]), a2 = row_ror<8>(acc[2][CO - 1][i]),
                       a3 = row_ror<12>(acc[3][CO - 1][i]);
-          v[i] = act<ACT>(s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3);
+          v[i] = s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const float2 r = act2<ACT>(v[i], v[i + 1]);
+          v[i] = r.x;
+          v[i + 1] = r.y;
         }
         const int o = 16 + cc;
         if (o < Cout && pxg + 16 * s < W) store4<BF>(yb + yrowp + (w0 + 64 * pg + 16 * s) * ES, v);
@@ -559,7 +595,7 @@ int64_t resident_wgs() {
   if (cache[dev] == 0) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const auto kern = reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, BF ? 3 : 1>);
+    const auto kern = reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, BF ? FNO_BF_ACT : 1>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
     cache[dev] = static_cast<int64_t>(cus) * per_cu;
   }
@@ -592,7 +628,7 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
   hipLaunchKernelGGL((fno_c2r_pw_kernel<BF, KS, CO, A>), grid, dim3(256), 0, st, yw, p.x, p.wc, p.bias, p.y, g0, rot, \
                      p.Cin, p.Cout, p.H, p.W, p.m, nch, units)
   if (!p.gelu) L_(0);
-  else if (BF) L_(3);
+  else if (BF) L_(FNO_BF_ACT);
   else L_(1);
 #undef L_
 }
