@@ -95,11 +95,12 @@ def _host_group():
     process group: ``new_group`` is collective, so every rank reaches this in the same order)."""
     if dist.get_backend() == "gloo":
         return None
-    key = id(dist.group.WORLD)
-    if key not in _HOST_GROUP:
-        _HOST_GROUP.clear()
-        _HOST_GROUP[key] = dist.new_group(backend="gloo")
-    return _HOST_GROUP[key]
+    world = dist.group.WORLD
+    # keyed by the group object itself (held here, so a later default group cannot reuse its id)
+    if _HOST_GROUP.get("world") is not world:
+        _HOST_GROUP["world"] = world
+        _HOST_GROUP["gloo"] = dist.new_group(backend="gloo")
+    return _HOST_GROUP["gloo"]
 
 
 def ipc_peer_access_problem(device: torch.device) -> Optional[str]:
