@@ -191,7 +191,10 @@ def time_fno_block_us(rounds: int = 5) -> dict:
     blk = FNOBlock(20, 32, 32, backend="amd").cuda().eval()
     x = torch.randn(1, 20, 720, 1440, device="cuda").to(torch.bfloat16)
     with torch.no_grad():
-        return {"fno_block_720x1440_bf16_us": _graph_us(lambda: blk(x), 20, rounds)}
+        # the FNO layer (spectral conv + 1x1 conv + GELU, the number tracked since round 1) and the
+        # SpectralConv2d alone (rfft2 -> complex mul -> irfft2: config 3's literal definition)
+        return {"fno_block_720x1440_bf16_us": _graph_us(lambda: blk(x), 20, rounds),
+                "spectral_conv2d_720x1440_bf16_us": _graph_us(lambda: blk.spectral(x), 20, rounds)}
 
 
 def run_steps(runner, steps: int, warmup: int, world: int, dev, cuda: bool) -> float:

@@ -294,6 +294,69 @@ at::Tensor fno_c2r_pw_meta(const at::Tensor& yw, const at::Tensor& x, const at::
   return at::empty({x.size(0), yw.size(1), x.size(2), x.size(3)}, x.options());
 }
 
+// ------------------------------------------------------------------ SpectralConv2d tail (C2R-W only)
+// yw [B, Cout, H, m, 2] fp32 (inverse-H-transformed kept modes, carrying the 1/(H W) scale) ->
+// y [B, Cout, H, W] = irfft_W(yw) in out_dtype (float32 default, or bfloat16): the fno_c2r_pw kernel
+// without its pointwise branch (no x read, no 1x1 conv, no activation) -- the classic FNO
+// SpectralConv2d ends here (BASELINE config 3: rfft2 -> complex mul -> irfft2).
+at::ScalarType fno_c2r_dtype(const at::Tensor& yw, int64_t W, const std::optional<at::ScalarType>& out_dtype) {
+  TORCH_CHECK(yw.dim() == 5 && yw.size(4) == 2, "fno_c2r: yw must be [B, Cout, H, m, 2]");
+  TORCH_CHECK(W >= 1 && 2 * (yw.size(3) - 1) <= W, "fno_c2r: more modes than the half spectrum of W");
+  const at::ScalarType dt = out_dtype.has_value() ? *out_dtype : at::kFloat;
+  TORCH_CHECK(dt == at::kFloat || dt == at::kBFloat16, "fno_c2r: out_dtype must be float32 or bfloat16");
+  return dt;
+}
+
+at::Tensor fno_c2r_cpu(const at::Tensor& yw, int64_t W, std::optional<at::ScalarType> out_dtype) {
+  const at::ScalarType dt = fno_c2r_dtype(yw, W, out_dtype);
+  const int64_t m = yw.size(3);
+  at::Tensor full = at::zeros({yw.size(0), yw.size(1), yw.size(2), W / 2 + 1}, yw.options().dtype(at::kComplexDouble));
+  full.narrow(3, 0, m).copy_(at::view_as_complex(yw.to(at::kDouble).contiguous()));
+  return at::fft_irfft(full, W, 3, "forward").to(dt);
+}
+
+at::Tensor fno_c2r_cuda(const at::Tensor& yw_, int64_t W, std::optional<at::ScalarType> out_dtype) {
+  const c10::DeviceGuard guard(yw_.device());
+  const at::ScalarType dt = fno_c2r_dtype(yw_, W, out_dtype);
+  const int64_t B = yw_.size(0), Cout = yw_.size(1), H = yw_.size(2), m = yw_.size(3);
+  if (!fno_c2r_pw_supported(1, static_cast<int>(Cout), static_cast<int>(m), static_cast<int>(W), dt == at::kBFloat16) ||
+      B * Cout * H * W >= (int64_t(1) << 31)) {
+    // shapes outside the fused kernel: C2R on the FFT kernels
+    static auto c2r = c10::Dispatcher::singleton()
+                          .findSchemaOrThrow("amd_dft::c2r", "")
+                          .typed<at::Tensor(const at::Tensor&, at::IntArrayRef, at::IntArrayRef, double,
+                                            at::IntArrayRef, std::optional<at::ScalarType>)>();
+    const std::vector<int64_t> dim{3}, out_size{W};
+    return c2r.call(yw_.to(at::kFloat).contiguous(), dim, out_size, 1.0, {}, dt);
+  }
+  at::Tensor yw = yw_.to(at::kFloat).contiguous();
+  at::Tensor y = at::empty({B, Cout, H, W}, yw.options().dtype(dt));
+  auto tabs = get_dft_gemm_tables(dt == at::kBFloat16 ? DftTable::C2R_BF16 : DftTable::C2R_F32, static_cast<int>(W),
+                                  static_cast<int>(m), yw.device());
+  FnoC2RPwLaunch p;
+  p.yw = yw.data_ptr();
+  p.x = nullptr;  // spectral path only
+  p.wc = nullptr;
+  p.bias = nullptr;
+  p.y = y.data_ptr();
+  p.g0 = tabs.first.data_ptr();
+  p.rot = tabs.second.data_ptr();
+  p.B = static_cast<int>(B);
+  p.Cin = 0;
+  p.Cout = static_cast<int>(Cout);
+  p.H = static_cast<int>(H);
+  p.W = static_cast<int>(W);
+  p.m = static_cast<int>(m);
+  p.bf16 = dt == at::kBFloat16;
+  p.gelu = 0;
+  launch_fno_c2r_pw(p, c10::hip::getCurrentHIPStream(yw.device().index()).stream());
+  return checked(y, "fno_c2r");
+}
+
+at::Tensor fno_c2r_meta(const at::Tensor& yw, int64_t W, std::optional<at::ScalarType> out_dtype) {
+  return at::empty({yw.size(0), yw.size(1), yw.size(2), W}, yw.options().dtype(out_dtype.has_value() ? *out_dtype : at::kFloat));
+}
+
 // ------------------------------------------------------------------ LayerNorm (+ residual)
 std::tuple<at::Tensor, at::Tensor> layer_norm_cpu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                   double eps, const std::optional<at::Tensor>& residual) {
@@ -513,6 +576,7 @@ TORCH_LIBRARY_FRAGMENT(amd_dft, m) {
   m.def("fno_mix(Tensor x, Tensor w, int path=0) -> Tensor");
   m.def("fno_pointwise(Tensor? spec, Tensor x, Tensor w, Tensor? bias=None, bool gelu=True) -> Tensor");
   m.def("fno_c2r_pw(Tensor yw, Tensor x, Tensor wc, Tensor? bias=None, bool gelu=True) -> Tensor");
+  m.def("fno_c2r(Tensor yw, int W, ScalarType? out_dtype=None) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
@@ -524,6 +588,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CUDA, m) {
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cuda));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cuda));
   m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cuda));
+  m.impl("fno_c2r", AMD_DFT_TRACED("amd_dft::fno_c2r", amd_dft::fno_c2r_cuda));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
@@ -535,6 +600,7 @@ TORCH_LIBRARY_IMPL(amd_dft, CPU, m) {
   m.impl("fno_mix", AMD_DFT_TRACED("amd_dft::fno_mix", amd_dft::fno_mix_cpu));
   m.impl("fno_pointwise", AMD_DFT_TRACED("amd_dft::fno_pointwise", amd_dft::fno_pointwise_cpu));
   m.impl("fno_c2r_pw", AMD_DFT_TRACED("amd_dft::fno_c2r_pw", amd_dft::fno_c2r_pw_cpu));
+  m.impl("fno_c2r", AMD_DFT_TRACED("amd_dft::fno_c2r", amd_dft::fno_c2r_cpu));
 }
 
 TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
@@ -546,4 +612,5 @@ TORCH_LIBRARY_IMPL(amd_dft, Meta, m) {
   m.impl("fno_mix", &amd_dft::fno_mix_meta);
   m.impl("fno_pointwise", &amd_dft::fno_pointwise_meta);
   m.impl("fno_c2r_pw", &amd_dft::fno_c2r_pw_meta);
+  m.impl("fno_c2r", &amd_dft::fno_c2r_meta);
 }

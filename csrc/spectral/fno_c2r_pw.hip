@@ -167,8 +167,10 @@ __device__ __forceinline__ void store4(char* dst, const float (&v)[4]) {
   else *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-template <bool BF, int KS, int CO, int ACT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) fno_c2r_pw_kernel(const float2* __restrict__ yw, const void* __restrict__ x,
+// PW = false: the spectral path alone (SpectralConv2d: y = irfft_W(Y), no x, no 1x1 conv, no activation) --
+// no x staging in LDS (32 KB per workgroup instead of 69) and no x prefetch registers
+template <bool BF, int KS, int CO, int ACT, bool PW = true>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, PW ? 2 : 4))) fno_c2r_pw_kernel(const float2* __restrict__ yw, const void* __restrict__ x,
                                                          const float* __restrict__ wc, const float* __restrict__ bias,
                                                          void* __restrict__ y, const bf16x8* __restrict__ g0,
                                                          const float2* __restrict__ rot, int Cin, int Cout, int H,
@@ -179,7 +181,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr bool YLO = !BF || FNO_BF_YLO;  // the G_hi * Y_lo term
   constexpr int NG = PREC3 ? 2 : 1;
   __shared__ bf16x8 g0s[KS][PT][NG][64];
-  __shared__ __attribute__((aligned(16))) char xs_raw[4][32 * XP * ES];
+  static_assert(PW || ACT == 0, "the spectral-only tail has no activation");
+  __shared__ __attribute__((aligned(16))) char xs_raw[4][PW ? 32 * XP * ES : 16];
   // chunk rotations in LDS (needed right before each chunk's MFMAs; an L2 round trip there
   // stalled every chunk)
   // (launch_fno_c2r_pw guarantees nch * 16 KS <= kFnoRotMax)
@@ -243,6 +246,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
   auto load_x = [&](const UPos& q) {
+    if constexpr (!PW) return;
     const int cw = q.c * CH + st_px;
     const char* src = static_cast<const char*>(x) +
                       (((static_cast<int64_t>(q.b) * Cin + st_ch) * H + q.h) * W + cw) * ES;
@@ -317,7 +321,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   for (int ot = 0; ot < CO; ++ot) {
     const int o = min(16 * ot + l15, Cout - 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wcv[ot][j] = wc[o * Cin + min(8 * lq + j, Cin - 1)];
+    for (int j = 0; j < 8; ++j) wcv[ot][j] = PW ? wc[o * Cin + min(8 * lq + j, Cin - 1)] : 0.f;
     bo[ot] = bias != nullptr ? bias[o] : 0.f;
   }
 #pragma unroll
@@ -346,7 +350,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
   // channel rows >= Cin stay zero (their weights are zero, but 0 * stale-NaN is not); rows < Cin
   // are rewritten by every chunk before they are read
-  {
+  if constexpr (PW) {
     constexpr int RW = XP * ES / 16;  // 16-byte words per channel row
     const int nz = (32 - Cin) * RW;   // per wave tile
     for (int t = threadIdx.x; t < 4 * nz; t += 256) {
@@ -371,7 +375,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int ch = st_ch + RPI * q;
-      if (ch < Cin) {
+      if (PW && ch < Cin) {
         Raw* dst = reinterpret_cast<Raw*>(xs + (ch * XP + st_px) * ES);
 #pragma unroll
         for (int t = 0; t < NR; ++t) dst[t] = xr[q][t];
@@ -414,7 +418,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
         for (int ot = 0; ot < CO; ++ot) acc[p4][ot] = f32x4{bo[ot], bo[ot], bo[ot], bo[ot]};
         bf16x8 ax, axl;
-        if constexpr (BF) {
+        if constexpr (!PW) {
+        } else if constexpr (BF) {
           // rows 8lq + (0..3) and 8lq + (4..7), cols 16pt..16pt+15: lane 4q'+p addresses row q', cols 4p..4p+3
           const int e0 = (8 * lq + (l15 >> 2)) * XP + 16 * pt + 4 * (l15 & 3);
           const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(xs_tr + e0 / 4);
@@ -432,7 +437,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
           axl = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
         }
 #pragma unroll
-        for (int ot = 0; ot < CO; ++ot) {
+        for (int ot = 0; ot < CO && PW; ++ot) {
           acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wh[ot], acc[p4][ot], 0, 0, 0);
           if constexpr (!BF) {  // bf16 output: bf16 conv weights, as a bf16 nn.Conv2d has
             acc[p4][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, Wl[ot], acc[p4][ot], 0, 0, 0);
@@ -587,7 +592,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 // workgroups of one kernel instance resident on the current device (occupancy x CUs), cached
-template <bool BF, int KS, int CO>
+template <bool BF, int KS, int CO, bool PW>
 int64_t resident_wgs() {
   static int64_t cache[64] = {};
   int dev = 0;
@@ -595,7 +600,8 @@ int64_t resident_wgs() {
   if (cache[dev] == 0) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const auto kern = reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, BF ? FNO_BF_ACT : 1>);
+    const auto kern = PW ? reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, BF ? FNO_BF_ACT : 1>)
+                         : reinterpret_cast<const void*>(&fno_c2r_pw_kernel<BF, KS, CO, 0, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
     cache[dev] = static_cast<int64_t>(cus) * per_cu;
   }
@@ -619,7 +625,9 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
     return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1) << 40;
   }();
   const int64_t nwg = std::max<int64_t>(
-      std::min<int64_t>(std::min<int64_t>((units + 4 * upw - 1) / (4 * upw), resident_wgs<BF, KS, CO>()), wgs_cap), 1);
+      std::min<int64_t>(std::min<int64_t>((units + 4 * upw - 1) / (4 * upw),
+                                          p.x ? resident_wgs<BF, KS, CO, true>() : resident_wgs<BF, KS, CO, false>()),
+                        wgs_cap), 1);
   const dim3 grid(static_cast<uint32_t>(nwg));
   const float2* yw = static_cast<const float2*>(p.yw);
   const bf16x8* g0 = static_cast<const bf16x8*>(p.g0);
@@ -627,9 +635,16 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
 #define L_(A)                                                                                                     \
   hipLaunchKernelGGL((fno_c2r_pw_kernel<BF, KS, CO, A>), grid, dim3(256), 0, st, yw, p.x, p.wc, p.bias, p.y, g0, rot, \
                      p.Cin, p.Cout, p.H, p.W, p.m, nch, units)
-  if (!p.gelu) L_(0);
-  else if (BF) L_(FNO_BF_ACT);
-  else L_(1);
+  if (p.x == nullptr) {  // spectral path only (p.gelu is 0: checked by launch_fno_c2r_pw)
+    hipLaunchKernelGGL((fno_c2r_pw_kernel<BF, KS, CO, 0, false>), grid, dim3(256), 0, st, yw, nullptr, nullptr, p.bias,
+                       p.y, g0, rot, 0, p.Cout, p.H, p.W, p.m, nch, units);
+  } else if (!p.gelu) {
+    L_(0);
+  } else if (BF) {
+    L_(FNO_BF_ACT);
+  } else {
+    L_(1);
+  }
 #undef L_
 }
 
@@ -660,7 +675,8 @@ bool fno_c2r_pw_supported(int cin, int cout, int m, int W, bool bf16) {
 
 void launch_fno_c2r_pw(const FnoC2RPwLaunch& p, void* stream) {
   if (p.B == 0 || p.H == 0) return;
-  if (!fno_c2r_pw_supported(p.Cin, p.Cout, p.m, p.W, p.bf16 != 0))
+  if (p.x == nullptr && p.gelu) throw std::runtime_error("amd_dft: fno_c2r: the spectral-only tail takes no activation");
+  if (!fno_c2r_pw_supported(p.x == nullptr ? 1 : p.Cin, p.Cout, p.m, p.W, p.bf16 != 0))
     throw std::runtime_error("amd_dft: fno_c2r_pw: needs Cin, Cout <= 32, m <= 64, W % 8 == 0, W <= 4096 (bf16)");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (p.bf16) launch_ks<true>(p, st);

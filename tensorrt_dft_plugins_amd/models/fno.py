@@ -14,7 +14,8 @@ kernels per stage, and the full-resolution spectral output is never written to H
      ``csrc/spectral/fno_mix.hip``, plus ``c2c_axis`` where no fixed column kernel covers H);
   3. ``fno_c2r_pw``: the inverse truncated DFT
      along W on MFMA fused with the 1x1 convolution, bias and GELU
-     (``csrc/spectral/fno_c2r_pw.hip``) -- reads x, writes y, nothing else.
+     (``csrc/spectral/fno_c2r_pw.hip``) -- reads x, writes y, nothing else; ``SpectralConv2d`` on its
+     own ends with ``fno_c2r``, the same kernel without the pointwise branch (writes y only).
 
 Backends: ``"torch"`` (torch.fft + einsum + conv2d, the numerics oracle), ``"contrib"`` (the same
 layer written the reference's way: ONNX-contrib ``OnnxRfft2`` / ``OnnxIrfft2`` + real/imaginary
@@ -30,8 +31,6 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import dft as D
-from ..ops import spectral as S
 
 __all__ = ["FNOConfig", "SpectralConv2d", "FNOBlock", "FNO2d", "spectral_conv2d_reference", "spectral_conv2d_contrib"]
 
@@ -106,11 +105,15 @@ class SpectralConv2d(nn.Module):
             return spectral_conv2d_reference(x, self.weight, m1, m2)
         if self.backend == "contrib":
             return spectral_conv2d_contrib(x, self.weight, m1, m2)
-        keep = [(m1, m1), (m2, 0)]
-        xm = D.rfftn_pruned(x, [2, 3], keep)  # [B, Cin, 2*m1, m2, 2] fp32
-        ym = S.fno_spectral_mix(xm.reshape(B, C, 2 * m1 * m2, 2), self._packed_weight())
-        return D.irfftn_pruned(ym.reshape(B, self.out_ch, 2 * m1, m2, 2), [2, 3], [H, W], keep,
-                               out_dtype=x.dtype)
+        # FNOBlock's kernels without the pointwise branch: truncated DFT along W on MFMA, pruned FFT
+        # along H, mixing inside the pruned inverse H transform, inverse truncated DFT along W (fno_c2r:
+        # the layer tail with no x read) -- the full-resolution spectrum never exists
+        ops = torch.ops.amd_dft
+        xw = ops.dftw_r2c(x, m2, 1.0)  # [B, Cin, H, m2, 2]
+        xm = ops.c2c_axis(xw, 2, H, H, 0, m1, m1, False, 1.0)  # [B, Cin, 2*m1, m2, 2]
+        yw = ops.fno_mix_c2c(xm, self._packed_weight(), H, m1, m1, 1.0 / (H * W), 0)  # [B, Cout, H, m2, 2]
+        out_dt = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        return ops.fno_c2r(yw, W, out_dt)
 
     def _packed_weight(self) -> torch.Tensor:
         w = self.weight

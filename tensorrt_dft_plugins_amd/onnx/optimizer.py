@@ -1110,7 +1110,7 @@ def _afno_mlp_ref(X: torch.Tensor, w: List[torch.Tensor], b: List[torch.Tensor],
 def rewrite_fno(ctx: Ctx) -> None:
     """FNO spectral conv: Rfft over the last two dims -> per-mode linear channel mixing on the
     modes [0, m1) u [H - m1, H) x [0, m2) -> Irfft (+ Conv1x1(x) + GELU) -> dftw_r2c + c2c_axis +
-    fno_mix_c2c + fno_c2r_pw (or c2r)."""
+    fno_mix_c2c + fno_c2r_pw (without the pointwise branch: fno_c2r, or c2r for other dtypes)."""
     g = ctx.g
     for rf in [n for n in g.nodes if n.is_("Rfft", CONTRIB_DOMAIN)]:
         if rf not in g.nodes or rf.attrs.get("signal_ndim", 1) != 2:
@@ -1201,6 +1201,8 @@ def rewrite_fno(ctx: Ctx) -> None:
                 bcn = g.add_const("fno_pw_b", g.consts[conv.inputs[2]].float()) if len(conv.inputs) > 2 and \
                     conv.inputs[2] else None
                 new.append(amd_node(g, "fno_c2r_pw", [yw, x, wcn, bcn], [o], gelu=gelu))
+            elif dt in (torch.float32, torch.bfloat16):  # SpectralConv2d alone: the layer tail without x
+                new.append(amd_node(g, "fno_c2r", [yw], [o], W=W, out_dtype=dt))
             else:
                 new.append(amd_node(g, "c2r", [yw], [o], dim=[3], out_size=[W], scale=1.0, keep=[m2, 0], out_dtype=dt))
             g.meta[o] = (g.shape(out), g.dtype(out))

@@ -182,6 +182,55 @@ def test_dftw_r2c_cpu():
     assert rel_l2(torch.view_as_complex(y.contiguous()), ref) < 1e-6
 
 
+def test_fno_c2r_cpu():
+    """fno_c2r: the layer tail without its pointwise branch = irfft along W of the kept modes."""
+    torch.manual_seed(13)
+    B, Co, H, W, m = 2, 3, 4, 16, 6
+    yw = torch.randn(B, Co, H, m, 2)
+    full = torch.zeros(B, Co, H, W // 2 + 1, dtype=torch.complex128)
+    full[..., :m] = torch.view_as_complex(yw.double())
+    ref = torch.fft.irfft(full, n=W, dim=3, norm="forward")
+    y = torch.ops.amd_dft.fno_c2r(yw, W)
+    assert y.dtype == torch.float32 and y.shape == (B, Co, H, W)
+    assert rel_l2(y, ref) < 1e-6
+    yb = torch.ops.amd_dft.fno_c2r(yw, W, torch.bfloat16)
+    assert yb.dtype == torch.bfloat16 and rel_l2(yb.float(), ref) < 1e-2
+    with pytest.raises(RuntimeError):
+        torch.ops.amd_dft.fno_c2r(yw, 8)  # 6 modes need W >= 10
+    assert torch.ops.amd_dft.fno_c2r(yw.to("meta"), W, torch.bfloat16).shape == (B, Co, H, W)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fno_c2r_kernel_gpu(device, dt):
+    """The spectral-only tail kernel (fno_c2r_pw without x / conv / activation) vs the fp64 irfft, at the
+    FNO grid (720 x 1440, 32 modes, 20 channels) and a ragged one (W not a multiple of the chunk)."""
+    torch.manual_seed(14)
+    for B, Co, H, W, m in [(1, 20, 720, 1440, 32), (2, 5, 9, 200, 17)]:
+        yw = torch.randn(B, Co, H, m, 2) / (H * W) ** 0.5
+        ref = torch.ops.amd_dft.fno_c2r(yw, W)
+        y = torch.ops.amd_dft.fno_c2r(yw.to(device), W, dt)
+        assert y.dtype == dt and y.shape == (B, Co, H, W)
+        assert rel_l2(y.float().cpu(), ref) < (2e-5 if dt == torch.float32 else 8e-3), (B, Co, H, W, m)
+
+
+@pytest.mark.gpu
+def test_spectral_conv2d_gpu_full_grid(device):
+    """BASELINE config 3's SpectralConv2d alone (rfft2 -> per-mode complex mixing -> irfft2), 20 ch,
+    720 x 1440, modes 32 x 32, on the amd kernels vs the plain-PyTorch reference (fp32 and bf16)."""
+    torch.manual_seed(15)
+    blk = _block(20, 32, 32).to(device)
+    sp = blk.spectral
+    x = torch.randn(1, 20, 720, 1440, device=device)
+    with torch.no_grad():
+        ref = sp(x)
+        sp.backend = "amd"
+        out = sp(x)
+        outb = sp(x.to(torch.bfloat16))
+    assert out.dtype == torch.float32 and rel_l2(out, ref) < 1e-4
+    assert outb.dtype == torch.bfloat16 and rel_l2(outb.float(), ref) < 2e-2
+
+
 def test_fno_c2r_pw_cpu():
     torch.manual_seed(12)
     B, Ci, Co, H, W, m = 2, 5, 3, 4, 16, 6
