@@ -73,22 +73,23 @@ int main() {
     CK(hipMalloc(&st, slots * 8));
     CK(hipMemset(st, 0, slots * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_fno_stamps), &st, sizeof(st)));
+    for (int pw = 1; pw >= 0; --pw) {  // the FNO layer tail, then the SpectralConv2d tail (fno_c2r: no x)
     FnoC2RPwLaunch p;
     p.yw = yw;
-    p.x = x;
+    p.x = pw ? x : nullptr;
     p.wc = wc;
     p.bias = bias;
     p.y = y;
     p.g0 = g0;
     p.rot = rot;
     p.B = B;
-    p.Cin = C;
+    p.Cin = pw ? C : 0;
     p.Cout = C;
     p.H = H;
     p.W = W;
     p.m = m;
     p.bf16 = bf;
-    p.gelu = 1;
+    p.gelu = pw;
     for (int i = 0; i < 5; ++i) launch_fno_c2r_pw(p, nullptr);
     CK(hipDeviceSynchronize());
     CK(hipMemset(st, 0, slots * 8));
@@ -114,13 +115,15 @@ int main() {
       starts.push_back(r[6]);
     }
     std::sort(starts.begin(), starts.end());
-    std::printf("fno_c2r_pw %s [1,20,720,1440] m32: %.1f us (one call), %zu waves, units/wave median %lld\n",
-                bf ? "bf16" : "fp32", ms * 1000.f, tot.size(), pct(ph[5], 0.5));
+    std::printf("%s %s [1,20,720,1440] m32: %.1f us (one call), %zu waves, units/wave median %lld\n",
+                pw ? "fno_c2r_pw" : "fno_c2r (no x)", bf ? "bf16" : "fp32", ms * 1000.f, tot.size(), pct(ph[5], 0.5));
     const char* names[] = {"setup (tables, weights, zero)", "spectrum reload (row change)", "x staging + rotate/split",
                            "MFMA", "epilogue (act + stores)"};
     for (int i = 0; i < 5; ++i) std::printf("  %-32s median %7lld p90 %7lld\n", names[i], pct(ph[i], 0.5), pct(ph[i], 0.9));
     std::printf("  wave total                       median %7lld p90 %7lld; wave start spread p90 %.2f us\n", pct(tot, 0.5),
                 pct(tot, 0.9), starts.empty() ? 0.0 : (pct(starts, 0.9) - starts[0]) / 100.0);
+    CK(hipMemset(st, 0, slots * 8));
+    }
     CK(hipFree(x));
     CK(hipFree(y));
     CK(hipFree(yw));

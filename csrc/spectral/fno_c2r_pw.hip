@@ -592,6 +592,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, PW 
 }
 
 // workgroups of one kernel instance resident on the current device (occupancy x CUs), cached
+// compute units of the current device, cached
+int64_t device_cus() {
+  static int64_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
 template <bool BF, int KS, int CO, bool PW>
 int64_t resident_wgs() {
   static int64_t cache[64] = {};
@@ -624,10 +637,13 @@ void launch_g(const FnoC2RPwLaunch& p, hipStream_t st) {
     const char* e = tuning_env("MI_DFT_FNO_WGS");
     return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1) << 40;
   }();
-  const int64_t nwg = std::max<int64_t>(
-      std::min<int64_t>(std::min<int64_t>((units + 4 * upw - 1) / (4 * upw),
-                                          p.x ? resident_wgs<BF, KS, CO, true>() : resident_wgs<BF, KS, CO, false>()),
-                        wgs_cap), 1);
+  const int64_t res = p.x ? resident_wgs<BF, KS, CO, true>() : resident_wgs<BF, KS, CO, false>();
+  int64_t nwg = std::max<int64_t>(std::min<int64_t>(std::min<int64_t>((units + 4 * upw - 1) / (4 * upw), res), wgs_cap), 1);
+  // a whole number of workgroups per CU: the grid is one round, so a CU holding one workgroup more than
+  // the others finishes last (fno_c2r at 720 x 1440: 540 -> 512 workgroups, 45.0 -> 42.6 us SpectralConv2d;
+  // profiles/fno_tail_phases_r6.txt)
+  const int64_t cus = device_cus();
+  if (nwg > cus) nwg = nwg / cus * cus;
   const dim3 grid(static_cast<uint32_t>(nwg));
   const float2* yw = static_cast<const float2*>(p.yw);
   const bf16x8* g0 = static_cast<const bf16x8*>(p.g0);
