@@ -11,5 +11,5 @@ spec = importlib.util.spec_from_file_location("benchmain", os.path.join(root, "b
 bm = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(bm)
 bm.tdp.load_plugins()
-knobs = {k: os.environ[k] for k in ("MI_DFT_LIB", "MI_DFT_FNO_UPW", "MI_DFT_FNO_WGS") if k in os.environ}
+knobs = {k: os.environ[k] for k in ("MI_DFT_LIB", "MI_DFT_FNO_UPW", "MI_DFT_FNO_WGS", "MI_DFT_FIXED_CFG") if k in os.environ}
 print(json.dumps({**knobs, **bm.time_fno_block_us()}), flush=True)
