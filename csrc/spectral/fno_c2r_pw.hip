@@ -137,6 +137,12 @@ __device__ __forceinline__ float act(float v) {
 #ifndef FNO_BF_ACT
 #define FNO_BF_ACT 3  // bf16 output's GELU: 3 the fitted erf form (default), 2 the tanh form (A/B build: its cost)
 #endif
+#ifndef FNO_Y_VEC
+#define FNO_Y_VEC 1  // spectrum row: 16-byte loads of 4 modes (0: one 8-byte load per mode)
+#endif
+#ifndef FNO_ROT_TRIM
+#define FNO_ROT_TRIM 1  // setup: load only the rotation-table rows the grid uses (0: the kFnoRotMax bound)
+#endif
 #ifndef FNO_ACT_PACKED
 #define FNO_ACT_PACKED 1  // epilogue GELU on value pairs with packed f32 VALU (csrc/nn/gelu.h); 0: per value
 #endif
@@ -270,12 +276,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, PW 
 #pragma unroll
     for (int ot = 0; ot < CO; ++ot)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k0 = 16 * ks + 4 * lq;
+        if (FNO_Y_VEC && (m & 1) == 0 && k0 + 3 < m) {
+          // 4 consecutive modes as two 16-byte loads; channels >= Cout read channel Cout - 1 (their
+          // MFMA output columns are never stored, and a column only feeds its own outputs)
+          const int o = min(16 * ot + l15, Cout - 1);
+          const float4* src = reinterpret_cast<const float4*>(yw + ((b * Cout + o) * H + h) * m + k0);
+          const float4 v0 = src[0], v1 = src[1];
+          Yv[ot][ks][0] = make_float2(v0.x, v0.y);
+          Yv[ot][ks][1] = make_float2(v0.z, v0.w);
+          Yv[ot][ks][2] = make_float2(v1.x, v1.y);
+          Yv[ot][ks][3] = make_float2(v1.z, v1.w);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int o = 16 * ot + l15, k = 16 * ks + 4 * lq + q;
-          Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
+          for (int q = 0; q < 4; ++q) {
+            const int o = 16 * ot + l15, k = k0 + q;
+            Yv[ot][ks][q] = (o < Cout && k < m) ? yw[((b * Cout + o) * H + h) * m + k] : make_float2(0.f, 0.f);
+          }
         }
+      }
     const int64_t y0 = ((b * Cout * H + h) * W + 4 * lq) * ES;
     ybase = (b * Cout * H + h) * W * ES;
 #pragma unroll
@@ -307,7 +327,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, PW 
   float2 rv[NRT];
   bf16x8 gv[NGT];
 #pragma unroll
-  for (int q = 0; q < NRT; ++q) rv[q] = rot[min(static_cast<int>(threadIdx.x) + 256 * q, nrot - 1)];
+  for (int q = 0; q < NRT; ++q)  // (wave-uniform guard: only the table's ceil(nrot / 256) rows are requested)
+    if (!FNO_ROT_TRIM || 256 * q < nrot) rv[q] = rot[min(static_cast<int>(threadIdx.x) + 256 * q, nrot - 1)];
 #pragma unroll
   for (int q = 0; q < NGT; ++q) {
     const int t = min(static_cast<int>(threadIdx.x) + 256 * q, KS * PT * NG * 64 - 1);
