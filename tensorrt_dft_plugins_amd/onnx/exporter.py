@@ -283,7 +283,9 @@ def export(model: torch.nn.Module, args: Any, f: Optional[str | io.BytesIO] = No
     if not isinstance(args, tuple):
         args = (args,)
     buf = io.BytesIO()
-    with _no_onnxscript_pass(), warnings.catch_warnings():
+    # no_grad: the trace is the same graph (byte-identical export), but autograd no longer keeps every
+    # intermediate for a backward pass -- a batch-32 FourCastNet trace held ~170 GB of activations
+    with _no_onnxscript_pass(), warnings.catch_warnings(), torch.no_grad():
         warnings.simplefilter("ignore")
         torch.onnx.export(
             model, args, buf, dynamo=False, operator_export_type=torch.onnx.OperatorExportTypes.ONNX,
