@@ -198,10 +198,16 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 #ifndef GEMM_HALF_BAL
 #define GEMM_HALF_BAL 0  // 1: measured slower (profiles/gemm_dma_balance_r6.txt)
 #endif
+// GEMM_PRIO: wave priority in the main loop -- 0 (default): s_setprio 1 around every MFMA cluster; 1: one static
+// s_setprio 1 for the younger wave group (waves 4-7, the VALU-arbitration loser; MI355X_MICROARCH.md "Two waves per
+// SIMD" item 4) and no per-cluster flips
+#ifndef GEMM_PRIO
+#define GEMM_PRIO 0
+#endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
                                               Mid&& mid) {
-  __builtin_amdgcn_s_setprio(1);
+  if (GEMM_PRIO == 0) __builtin_amdgcn_s_setprio(1);
   constexpr int NP = SPLIT ? 3 : 2;
 #pragma unroll
   for (int s = 0; s < NP; ++s) {
@@ -220,7 +226,7 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  __builtin_amdgcn_s_setprio(0);
+  if (GEMM_PRIO == 0) __builtin_amdgcn_s_setprio(0);
 }
 
 // vmcnt(2n): the region issued 3 phases ago has landed, n younger regions may still fly
@@ -382,6 +388,7 @@ __global__ void __launch_bounds__(kThreads) gemm_bf16_kernel(GemmLaunch p) {
   // HALF: two-phase K-tile schedule (see the main loop); wave group as a scalar for its branches
   constexpr bool HALF = ((GEMM_HALF >> (SPLIT ? 1 : 0)) & 1) && !PERSIST && MODE != 1;
   const int wrs = __builtin_amdgcn_readfirstlane(wr);
+  if (GEMM_PRIO == 1 && wrs == 1) __builtin_amdgcn_s_setprio(1);  // wave-uniform (readfirstlane): a real branch
   // HALF batch(kt): R0 (each group its own feature rows) + R1 / R2 (all token rows, wave group 1 only).
   // BAL (GEMM_HALF_BAL): wave group 1 issues R2(kt) one section later, in its read-A section of K-tile
   // kt - 1 (ahead of that section's R3), instead of in the read-B section with R0 / R1: its sections
