@@ -263,6 +263,8 @@ at::Tensor fno_c2r_pw_cuda(const at::Tensor& yw_, const at::Tensor& x_, const at
               "fno_c2r_pw: tensor too large");
   at::Tensor x = x_.contiguous();
   at::Tensor yw = yw_.to(at::kFloat).contiguous();
+  // the tail kernel reads 4 modes per 16-byte load: a view at an odd float2 offset gets its own copy
+  if (reinterpret_cast<uintptr_t>(yw.data_ptr()) % 16 != 0) yw = yw.clone();
   at::Tensor wc = wc_.to(at::kFloat).reshape({Cout, Cin}).contiguous();
   at::Tensor bf;
   if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
@@ -330,6 +332,8 @@ at::Tensor fno_c2r_cuda(const at::Tensor& yw_, int64_t W, std::optional<at::Scal
     return c2r.call(yw_.to(at::kFloat).contiguous(), dim, out_size, 1.0, {}, dt);
   }
   at::Tensor yw = yw_.to(at::kFloat).contiguous();
+  // the tail kernel reads 4 modes per 16-byte load: a view at an odd float2 offset gets its own copy
+  if (reinterpret_cast<uintptr_t>(yw.data_ptr()) % 16 != 0) yw = yw.clone();
   at::Tensor y = at::empty({B, Cout, H, W}, yw.options().dtype(dt));
   auto tabs = get_dft_gemm_tables(dt == at::kBFloat16 ? DftTable::C2R_BF16 : DftTable::C2R_F32, static_cast<int>(W),
                                   static_cast<int>(m), yw.device());

@@ -215,6 +215,25 @@ def test_fno_c2r_kernel_gpu(device, dt):
 
 
 @pytest.mark.gpu
+def test_fno_c2r_unaligned_view_gpu(device):
+    """The tail reads 4 modes per 16-byte load: a spectrum view starting 8 bytes into its storage still works."""
+    torch.manual_seed(16)
+    B, Co, H, W, m = 1, 20, 6, 1440, 32
+    flat = torch.randn(B * Co * H * m * 2 + 2, device=device)
+    yw = flat[2:].view(B, Co, H, m, 2)
+    assert yw.data_ptr() % 16 == 8
+    ref = torch.ops.amd_dft.fno_c2r(yw.cpu(), W)
+    for dt in (torch.float32, torch.bfloat16):
+        y = torch.ops.amd_dft.fno_c2r(yw, W, dt)
+        assert rel_l2(y.float().cpu(), ref) < (2e-5 if dt == torch.float32 else 8e-3)
+    x = torch.randn(B, 4, H, W, device=device)
+    wc = torch.randn(Co, 4, device=device)
+    y = torch.ops.amd_dft.fno_c2r_pw(yw, x, wc, None, False)
+    refp = torch.ops.amd_dft.fno_c2r_pw(yw.cpu(), x.cpu(), wc.cpu(), None, False)
+    assert rel_l2(y.cpu(), refp) < 2e-5
+
+
+@pytest.mark.gpu
 def test_spectral_conv2d_gpu_full_grid(device):
     """BASELINE config 3's SpectralConv2d alone (rfft2 -> per-mode complex mixing -> irfft2), 20 ch,
     720 x 1440, modes 32 x 32, on the amd kernels vs the plain-PyTorch reference (fp32 and bf16)."""
