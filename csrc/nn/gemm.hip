@@ -198,11 +198,13 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* stage, int wc
 #ifndef GEMM_HALF_BAL
 #define GEMM_HALF_BAL 0  // 1: measured slower (profiles/gemm_dma_balance_r6.txt)
 #endif
-// GEMM_PRIO: wave priority in the main loop -- 0 (default): s_setprio 1 around every MFMA cluster; 1: one static
-// s_setprio 1 for the younger wave group (waves 4-7, the VALU-arbitration loser; MI355X_MICROARCH.md "Two waves per
-// SIMD" item 4) and no per-cluster flips
+// GEMM_PRIO: wave priority in the main loop -- 2 (default): none (both waves of a SIMD at priority 0; the clusters
+// stay between their barriers through barrier()'s sched_barrier fences); 0: s_setprio 1 around every MFMA cluster (the
+// round 2-5 form); 1: one static s_setprio 1 for the younger wave group (waves 4-7, the VALU-arbitration loser;
+// MI355X_MICROARCH.md "Two waves per SIMD" item 4).  profiles/gemm_prio_r6.txt: the x3 GEMMs 0.5-1.5 % faster without
+// priorities, the fp32 step +0.25 % over six paired runs.
 #ifndef GEMM_PRIO
-#define GEMM_PRIO 0
+#define GEMM_PRIO 2
 #endif
 template <int MI, int NI, bool SPLIT, class Mid>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[8][4], const bf16x8 (&a)[8], const bf16x8 (&b)[4],
